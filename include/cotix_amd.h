@@ -1,0 +1,141 @@
+/* cotix_amd.h -- C-ABI of the MI355X-native cotix hot path (libcotix_amd.so).
+ *
+ * Drop-in boundary for the per-step physics of cotix (DelftMercurians/
+ * Parallax).  Plain pointers and sizes only; every float/uint32 pointer
+ * argument named "device" is HIP device memory owned by the caller; the
+ * library allocates only scene workspace at cotix_scene_create and nothing
+ * per step.  Calls are stream-ordered on the given hipStream_t (pass NULL for
+ * the default stream); a scene handle is not re-entrant across streams.
+ *
+ * Return codes: 0 = ok, <0 = error (message in cotix_last_error()).
+ *
+ * Reference interfaces replaced (file:line in the reference repository):
+ *   cotix_step            examples/test_viz.py:24-44 (LunarLander f) and :61-69
+ *                         (RoboCup f): Euler -> [gravity] -> collider ->
+ *                         [LunarLander.step] -> key = split(key)[0], n_steps times
+ *   cotix_physics_euler   ExplicitEulerPhysics.step   cotix/_physics_solvers.py:16-33
+ *   cotix_collider_resolve RandomizedCollider.resolve cotix/_colliders.py:74-351
+ *   cotix_lunar_constraints LunarLander.step          cotix/_lunar_lander.py:145-218
+ *   cotix_contacts        _contact_funcs[(Ta,Tb)](a,b) cotix/_colliders.py:21-35,
+ *                         cotix/_contacts.py:30-315
+ *   cotix_resolve         resolve_collision            cotix/_collision_resolution.py:52-151
+ *   cotix_threefry2x32 / cotix_random_split / cotix_random_uniform
+ *                         jax.random primitives called at cotix/_colliders.py:142-295
+ *   cotix_order_clockwise order_clockwise              cotix/_geometry_utils.py:60-67
+ */
+#ifndef COTIX_AMD_H
+#define COTIX_AMD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cotix_scene cotix_scene;
+typedef struct ihipStream_t* cotix_stream_t; /* == hipStream_t */
+
+/* shape registry type ids (exact Python types of cotix/_convex_shapes.py) */
+enum {
+  COTIX_CIRCLE = 0,
+  COTIX_AABB = 1,
+  COTIX_POLYGON = 2,
+  COTIX_POLYGON3 = 3,
+  COTIX_POLYGON4 = 4,
+  COTIX_POLYGON5 = 5,
+  COTIX_POLYGON6 = 6
+};
+
+/* contact function ids (values of the _contact_funcs registry) */
+enum {
+  COTIX_FN_AABB_AABB = 0,
+  COTIX_FN_CIRCLE_CIRCLE = 1,
+  COTIX_FN_CIRCLE_AABB = 2,
+  COTIX_FN_POLY_POLY = 3,
+  COTIX_FN_AABB_POLY = 4,
+  COTIX_FN_CIRCLE_POLY = 5
+};
+
+/* cotix_step stage bits */
+enum {
+  COTIX_STAGE_EULER = 1,        /* ExplicitEulerPhysics.step                  */
+  COTIX_STAGE_GRAVITY = 2,      /* body 0 velocity += (0, -0.002)  (LL driver) */
+  COTIX_STAGE_COLLIDER = 4,     /* RandomizedCollider.resolve(bodies, key)    */
+  COTIX_STAGE_LUNAR = 8,        /* LunarLander.step joint constraints          */
+  COTIX_STAGE_ADVANCE_KEY = 16, /* key = split(key)[0]                        */
+  COTIX_STAGES_ROBOCUP = 1 | 4 | 16,
+  COTIX_STAGES_LUNAR = 1 | 2 | 4 | 8 | 16
+};
+
+/* per-env error bits (eqx.error_if sites on the path) */
+enum {
+  COTIX_ERR_CIRCLE_AABB_CCP = 1 /* cotix/_contacts.py:105-107 */
+};
+
+/* Compile a scene (the collider's trace-time enumeration, cotix/_colliders.py:86-131).
+ *   body_params [n_bodies][4] host: mass, inertia, elasticity, friction_coefficient
+ *   part_body   [n_parts]  host: owning body (parts grouped by body, in shape order)
+ *   part_type   [n_parts]  host: COTIX_CIRCLE .. COTIX_POLYGON6
+ *   part_nverts [n_parts]  host: vertex count for polygons (ignored otherwise)
+ * Illegal type pairs are rejected here (the reference raises RuntimeError
+ * at trace time, cotix/_colliders.py:103-107). */
+int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                       const int* part_type, const int* part_nverts, cotix_scene** out);
+int cotix_scene_destroy(cotix_scene* scene);
+/* floats of local part geometry the scene expects per env (circle: r,cx,cy,0;
+ * AABB: lo.x,lo.y,up.x,up.y; polygon: x,y per vertex), parts in order. */
+int cotix_scene_geom_floats(const cotix_scene* scene);
+/* introspection for tests: counts of distinct contacts / cells / candidates / type keys */
+int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, int* n_candidates, int* n_types);
+
+/* Fused step, n_steps times, in place.
+ *   dyn   device f32 [n_bodies][6][B]  (px, py, vx, vy, angle, angular_velocity)
+ *   keys  device u32 [B][2]            collider key per env (advanced when
+ *                                      COTIX_STAGE_ADVANCE_KEY is set)
+ *   err   device u32 [B]               OR-ed error bits (caller zeroes)
+ *   geom  device f32 [geom_floats] (geom_stride == 0, shared by all envs) or
+ *                    [B][geom_stride] (per-env geometry, geom_stride >= geom_floats)
+ *   action nullable device f32 [n_steps][B][2]: added to the velocity of body
+ *          action_body after the Euler stage (differentiable-config hook). */
+int cotix_step(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
+               int geom_stride, int B, int n_steps, float dt, int stages, const float* action,
+               int action_body, cotix_stream_t stream);
+
+/* cotix_step with episode restarts: after every env-step, an env whose error
+ * bits are set (the reference raises XlaRuntimeError there) is restored from
+ *   dyn_reset device f32 [n_bodies][6][B]; its err word is cleared and
+ *   resets[env] (device u32 [B], nullable) is incremented.  The key chain
+ * continues.  Used by the benchmark to keep a sustained batch. */
+int cotix_step_autoreset(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
+                         int geom_stride, int B, int n_steps, float dt, int stages, const float* dyn_reset,
+                         uint32_t* resets, cotix_stream_t stream);
+
+/* Operator-level entry points (batched over n independent items). */
+int cotix_physics_euler(float* dyn, int n_bodies, int B, float dt, cotix_stream_t stream);
+int cotix_collider_resolve(cotix_scene* scene, float* dyn, const uint32_t* keys, uint32_t* err,
+                           const float* geom, int geom_stride, int B, cotix_stream_t stream);
+int cotix_lunar_constraints(float* dyn, int B, cotix_stream_t stream);
+/* shapes a, b: device f32 [n][18] = (kind, nverts, d[16]); out device f32
+ * [n][4] = (pen.x, pen.y, cp.x, cp.y); err device u32 [n] (may be NULL). */
+int cotix_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err,
+                   cotix_stream_t stream);
+/* dyn1/dyn2 device f32 [n][6] updated in place; par1/par2 [n][4]; contact [n][4] */
+int cotix_resolve(int n, float* dyn1, const float* par1, float* dyn2, const float* par2,
+                  const float* contact, cotix_stream_t stream);
+/* threefry2x32-20 block: out[i] = threefry(keys[i], ctr[i]) (all device u32 [n][2]) */
+int cotix_threefry2x32(const uint32_t* keys, const uint32_t* ctr, uint32_t* out, int n,
+                       cotix_stream_t stream);
+/* out [n][num][2] = jax.random.split(keys[i], num) */
+int cotix_random_split(const uint32_t* keys, int n, int num, uint32_t* out, cotix_stream_t stream);
+/* out [n][count] = jax.random.uniform(keys[i], (count,), lo, hi) (f32) */
+int cotix_random_uniform(const uint32_t* keys, int n, int count, float lo, float hi, float* out,
+                         cotix_stream_t stream);
+/* polygons xy device f32 [n][nverts][2] sorted in place (order_clockwise) */
+int cotix_order_clockwise(float* xy, int n, int nverts, cotix_stream_t stream);
+
+const char* cotix_last_error(void);
+const char* cotix_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COTIX_AMD_H */

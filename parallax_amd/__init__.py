@@ -1,0 +1,16 @@
+"""parallax_amd -- MI355X-native batched 2-D rigid-body stepper for cotix
+(DelftMercurians/Parallax).  The hot path is HIP for gfx950 in
+libcotix_amd.so (include/cotix_amd.h); this package is the Python host side
+mirroring the reference's body/shape/operator surface.
+"""
+from . import _ffi  # noqa: F401  (raises ImportError when the HIP library is missing)
+from . import random  # noqa: F401
+from .bodies import AnyBody, BodyView  # noqa: F401
+from .env import BatchedEnv  # noqa: F401
+from .physics import (ContactInfo, ExplicitEulerPhysics, RandomizedCollider, SimpleConstraintSolver,  # noqa: F401
+                      contact_funcs, resolve_collision, run_contacts)
+from .scenarios import LunarLander, RoboCupEnv  # noqa: F401
+from .shapes import AABB, Circle, Polygon, Polygon3, Polygon4, Polygon5, Polygon6, UniversalShape  # noqa: F401
+from .world import Scene, World  # noqa: F401
+
+__version__ = "0.1.0"

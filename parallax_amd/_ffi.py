@@ -1,0 +1,78 @@
+"""ctypes binding of libcotix_amd.so (include/cotix_amd.h).
+
+The product path has no fallback: if the HIP library is missing this module
+raises ImportError, and every op raises RuntimeError on a non-zero return.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("COTIX_AMD_LIB", os.path.join(_HERE, "_lib", "libcotix_amd.so"))
+
+# enums mirrored from include/cotix_amd.h
+CIRCLE, AABB, POLYGON, POLYGON3, POLYGON4, POLYGON5, POLYGON6 = range(7)
+FN_AABB_AABB, FN_CIRCLE_CIRCLE, FN_CIRCLE_AABB, FN_POLY_POLY, FN_AABB_POLY, FN_CIRCLE_POLY = range(6)
+STAGE_EULER, STAGE_GRAVITY, STAGE_COLLIDER, STAGE_LUNAR, STAGE_ADVANCE_KEY = 1, 2, 4, 8, 16
+STAGES_ROBOCUP = STAGE_EULER | STAGE_COLLIDER | STAGE_ADVANCE_KEY
+STAGES_LUNAR = STAGE_EULER | STAGE_GRAVITY | STAGE_COLLIDER | STAGE_LUNAR | STAGE_ADVANCE_KEY
+ERR_CIRCLE_AABB_CCP = 1
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+SIGNATURES = {
+    "cotix_scene_create": (_I, [_I, _P, _I, _P, _P, _P, ctypes.POINTER(_P)]),
+    "cotix_scene_destroy": (_I, [_P]),
+    "cotix_scene_geom_floats": (_I, [_P]),
+    "cotix_scene_info": (_I, [_P, _P, _P, _P, _P]),
+    "cotix_step": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P]),
+    "cotix_step_autoreset": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
+    "cotix_physics_euler": (_I, [_P, _I, _I, _F, _P]),
+    "cotix_collider_resolve": (_I, [_P, _P, _P, _P, _P, _I, _I, _P]),
+    "cotix_lunar_constraints": (_I, [_P, _I, _P]),
+    "cotix_contacts": (_I, [_I, _I, _P, _P, _P, _P, _P]),
+    "cotix_resolve": (_I, [_I, _P, _P, _P, _P, _P, _P]),
+    "cotix_threefry2x32": (_I, [_P, _P, _P, _I, _P]),
+    "cotix_random_split": (_I, [_P, _I, _I, _P, _P]),
+    "cotix_random_uniform": (_I, [_P, _I, _I, _F, _F, _P, _P]),
+    "cotix_order_clockwise": (_I, [_P, _I, _I, _P]),
+    "cotix_last_error": (ctypes.c_char_p, []),
+    "cotix_version": (ctypes.c_char_p, []),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libcotix_amd.so not found at %s -- build it with `python __graft_entry__.py` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc, what=""):
+    if rc != 0:
+        raise RuntimeError("%s failed: %s" % (what, lib.cotix_last_error().decode()))
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a contiguous torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,745 @@
+// Device-side building blocks of the cotix hot path for gfx950 (CDNA4).
+//
+// Every function here restates one reference function; the cited file:line
+// is in /root/reference (DelftMercurians/Parallax, package `cotix`).  Numeric
+// contract (shared with the oracle, DESIGN.md "Numerics"): IEEE f32, one
+// rounding per operation, NO fma contraction (built with -ffp-contract=off),
+// the reference expression's evaluation order, NaN-propagating min/max/clip,
+// argmin/argmax = first NaN else first extremum, and deterministic f32
+// sin/cos/atan2 kernels (cephes polynomials) so results are bit-identical
+// to the CPU oracle.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIP__) || defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define CX_DEV __device__ __forceinline__
+#define CX_MF __device__ __forceinline__  // member functions
+#else
+// host build of the same code: used ONLY by the CPU emulation harness of the
+// test suite (tests/emu/), to run the kernel logic under AddressSanitizer.
+#define CX_DEV static inline
+#define CX_MF inline
+static inline float __uint_as_float(uint32_t u) {
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+#endif
+
+namespace cx {
+
+// ---------------------------------------------------------------------------
+// float helpers
+// ---------------------------------------------------------------------------
+CX_DEV bool isn(float x) { return x != x; }
+CX_DEV float qnan() { return __builtin_nanf(""); }
+CX_DEV float finf() { return __builtin_inff(); }
+
+// lax.max / lax.min: NaN-propagating, ties keep the first operand.
+CX_DEV float fmax_(float a, float b) { return isn(a) ? a : (isn(b) ? b : (a >= b ? a : b)); }
+CX_DEV float fmin_(float a, float b) { return isn(a) ? a : (isn(b) ? b : (a <= b ? a : b)); }
+// jnp.clip (jax 0.4.x): minimum(hi, maximum(lo, x))
+CX_DEV float clip_(float x, float lo, float hi) { return fmin_(hi, fmax_(lo, x)); }
+
+struct v2 {
+  float x, y;
+};
+CX_DEV v2 mk(float x, float y) { return v2{x, y}; }
+CX_DEV v2 add(v2 a, v2 b) { return v2{a.x + b.x, a.y + b.y}; }
+CX_DEV v2 sub(v2 a, v2 b) { return v2{a.x - b.x, a.y - b.y}; }
+CX_DEV v2 neg(v2 a) { return v2{-a.x, -a.y}; }
+CX_DEV v2 scl(v2 a, float s) { return v2{a.x * s, a.y * s}; }
+CX_DEV v2 divs(v2 a, float s) { return v2{a.x / s, a.y / s}; }
+CX_DEV float dot(v2 a, v2 b) { return a.x * b.x + a.y * b.y; }
+CX_DEV float crs(v2 a, v2 b) { return a.x * b.y - a.y * b.x; }  // jnp.cross (2-D)
+CX_DEV float sumsq(v2 a) { return a.x * a.x + a.y * a.y; }
+CX_DEV float nrm(v2 a) { return __builtin_sqrtf(sumsq(a)); }
+CX_DEV bool vnan(v2 a) { return isn(a.x) || isn(a.y); }
+CX_DEV v2 fnormal(v2 a) { return v2{-a.y, a.x}; }  // fast_normal, _geometry_utils.py:30-34
+
+// ---------------------------------------------------------------------------
+// deterministic f32 transcendentals (the build's fixed choice; see oracle)
+// ---------------------------------------------------------------------------
+CX_DEV float sin_poly(float r) {
+  float z = r * r;
+  return (((-1.9515295891e-4f * z + 8.3321608736e-3f) * z + -1.6666654611e-1f) * z) * r + r;
+}
+CX_DEV float cos_poly(float r) {
+  float z = r * r;
+  return ((((2.443315711809948e-5f * z + -1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z) * z -
+          0.5f * z) +
+         1.0f;
+}
+CX_DEV void sincos32(float x, float* s_out, float* c_out) {
+  if (isn(x) || __builtin_isinf(x)) {
+    *s_out = qnan();
+    *c_out = qnan();
+    return;
+  }
+  float t = x * 0.636619772367581343f;
+  float k = (t + 12582912.0f) - 12582912.0f;
+  float r = ((x - k * 1.5703125f) - k * 4.837512969970703125e-4f) - k * 7.54978995489188216e-8f;
+  float s = sin_poly(r), c = cos_poly(r);
+  int q = ((int)k) & 3;
+  if (q == 0) { *s_out = s; *c_out = c; }
+  else if (q == 1) { *s_out = c; *c_out = -s; }
+  else if (q == 2) { *s_out = -s; *c_out = -c; }
+  else { *s_out = -c; *c_out = s; }
+}
+CX_DEV float atan01(float t) {
+  float y0 = 0.0f;
+  if (t > 0.4142135623730950f) {
+    y0 = 0.785398163397448309616f;
+    t = (t - 1.0f) / (t + 1.0f);
+  }
+  float z = t * t;
+  float p = ((((8.05374449538e-2f * z + -1.38776856032e-1f) * z + 1.99777106478e-1f) * z + -3.33329491539e-1f) * z) * t + t;
+  return y0 + p;
+}
+CX_DEV float atan2_32(float y, float x) {
+  const float PI = 3.14159265358979323846f, PIO2 = 1.57079632679489661923f;
+  if (isn(x) || isn(y)) return qnan();
+  if (y == 0.0f) {
+    if (x > 0.0f || (x == 0.0f && !__builtin_signbit(x))) return y;
+    return __builtin_signbit(y) ? -PI : PI;
+  }
+  if (x == 0.0f) return y < 0.0f ? -PIO2 : PIO2;
+  float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
+  float r = (ay <= ax) ? atan01(ay / ax) : (PIO2 - atan01(ax / ay));
+  if (x < 0.0f) r = PI - r;
+  return y < 0.0f ? -r : r;
+}
+// lax.sort order key: -0 == +0, NaN after everything (all NaN equal).
+CX_DEV bool sort_lt(float a, float b) {
+  if (isn(a)) return false;
+  if (isn(b)) return true;
+  return a < b;
+}
+
+// ---------------------------------------------------------------------------
+// threefry2x32-20 and the jax.random legacy layouts (jax/_src/prng.py)
+// ---------------------------------------------------------------------------
+struct key2 {
+  uint32_t a, b;
+};
+CX_DEV uint32_t rotl(uint32_t v, uint32_t r) { return (v << r) | (v >> (32u - r)); }
+#define CX_RND(r) \
+  x0 += x1;       \
+  x1 = rotl(x1, r); \
+  x1 ^= x0;
+CX_DEV key2 threefry(key2 k, uint32_t x0, uint32_t x1) {
+  const uint32_t k0 = k.a, k1 = k.b, k2 = k.a ^ k.b ^ 0x1BD11BDAu;
+  x0 += k0;
+  x1 += k1;
+  CX_RND(13) CX_RND(15) CX_RND(26) CX_RND(6)
+  x0 += k1; x1 += k2 + 1u;
+  CX_RND(17) CX_RND(29) CX_RND(16) CX_RND(24)
+  x0 += k2; x1 += k0 + 2u;
+  CX_RND(13) CX_RND(15) CX_RND(26) CX_RND(6)
+  x0 += k0; x1 += k1 + 3u;
+  CX_RND(17) CX_RND(29) CX_RND(16) CX_RND(24)
+  x0 += k1; x1 += k2 + 4u;
+  CX_RND(13) CX_RND(15) CX_RND(26) CX_RND(6)
+  x0 += k2; x1 += k0 + 5u;
+  return key2{x0, x1};
+}
+#undef CX_RND
+// word m of the flat output of split(key, num) (counters iota(2*num)).
+CX_DEV uint32_t split_word(key2 k, uint32_t num, uint32_t m) {
+  if (m < num) return threefry(k, m, num + m).a;
+  return threefry(k, m - num, m).b;
+}
+// split(key, num)[idx]: two threefry blocks (one when num == 1).
+CX_DEV key2 split_at(key2 k, uint32_t num, uint32_t idx) {
+  if (num == 1u) return threefry(k, 0u, 1u);
+  return key2{split_word(k, num, 2u * idx), split_word(k, num, 2u * idx + 1u)};
+}
+// the single 32-bit word of random_bits(key, ()) (odd count -> zero pad).
+CX_DEV uint32_t bits1(key2 k) { return threefry(k, 0u, 0u).a; }
+CX_DEV float unit_float(uint32_t bits) { return __uint_as_float((bits >> 9) | 0x3F800000u) - 1.0f; }
+// jax.random.uniform(key, (), lo, hi): max(lo, f*(hi-lo)+lo)
+CX_DEV float uniform1(key2 k, float lo, float hi) { return fmax_(lo, unit_float(bits1(k)) * (hi - lo) + lo); }
+// jax.random.bernoulli(key, 0.5, ()): top bit of the word is 0.
+CX_DEV bool bernoulli_half(key2 k) { return (bits1(k) >> 31) == 0u; }
+
+// jnp.cumsum via lax.associative_scan (CPU lowering), n <= 16.
+CX_DEV void cumsum_assoc(const float* in, int n, float* out) {
+  float lv[5][16];
+  int ln[5];
+  int L = 0;
+  for (int k = 0; k < n; ++k) lv[0][k] = in[k];
+  ln[0] = n;
+  while (ln[L] >= 2 && L < 4) {
+    int m = ln[L] / 2;
+    for (int k = 0; k < m; ++k) lv[L + 1][k] = lv[L][2 * k] + lv[L][2 * k + 1];
+    ln[L + 1] = m;
+    ++L;
+  }
+  // lv[L] is its own scan (length < 2); walk back down.
+  float res[16];
+  for (int k = 0; k < ln[L]; ++k) res[k] = lv[L][k];
+  for (int l = L - 1; l >= 0; --l) {
+    int nl = ln[l], no = ln[l + 1];
+    float odd[16], even[16], outl[16];
+    for (int k = 0; k < no; ++k) odd[k] = res[k];
+    int ne_tail = (nl % 2 == 0) ? no - 1 : no;
+    even[0] = lv[l][0];
+    for (int k = 0; k < ne_tail; ++k) even[k + 1] = odd[k] + lv[l][2 * k + 2];
+    for (int k = 0; k < nl; ++k) outl[k] = (k % 2 == 0) ? even[k / 2] : odd[k / 2];
+    for (int k = 0; k < nl; ++k) res[k] = outl[k];
+  }
+  for (int k = 0; k < n; ++k) out[k] = res[k];
+}
+
+// ---------------------------------------------------------------------------
+// shapes (cotix/_convex_shapes.py); world-frame geometry in 16 floats
+// ---------------------------------------------------------------------------
+enum : int { KIND_CIRCLE = 0, KIND_AABB = 1, KIND_POLY = 2 };
+constexpr int MAXV = 8;
+struct Shape {
+  int kind, n;
+  float d[2 * MAXV];  // circle: r,cx,cy; aabb: lo.x,lo.y,up.x,up.y; poly: xy*n
+};
+CX_DEV v2 vert(const Shape& s, int k) { return v2{s.d[2 * k], s.d[2 * k + 1]}; }
+
+CX_DEV int argmax_first(const float* v, int n) {
+  for (int k = 0; k < n; ++k)
+    if (isn(v[k])) return k;
+  int b = 0;
+  for (int k = 1; k < n; ++k)
+    if (v[k] > v[b]) b = k;
+  return b;
+}
+CX_DEV int argmin_first(const float* v, int n) {
+  for (int k = 0; k < n; ++k)
+    if (isn(v[k])) return k;
+  int b = 0;
+  for (int k = 1; k < n; ++k)
+    if (v[k] < v[b]) b = k;
+  return b;
+}
+
+// get_support: Circle :22-26, AABB :62-66, Polygon :149-155
+CX_DEV v2 support(const Shape& s, v2 d) {
+  if (s.kind == KIND_CIRCLE) {
+    float n = nrm(d);
+    v2 nd = v2{d.x / n, d.y / n};
+    return v2{nd.x * s.d[0] + s.d[1], nd.y * s.d[0] + s.d[2]};
+  }
+  if (s.kind == KIND_AABB) {
+    return v2{d.x >= 0.0f ? s.d[2] : s.d[0], d.y >= 0.0f ? s.d[3] : s.d[1]};
+  }
+  if (vnan(d)) return v2{qnan(), qnan()};
+  // argmax(v . d), first NaN else first max
+  int best = -1;
+  float bv = 0.0f;
+  for (int k = 0; k < s.n; ++k) {
+    float t = s.d[2 * k] * d.x + s.d[2 * k + 1] * d.y;
+    if (best < 0 || (!isn(bv) && (isn(t) || t > bv))) {
+      best = k;
+      bv = t;
+    }
+  }
+  return vert(s, best);
+}
+CX_DEV v2 minkowski(const Shape& a, const Shape& b, v2 d) { return sub(support(a, d), support(b, neg(d))); }
+
+CX_DEV bool circle_contains(const Shape& c, v2 p) {  // :28-29
+  float r = c.d[0] + 1e-6f;
+  return sumsq(sub(p, v2{c.d[1], c.d[2]})) <= r * r;
+}
+CX_DEV bool aabb_contains(const Shape& a, v2 p) {  // :105-106
+  return (p.x >= a.d[0] - 1e-6f) && (p.y >= a.d[1] - 1e-6f) && (p.x <= a.d[2] + 1e-6f) && (p.y <= a.d[3] + 1e-6f);
+}
+CX_DEV float fsign(float x) { return isn(x) ? x : (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x)); }
+CX_DEV bool poly_contains(const Shape& s, v2 p) {  // :168-175, edge k = (v_k, v_{k-1})
+  float s0 = 0.0f;
+  bool ok = true;
+  for (int k = 0; k < s.n; ++k) {
+    v2 e0 = vert(s, k), e1 = vert(s, k == 0 ? s.n - 1 : k - 1);
+    float sg = fsign(dot(sub(p, e0), fnormal(sub(e0, e1))));
+    if (k == 0) s0 = sg;
+    else ok = ok && (sg == s0);
+  }
+  return ok && !isn(s0);
+}
+// AABB vertices/edges as a 4-gon: [up, (up.x,lo.y), lo, (lo.x,up.y)] :82-103
+CX_DEV void aabb_verts(const Shape& a, v2* vs) {
+  vs[0] = v2{a.d[2], a.d[3]};
+  vs[1] = v2{a.d[2], a.d[1]};
+  vs[2] = v2{a.d[0], a.d[1]};
+  vs[3] = v2{a.d[0], a.d[3]};
+}
+
+// order_clockwise (cotix/_geometry_utils.py:60-67): sequential mean, atan2,
+// stable sort (insertion sort is stable).
+CX_DEV void order_clockwise(float* xy, int n) {
+  float sx = 0.0f, sy = 0.0f;
+  for (int k = 0; k < n; ++k) {
+    sx = sx + xy[2 * k];
+    sy = sy + xy[2 * k + 1];
+  }
+  float fn = (float)n;
+  float mx = sx / fn, my = sy / fn;
+  float ang[MAXV], px[MAXV], py[MAXV];
+  for (int k = 0; k < n; ++k) {
+    px[k] = xy[2 * k];
+    py[k] = xy[2 * k + 1];
+    ang[k] = atan2_32(py[k] - my, px[k] - mx);
+  }
+  for (int k = 1; k < n; ++k) {
+    float a = ang[k], x = px[k], y = py[k];
+    int j = k - 1;
+    while (j >= 0 && sort_lt(a, ang[j])) {
+      ang[j + 1] = ang[j];
+      px[j + 1] = px[j];
+      py[j + 1] = py[j];
+      --j;
+    }
+    ang[j + 1] = a;
+    px[j + 1] = x;
+    py[j + 1] = y;
+  }
+  for (int k = 0; k < n; ++k) {
+    xy[2 * k] = px[k];
+    xy[2 * k + 1] = py[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// contacts (cotix/_contacts.py); ContactInfo = (pen, cp), NaN cp = none
+// ---------------------------------------------------------------------------
+struct Contact {
+  v2 pen, cp;
+};
+CX_DEV Contact nan_contact() { return Contact{v2{0.0f, 0.0f}, v2{qnan(), qnan()}}; }
+
+CX_DEV Contact aabb_vs_aabb(const Shape& a, const Shape& b) {  // :61-96
+  const float alx = a.d[0], aly = a.d[1], aux = a.d[2], auy = a.d[3];
+  const float blx = b.d[0], bly = b.d[1], bux = b.d[2], buy = b.d[3];
+  bool below = auy <= bly, above = aly >= buy, left = aux <= blx, right = alx >= bux;
+  if (below || left || above || right) return nan_contact();
+  const float me = -1e-8f;
+  float dep[4] = {fmax_(auy - bly, me), fmax_(buy - aly, me), fmax_(aux - blx, me), fmax_(bux - alx, me)};
+  const float dx[4] = {0.0f, 0.0f, -1.0f, 1.0f}, dy[4] = {-1.0f, 1.0f, 0.0f, 0.0f};
+  int k = argmin_first(dep, 4);
+  float md = fmax_(0.0f, dep[k]);
+  Contact c;
+  c.pen = v2{md * dx[k], md * dy[k]};
+  v2 mu = v2{fmin_(aux, bux), fmin_(auy, buy)}, ml = v2{fmax_(alx, blx), fmax_(aly, bly)};
+  c.cp = divs(add(mu, ml), 2.0f);
+  return c;
+}
+
+CX_DEV Contact circle_vs_circle(const Shape& a, const Shape& b) {  // :30-58
+  v2 ap = v2{a.d[1], a.d[2]}, bp = v2{b.d[1], b.d[2]};
+  float ar = a.d[0], br = b.d[0];
+  v2 delta = sub(ap, bp);
+  float dist = nrm(delta);
+  v2 dir = (dist == 0.0f) ? v2{1.0f, 0.0f} : divs(delta, dist);
+  v2 pen = scl(dir, fmin_(dist - (ar + br), 0.0f));
+  v2 cp = divs(add(add(bp, scl(dir, br - ar)), ap), 2.0f);
+  if (!(dot(sub(ap, cp), sub(bp, cp)) <= 0.0f)) cp = circle_contains(a, bp) ? bp : ap;
+  if (dist <= ar + br) return Contact{neg(pen), cp};
+  return nan_contact();
+}
+
+// circle_vs_aabb :99-154.  *err |= 1 when eqx.error_if trips (ccp not in the
+// AABB); the guarded ccp then becomes NaN (EQX_ON_ERROR=nan semantics).
+CX_DEV Contact circle_vs_aabb(const Shape& a, const Shape& b, uint32_t* err) {
+  v2 ap = v2{a.d[1], a.d[2]};
+  float r = a.d[0];
+  v2 lo = v2{b.d[0], b.d[1]}, up = v2{b.d[2], b.d[3]};
+  v2 bc = v2{(lo.x + up.x) / 2.0f, (lo.y + up.y) / 2.0f};
+  v2 disp = sub(ap, bc);
+  v2 l = sub(lo, bc), h = sub(up, bc);
+  v2 ccp = add(bc, v2{clip_(disp.x, l.x, h.x), clip_(disp.y, l.y, h.y)});
+  if (!aabb_contains(b, ccp)) {
+    *err |= 1u;
+    ccp = v2{qnan(), qnan()};
+  }
+  v2 vs[4] = {lo, v2{lo.x, up.y}, up, v2{up.x, lo.y}};
+  bool perfect = false;
+  for (int k = 0; k < 4; ++k) perfect = perfect || (nrm(sub(vs[k], ccp)) < 1e-6f);
+  if (!circle_contains(a, ccp)) return nan_contact();
+  if (perfect) {
+    v2 d = sub(ccp, ap);
+    v2 dn = divs(d, nrm(d));
+    return Contact{neg(sub(add(ap, scl(dn, r)), ccp)), ccp};
+  }
+  float sh[4] = {(ap.y + r) - lo.y, up.y - (ap.y - r), (ap.x + r) - lo.x, up.x - (ap.x - r)};
+  const float dx[4] = {0.0f, 0.0f, 1.0f, -1.0f}, dy[4] = {1.0f, -1.0f, 0.0f, 0.0f};
+  int k = argmin_first(sh, 4);
+  float ns = -sh[k];
+  return Contact{v2{ns * dx[k], ns * dy[k]}, ccp};
+}
+
+// ---------------------------------------------------------------------------
+// GJK (cotix/_collisions.py:20-112, 277-310)
+// ---------------------------------------------------------------------------
+CX_DEV bool point_in_triangle0(v2 v1, v2 v2_, v2 v3) {  // _geometry_utils.py:12-27, pt = 0
+  v2 pt = v2{0.0f, 0.0f};
+  auto sgn = [](v2 p1, v2 p2, v2 p3) { return (p1.x - p3.x) * (p2.y - p3.y) - (p2.x - p3.x) * (p1.y - p3.y); };
+  float d1 = sgn(pt, v1, v2_), d2 = sgn(pt, v2_, v3), d3 = sgn(pt, v3, v1);
+  bool has_neg = (d1 < 0.0f) || (d2 < 0.0f) || (d3 < 0.0f);
+  bool has_pos = (d1 > 0.0f) || (d2 > 0.0f) || (d3 > 0.0f);
+  return !(has_neg && has_pos);
+}
+
+CX_DEV bool gjk(const Shape& a, const Shape& b, v2 d0, v2* simplex) {
+  v2 s0 = minkowski(a, b, d0);
+  v2 s1 = minkowski(a, b, neg(s0));
+  v2 dir = fnormal(sub(s1, s0));
+  if (dot(dir, neg(s1)) > 0.0f) {
+    v2 t = s0;
+    s0 = s1;
+    s1 = t;
+  } else {
+    dir = neg(dir);
+  }
+  v2 s2 = minkowski(a, b, dir);
+  for (int step = 0; step < 32; ++step) {
+    bool c1 = dot(s2, dir) <= 0.0f;
+    bool c2 = dot(fnormal(sub(s2, s0)), neg(s2)) < 0.0f;
+    bool c3 = dot(fnormal(sub(s1, s2)), neg(s2)) < 0.0f;
+    if (c1 || (c2 && c3)) break;
+    v2 c = s2;
+    v2 acn = fnormal(sub(c, s0)), cbn = fnormal(sub(s1, c));
+    if (dot(acn, neg(c)) >= 0.0f) {
+      s1 = c;
+      dir = acn;
+    } else {
+      s0 = c;
+      dir = cbn;
+    }
+    s2 = minkowski(a, b, dir);
+  }
+  v2 z = v2{0.0f, 0.0f};
+  if (!point_in_triangle0(s0, s1, s2)) {
+    s0 = z;
+    s1 = z;
+    s2 = z;
+  }
+  // check_for_collision_convex :300-310
+  float area = crs(sub(s1, s0), sub(s2, s0));
+  bool allzero = s0.x == 0.0f && s0.y == 0.0f && s1.x == 0.0f && s1.y == 0.0f && s2.x == 0.0f && s2.y == 0.0f;
+  bool anynan = vnan(s0) || vnan(s1) || vnan(s2);
+  simplex[0] = s0;
+  simplex[1] = s1;
+  simplex[2] = s2;
+  return !(allzero || anynan || area == 0.0f);
+}
+
+// ---------------------------------------------------------------------------
+// EPA (cotix/_collisions.py:115-273), edge buffer of NE = iters + 3 edges.
+// Distances are cached per edge (only the two rewritten edges change per
+// iteration); the reference recomputes all of them -- same values.
+// ---------------------------------------------------------------------------
+CX_DEV v2 closest_on_edge_to_origin(v2 a, v2 b) {  // :156-166, point = 0
+  v2 p = v2{0.0f, 0.0f};
+  float len = sumsq(sub(a, b));
+  if (len == 0.0f) return sub(p, a);
+  float t = dot(sub(p, b), sub(a, b)) / len;
+  t = clip_(t, 0.0f, 1.0f);
+  v2 proj = add(b, scl(sub(a, b), t));
+  return sub(p, proj);
+}
+CX_DEV float edge_dist(v2 a, v2 b) {  // distance_to_origin :137-154,168-169
+  if (a.x == 0.0f && a.y == 0.0f && b.x == 0.0f && b.y == 0.0f) {
+    float i = finf();
+    return i * i + i * i;
+  }
+  v2 p = v2{0.0f, 0.0f};
+  float len = sumsq(sub(a, b));
+  float t = dot(sub(p, b), sub(a, b)) / len;
+  t = clip_(t, 0.0f, 1.0f);
+  v2 proj = add(b, scl(sub(a, b), t));
+  v2 disp = sub(p, proj);
+  if (len == 0.0f) disp = neg(a);
+  return sumsq(disp);
+}
+
+template <int NE>
+CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters) {
+  v2 e0[NE], e1[NE];
+  float dist[NE];
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    e0[k] = v2{0.0f, 0.0f};
+    e1[k] = v2{0.0f, 0.0f};
+  }
+  e0[0] = simplex[0]; e1[0] = simplex[1];
+  e0[1] = simplex[1]; e1[1] = simplex[2];
+  e0[2] = simplex[2]; e1[2] = simplex[0];
+  const int ne = iters + 3;
+#pragma unroll
+  for (int k = 0; k < NE; ++k) dist[k] = (k < ne) ? edge_dist(e0[k], e1[k]) : finf();
+  auto argmin_d = [&]() {
+    int nanidx = -1, b = 0;
+    float bv = dist[0];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      if (k < ne) {
+        if (nanidx < 0 && isn(dist[k])) nanidx = k;
+        if (k > 0 && dist[k] < bv) {
+          bv = dist[k];
+          b = k;
+        }
+      }
+    }
+    return nanidx >= 0 ? nanidx : b;
+  };
+  int bei = argmin_d();
+  v2 best0 = e0[0], best1 = e1[0];
+#pragma unroll
+  for (int k = 0; k < NE; ++k)
+    if (k == bei) { best0 = e0[k]; best1 = e1[k]; }
+  v2 newp = simplex[2];
+  v2 prev0 = e0[0], prev1 = e1[0];
+  for (int i = 0; i < iters; ++i) {
+    bool c1 = sumsq(sub(best0, best1)) > 1e-9f;
+    bool c2 = crs(best0, best1) >= 0.0f;
+    v2 n = fnormal(sub(prev0, prev1));
+    n = divs(n, nrm(n));
+    float d = dot(newp, n);
+    float ed = nrm(closest_on_edge_to_origin(prev0, prev1));
+    bool c4 = (d - ed > 1e-6f) || (d <= 0.0f);
+    if (!(c4 && !vnan(best0) && !vnan(best1) && c1 && c2)) break;
+    n = fnormal(sub(best0, best1));
+    n = divs(n, nrm(n));
+    newp = minkowski(a, b, n);
+    const int slot = i + 3;
+    const float dA = edge_dist(best0, newp), dB = edge_dist(newp, best1);
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      if (k == bei) { e1[k] = newp; dist[k] = dA; }
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      if (k == slot) { e0[k] = newp; e1[k] = best1; dist[k] = dB; }
+    }
+    prev0 = best0;
+    prev1 = best1;
+    bei = argmin_d();
+#pragma unroll
+    for (int k = 0; k < NE; ++k)
+      if (k == bei) { best0 = e0[k]; best1 = e1[k]; }
+  }
+  return closest_on_edge_to_origin(best0, best1);
+}
+
+// generic-iteration EPA (circle_vs_polygon uses 128 iterations): buffer in
+// private memory.  Not on either scenario's path.
+CX_DEV v2 epa_big(const Shape& a, const Shape& b, const v2* simplex, int iters) {
+  constexpr int NE = 131;
+  v2 e0[NE], e1[NE];
+  float dist[NE];
+  const int ne = iters + 3;
+  for (int k = 0; k < ne; ++k) { e0[k] = v2{0.0f, 0.0f}; e1[k] = v2{0.0f, 0.0f}; }
+  e0[0] = simplex[0]; e1[0] = simplex[1];
+  e0[1] = simplex[1]; e1[1] = simplex[2];
+  e0[2] = simplex[2]; e1[2] = simplex[0];
+  for (int k = 0; k < ne; ++k) dist[k] = edge_dist(e0[k], e1[k]);
+  int bei = argmin_first(dist, ne);
+  v2 best0 = e0[bei], best1 = e1[bei], newp = simplex[2], prev0 = e0[0], prev1 = e1[0];
+  for (int i = 0; i < iters; ++i) {
+    bool c1 = sumsq(sub(best0, best1)) > 1e-9f;
+    bool c2 = crs(best0, best1) >= 0.0f;
+    v2 n = fnormal(sub(prev0, prev1));
+    n = divs(n, nrm(n));
+    float d = dot(newp, n);
+    float ed = nrm(closest_on_edge_to_origin(prev0, prev1));
+    bool c4 = (d - ed > 1e-6f) || (d <= 0.0f);
+    if (!(c4 && !vnan(best0) && !vnan(best1) && c1 && c2)) break;
+    n = fnormal(sub(best0, best1));
+    n = divs(n, nrm(n));
+    newp = minkowski(a, b, n);
+    e1[bei] = newp;
+    dist[bei] = edge_dist(best0, newp);
+    e0[i + 3] = newp;
+    e1[i + 3] = best1;
+    dist[i + 3] = edge_dist(newp, best1);
+    prev0 = best0;
+    prev1 = best1;
+    bei = argmin_first(dist, ne);
+    best0 = e0[bei];
+    best1 = e1[bei];
+  }
+  return closest_on_edge_to_origin(best0, best1);
+}
+
+// ---------------------------------------------------------------------------
+// edge-based contact point (cotix/_contacts.py:205-267)
+// ---------------------------------------------------------------------------
+CX_DEV v2 edge_vs_edge(v2 pa0, v2 pa1, v2 qb0, v2 qb1) {  // :206-225
+  v2 p = pa0, r = sub(pa1, pa0), q = qb0, s = sub(qb1, qb0);
+  auto c2 = [](v2 u, v2 v) { return u.x * v.y - v.x * u.y; };
+  float c = c2(r, s);
+  float t = c2(sub(q, p), s) / c;
+  float u = c2(sub(q, p), r) / c;
+  if (c != 0.0f && t >= 0.0f && t <= 1.0f && u >= 0.0f && u <= 1.0f) return add(p, scl(r, t));
+  return v2{qnan(), qnan()};
+}
+// A and B given as convex n-gons with edges (v_k, v_{k-1}) -- the AABB's
+// own edge list [(v0,v1),(v1,v2),(v2,v3),(v3,v0)] is passed explicitly.
+struct EdgeSet {
+  int n;
+  v2 v[MAXV];      // vertices (get_vertices)
+  v2 ea[MAXV], eb[MAXV];  // edges (get_edges)
+};
+CX_DEV void edges_of_poly(const Shape& s, EdgeSet* e) {
+  e->n = s.n;
+  for (int k = 0; k < s.n; ++k) {
+    e->v[k] = vert(s, k);
+    e->ea[k] = vert(s, k);
+    e->eb[k] = vert(s, k == 0 ? s.n - 1 : k - 1);
+  }
+}
+CX_DEV void edges_of_aabb(const Shape& s, EdgeSet* e) {
+  e->n = 4;
+  aabb_verts(s, e->v);
+  for (int k = 0; k < 4; ++k) {
+    e->ea[k] = e->v[k];
+    e->eb[k] = e->v[(k + 1) & 3];
+  }
+}
+CX_DEV bool shape_contains(const Shape& s, v2 p) {
+  if (s.kind == KIND_AABB) return aabb_contains(s, p);
+  if (s.kind == KIND_CIRCLE) return circle_contains(s, p);
+  return poly_contains(s, p);
+}
+CX_DEV v2 contact_from_edges(const Shape& A, const EdgeSet& ea, const Shape& B, const EdgeSet& eb) {
+  float n = 0.0f;
+  v2 acc = v2{0.0f, 0.0f};
+  for (int k = 0; k < ea.n; ++k)
+    if (shape_contains(B, ea.v[k])) { acc = add(acc, ea.v[k]); n = n + 1.0f; }
+  for (int k = 0; k < eb.n; ++k)
+    if (shape_contains(A, eb.v[k])) { acc = add(acc, eb.v[k]); n = n + 1.0f; }
+  for (int jb = 0; jb < eb.n; ++jb)
+    for (int ia = 0; ia < ea.n; ++ia) {
+      v2 x = edge_vs_edge(ea.ea[ia], ea.eb[ia], eb.ea[jb], eb.eb[jb]);
+      if (!vnan(x)) { acc = add(acc, x); n = n + 1.0f; }
+    }
+  if (n > 0.0f) return divs(acc, n);
+  return v2{qnan(), qnan()};
+}
+
+// polygon_vs_polygon :294-315 / aabb_vs_polygon :270-291 (A may be an AABB)
+CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, v2 d0) {
+  v2 simplex[3];
+  if (!gjk(A, B, d0, simplex)) return nan_contact();
+  int iters = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
+  if (iters > 48) iters = 48;
+  Contact c;
+  if (iters + 3 <= 14) c.pen = epa<14>(A, B, simplex, iters);
+  else if (iters + 3 <= 20) c.pen = epa<20>(A, B, simplex, iters);
+  else c.pen = epa_big(A, B, simplex, iters);
+  EdgeSet ea, eb;
+  if (A.kind == KIND_AABB) edges_of_aabb(A, &ea);
+  else edges_of_poly(A, &ea);
+  edges_of_poly(B, &eb);
+  c.cp = contact_from_edges(A, ea, B, eb);
+  return c;
+}
+
+// circle_vs_polygon :157-202
+CX_DEV Contact circle_vs_polygon(const Shape& C, const Shape& P, v2 d0) {
+  v2 simplex[3];
+  if (!gjk(C, P, d0, simplex)) return nan_contact();
+  Contact c;
+  c.pen = epa_big(C, P, simplex, 128);
+  v2 pos = v2{C.d[1], C.d[2]};
+  float dists[MAXV];
+  v2 disps[MAXV];
+  for (int k = 0; k < P.n; ++k) {
+    v2 a = vert(P, k), b = vert(P, k == 0 ? P.n - 1 : k - 1);
+    if (a.x == 0.0f && a.y == 0.0f && b.x == 0.0f && b.y == 0.0f) {
+      disps[k] = v2{finf(), finf()};
+    } else {
+      float len = sumsq(sub(a, b));
+      float t = dot(sub(pos, b), sub(a, b)) / len;
+      t = clip_(t, 0.0f, 1.0f);
+      disps[k] = sub(pos, add(b, scl(sub(a, b), t)));
+    }
+    dists[k] = sumsq(disps[k]);
+  }
+  int k = argmin_first(dists, P.n);
+  c.cp = add(pos, disps[k]);
+  if (dists[k] > C.d[0] * C.d[0]) c.cp = pos;
+  return c;
+}
+
+// contact function ids (the _contact_funcs registry, cotix/_colliders.py:21-35)
+enum : int {
+  FN_AABB_AABB = 0,
+  FN_CIRCLE_CIRCLE = 1,
+  FN_CIRCLE_AABB = 2,
+  FN_POLY_POLY = 3,
+  FN_AABB_POLY = 4,
+  FN_CIRCLE_POLY = 5,
+};
+CX_DEV Contact run_contact(int fn, const Shape& a, const Shape& b, v2 d0, uint32_t* err) {
+  switch (fn) {
+    case FN_AABB_AABB: return aabb_vs_aabb(a, b);
+    case FN_CIRCLE_CIRCLE: return circle_vs_circle(a, b);
+    case FN_CIRCLE_AABB: return circle_vs_aabb(a, b, err);
+    case FN_POLY_POLY:
+    case FN_AABB_POLY: return convex_vs_polygon(a, b, d0);
+    default: return circle_vs_polygon(a, b, d0);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bodies / resolution (cotix/_collision_resolution.py, cotix/_bodies.py)
+// ---------------------------------------------------------------------------
+struct Dyn {
+  float px, py, vx, vy, a, w;
+};
+struct Params {
+  float mass, inertia, elast, fric;
+};
+CX_DEV v2 velocity_at(const Dyn& b, v2 p) {  // _bodies.py:50-55
+  v2 r = sub(p, v2{b.px, b.py});
+  return v2{b.vx + (-r.y) * b.w, b.vy + r.x * b.w};
+}
+CX_DEV void apply_impulse(Dyn& b, const Params& m, v2 imp, v2 point) {  // :68-73
+  v2 arm = sub(point, v2{b.px, b.py});
+  float torque = crs(arm, imp);
+  b.vx = b.vx + imp.x / m.mass;
+  b.vy = b.vy + imp.y / m.mass;
+  b.w = b.w + torque / m.inertia;
+}
+CX_DEV void resolve_collision(Dyn& b1, const Params& m1, Dyn& b2, const Params& m2, v2 pen, v2 cp) {  // :52-151
+  if (vnan(cp)) return;
+  v2 v1 = velocity_at(b1, cp), v2_ = velocity_at(b2, cp);
+  v2 relv = sub(v2_, v1);
+  float pn = nrm(pen);
+  v2 n = v2{pen.x / pn, pen.y / pn};
+  float vn = dot(relv, n);
+  float e = fmin_(m1.elast, m2.elast);
+  v2 r1 = sub(cp, v2{b1.px, b1.py}), r2 = sub(cp, v2{b2.px, b2.py});
+  float lev1 = r1.x * r1.x + r1.y * r1.y, lev2 = r2.x * r2.x + r2.y * r2.y;
+  float ang = lev1 / m1.inertia + lev2 / m2.inertia;
+  float nim = (-(1.0f + e)) * vn - (0.3f * nrm(pen)) / 0.01f;
+  float ni = nim / ((1.0f / m1.mass + 1.0f / m2.mass) + ang);
+  v2 imp = scl(n, ni);
+  float mu = (m1.fric + m2.fric) / 2.0f;
+  v2 vd = v2{relv.x + vn * n.x, relv.y + vn * n.y};
+  float vdn = nrm(vd);
+  v2 vdu = v2{vd.x / vdn, vd.y / vdn};
+  float idr = (-vdn) / ((1.0f / m1.mass + 1.0f / m2.mass) + ang);
+  idr = clip_(idr, 0.0f, ni * mu);
+  imp = add(imp, scl(vdu, idr));
+  if (dot(pen, relv) < 0.0f) return;
+  apply_impulse(b1, m1, neg(imp), cp);
+  apply_impulse(b2, m2, imp, cp);
+}
+CX_DEV v2 rotate(v2 v, float ang) {  // _geometry_utils.py:81-88
+  float s, c;
+  sincos32(ang, &s, &c);
+  return v2{c * v.x + (-s) * v.y, s * v.x + c * v.y};
+}
+
+}  // namespace cx

@@ -1,0 +1,178 @@
+// cotix_scene.h -- host-side scene compiler: the collider's trace-time work
+// (cotix/_colliders.py:86-131) done once per scene.  Host C++ only; shared by
+// the library (cotix_step.hip) and the CPU emulation harness (tests/emu).
+#pragma once
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+#include "cotix_kernel.h"
+
+namespace cxk {
+
+inline int scene_fail(std::string& err, const std::string& m) {
+  err = m;
+  return -1;
+}
+
+inline int registry_fn(int ta, int tb) {
+  // _contact_funcs keys (cotix/_colliders.py:21-35), exact types
+  using namespace cx;
+  if (ta == COTIX_AABB && tb == COTIX_AABB) return FN_AABB_AABB;
+  if (ta == COTIX_CIRCLE && tb == COTIX_CIRCLE) return FN_CIRCLE_CIRCLE;
+  if (ta == COTIX_CIRCLE && tb == COTIX_AABB) return FN_CIRCLE_AABB;
+  if (ta == COTIX_POLYGON && tb == COTIX_POLYGON) return FN_POLY_POLY;
+  if (ta == COTIX_AABB && (tb == COTIX_POLYGON || tb == COTIX_POLYGON4 || tb == COTIX_POLYGON6)) return FN_AABB_POLY;
+  if (ta == COTIX_CIRCLE && (tb == COTIX_POLYGON || tb == COTIX_POLYGON4 || tb == COTIX_POLYGON6))
+    return FN_CIRCLE_POLY;
+  if (ta == COTIX_POLYGON4 && (tb == COTIX_POLYGON4 || tb == COTIX_POLYGON6)) return FN_POLY_POLY;
+  if (ta == COTIX_POLYGON6 && tb == COTIX_POLYGON6) return FN_POLY_POLY;
+  return -1;
+}
+
+
+// Compiles the body/part description into SceneDev tables.  Returns 0 or -1
+// (message in err).  n_cand / fnset: candidate count and contact-function set.
+inline int compile_scene(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                         const int* part_type, const int* part_nverts, SceneDev& s, int& n_cand, int& fnset,
+                         std::string& err) {
+  if (!body_params || !part_body || !part_type) return scene_fail(err, "null argument");
+
+  if (n_bodies < 1 || n_bodies > MAXB) return scene_fail(err, "n_bodies out of range (1..16)");
+  if (n_parts < 1 || n_parts > MAXP) return scene_fail(err, "n_parts out of range (1..32)");
+  std::memset(&s, 0, sizeof(s));
+  s.nb = n_bodies;
+  s.np = n_parts;
+  // GJK start direction: random_direction(PRNGKey(1)) (cotix/_collisions.py:287-298)
+  uint32_t bx = 0xbd56c50bu, by = 0x3f7fa5d9u;
+  std::memcpy(&s.d0x, &bx, 4);
+  std::memcpy(&s.d0y, &by, 4);
+  for (int b = 0; b < n_bodies; ++b)
+    s.par[b] = cx::Params{body_params[4 * b], body_params[4 * b + 1], body_params[4 * b + 2], body_params[4 * b + 3]};
+  std::vector<std::vector<int>> parts_of(n_bodies);
+  int goff = 0, woff = 0;
+  for (int p = 0; p < n_parts; ++p) {
+    int b = part_body[p], t = part_type[p];
+    if (b < 0 || b >= n_bodies) return scene_fail(err, "part_body out of range");
+    if (p > 0 && b < part_body[p - 1]) return scene_fail(err, "parts must be grouped by body in body order");
+    s.part_body[p] = b;
+    if (t == COTIX_CIRCLE) {
+      s.part_kind[p] = cx::KIND_CIRCLE;
+      s.part_n[p] = 0;
+    } else if (t == COTIX_AABB) {
+      s.part_kind[p] = cx::KIND_AABB;
+      s.part_n[p] = 0;
+    } else if (t >= COTIX_POLYGON && t <= COTIX_POLYGON6) {
+      int n = (t == COTIX_POLYGON) ? (part_nverts ? part_nverts[p] : 0) : t;
+      if (n < 3 || n > cx::MAXV) return scene_fail(err, "polygon vertex count must be 3..8");
+      s.part_kind[p] = cx::KIND_POLY;
+      s.part_n[p] = n;
+    } else {
+      return scene_fail(err, "unknown part type");
+    }
+    int nf = s.part_kind[p] == cx::KIND_CIRCLE ? 4 : (s.part_kind[p] == cx::KIND_AABB ? 4 : 2 * s.part_n[p]);
+    s.part_goff[p] = goff;
+    s.part_woff[p] = woff;
+    goff += nf;
+    woff += nf;
+    parts_of[b].push_back(p);
+  }
+  s.G = goff;
+  s.W = woff;
+  // enumeration, cotix/_colliders.py:86-113 (dict insertion order of type keys)
+  std::vector<std::pair<int, int>> tkeys;
+  std::vector<std::vector<std::pair<int, int>>> l1, l2;  // (body, part)
+  for (int i = 0; i < n_bodies; ++i)
+    for (int j = 0; j < n_bodies; ++j) {
+      if (i <= j) continue;
+      for (int pa : parts_of[i])
+        for (int pb : parts_of[j]) {
+          int t1 = part_type[pa], t2 = part_type[pb];
+          std::pair<int, int> key;
+          if (registry_fn(t1, t2) >= 0) key = {t1, t2};
+          else if (registry_fn(t2, t1) >= 0) key = {t2, t1};
+          else return scene_fail(err, "illegal shape pair (cotix/_colliders.py:103-107)");
+          int k = -1;
+          for (size_t q = 0; q < tkeys.size(); ++q)
+            if (tkeys[q] == key) k = (int)q;
+          if (k < 0) {
+            k = (int)tkeys.size();
+            tkeys.push_back(key);
+            l1.emplace_back();
+            l2.emplace_back();
+          }
+          l1[k].push_back({i, pa});
+          l2[k].push_back({j, pb});
+        }
+    }
+  if ((int)tkeys.size() > MAXT) return scene_fail(err, "too many type keys");
+  s.nt = (int)tkeys.size();
+  std::map<std::tuple<int, int, int>, int> cid_of;
+  std::map<std::pair<int, int>, std::vector<uint32_t>> cells;  // forward scan order
+  std::vector<std::pair<int, int>> cell_order;
+  auto get_cid = [&](int a, int b, int fn) -> int {
+    auto key = std::make_tuple(a, b, fn);
+    auto it = cid_of.find(key);
+    if (it != cid_of.end()) return it->second;
+    int c = (int)cid_of.size();
+    cid_of[key] = c;
+    return c;
+  };
+  std::vector<std::tuple<int, int, int>> clist;
+  for (int k = 0; k < s.nt; ++k) {
+    int N1 = (int)l1[k].size(), N2 = (int)l2[k].size();
+    if (N1 > 511 || N2 > 511) return scene_fail(err, "candidate list longer than 511");
+    s.type_n1[k] = N1;
+    s.type_n2[k] = N2;
+    int fn = registry_fn(tkeys[k].first, tkeys[k].second);
+    for (int i2 = 0; i2 < N2; ++i2)
+      for (int i1 = 0; i1 < N1; ++i1) {
+        int bi = l1[k][i1].first, pa = l1[k][i1].second, bj = l2[k][i2].first, pb = l2[k][i2].second;
+        int a = pa, b = pb;
+        if (registry_fn(part_type[pa], part_type[pb]) < 0) std::swap(a, b);  // :155-157
+        bool cand = bi >= bj;
+        if (!cand && fn != cx::FN_CIRCLE_AABB) continue;  // masked & side-effect free
+        size_t before = cid_of.size();
+        int c = get_cid(a, b, fn);
+        if (cid_of.size() != before) clist.push_back(std::make_tuple(a, b, fn));
+        if (!cand) continue;
+        auto ck = std::make_pair(bi, bj);
+        if (!cells.count(ck)) cell_order.push_back(ck);
+        cells[ck].push_back((uint32_t)i1 | ((uint32_t)i2 << 9) | ((uint32_t)c << 18) | ((uint32_t)k << 27));
+      }
+  }
+  if ((int)clist.size() > MAXC || (int)clist.size() > 511) return scene_fail(err, "too many distinct contacts");
+  s.nc = (int)clist.size();
+  for (int c = 0; c < s.nc; ++c) {
+    s.c_pa[c] = std::get<0>(clist[c]);
+    s.c_pb[c] = std::get<1>(clist[c]);
+    s.c_fn[c] = std::get<2>(clist[c]);
+  }
+  if ((int)cells.size() > MAXL) return scene_fail(err, "too many cells");
+  s.nl = (int)cells.size();
+  int nc_tot = 0, l = 0;
+  for (auto& ck : cell_order) {
+    auto& v = cells[ck];
+    s.cell_i[l] = ck.first;
+    s.cell_j[l] = ck.second;
+    s.cell_beg[l] = nc_tot;
+    s.cell_cnt[l] = (int)v.size();
+    if (nc_tot + (int)v.size() > MAXCAND) return scene_fail(err, "too many candidates");
+    // types ascend, then (ind2, ind1) ascend in v: reverse = last write first
+    for (int q = (int)v.size() - 1; q >= 0; --q) s.cand[nc_tot++] = v[q];
+    ++l;
+  }
+  n_cand = nc_tot;
+  fnset = 0;
+  for (int c = 0; c < s.nc; ++c) {
+    int fn = s.c_fn[c];
+    fnset |= (fn == cx::FN_AABB_AABB || fn == cx::FN_CIRCLE_AABB || fn == cx::FN_CIRCLE_CIRCLE) ? FNS_ANALYTIC
+             : (fn == cx::FN_CIRCLE_POLY ? FNS_CIRCLE_POLY : FNS_CONVEX);
+  }
+  return 0;
+}
+
+}  // namespace cxk

@@ -1,0 +1,361 @@
+// cotix_step.hip -- MI355X (gfx950) kernels of the cotix per-step hot path and
+// the C-ABI declared in include/cotix_amd.h.  The fused step kernel's phases
+// live in cotix_kernel.h (design notes there and in DESIGN.md).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/cotix_amd.h"
+#include "cotix_device.h"
+#include "cotix_kernel.h"
+#include "cotix_scene.h"
+
+using cxk::BLK;
+using cxk::FNS_ANALYTIC;
+using cxk::FNS_CIRCLE_POLY;
+using cxk::FNS_CONVEX;
+using cxk::SceneDev;
+
+namespace {
+thread_local std::string g_err;
+int fail(const std::string& m) {
+  g_err = m;
+  return -1;
+}
+int hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) return fail(std::string(what) + ": " + hipGetErrorString(e));
+  return 0;
+}
+}  // namespace
+
+struct cotix_scene {
+  SceneDev host;
+  SceneDev* dev = nullptr;
+  int n_candidates = 0;
+  int fnset = 0;
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// the fused step kernel: one workgroup = one tile of E envs, all n_steps
+// ---------------------------------------------------------------------------
+template <int E, int FNSET>
+__global__ __launch_bounds__(BLK) void step_kernel(cxk::KArgs a) {
+  extern __shared__ uint32_t lds[];
+  const SceneDev& sc = *a.sc;
+  const cxk::Lay L = cxk::layout(sc);
+  const cxk::Tile<E> t{lds};
+  const int tid = threadIdx.x, env0 = blockIdx.x * E;
+  cxk::ph_load<E>(a, sc, L, t, env0, tid);
+  __syncthreads();
+  for (int step = 0; step < a.n_steps; ++step) {
+    cxk::ph_A<E>(a, sc, L, t, env0, tid, step);
+    __syncthreads();
+    if (a.stages & COTIX_STAGE_COLLIDER) {
+      if (!(a.dbg_skip & 1)) cxk::ph_T<E>(a, sc, L, t, env0, tid);
+      __syncthreads();
+      if (!(a.dbg_skip & 2)) cxk::ph_B<E, FNSET>(a, sc, L, t, env0, tid);
+      __syncthreads();
+      if (!(a.dbg_skip & 4)) cxk::ph_C<E>(a, sc, L, t, env0, tid);
+      __syncthreads();
+      if (!(a.dbg_skip & 8)) cxk::ph_D<E>(a, sc, L, t, env0, tid);
+      __syncthreads();
+    }
+    cxk::ph_E<E>(a, sc, L, t, env0, tid);
+    __syncthreads();
+  }
+  cxk::ph_store<E>(a, sc, L, t, env0, tid);
+}
+
+// ---------------------------------------------------------------------------
+// operator kernels
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ cx::Shape load_shape(const float* p) {
+  cx::Shape s;
+  s.kind = (int)p[0];
+  s.n = (int)p[1];
+  for (int k = 0; k < 2 * cx::MAXV; ++k) s.d[k] = p[2 + k];
+  return s;
+}
+__global__ void contacts_kernel(int fn, int n, const float* a, const float* b, float* out, uint32_t* err, float d0x,
+                                float d0y) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  cx::Shape A = load_shape(a + 18 * (size_t)i), Bs = load_shape(b + 18 * (size_t)i);
+  uint32_t er = 0u;
+  cx::Contact c = cx::run_contact(fn, A, Bs, cx::v2{d0x, d0y}, &er);
+  out[4 * (size_t)i + 0] = c.pen.x;
+  out[4 * (size_t)i + 1] = c.pen.y;
+  out[4 * (size_t)i + 2] = c.cp.x;
+  out[4 * (size_t)i + 3] = c.cp.y;
+  if (err) err[i] = er;
+}
+__global__ void resolve_kernel(int n, float* d1, const float* p1, float* d2, const float* p2, const float* con) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float* a = d1 + 6 * (size_t)i;
+  float* b = d2 + 6 * (size_t)i;
+  cx::Dyn x = cx::Dyn{a[0], a[1], a[2], a[3], a[4], a[5]}, y = cx::Dyn{b[0], b[1], b[2], b[3], b[4], b[5]};
+  const float* q1 = p1 + 4 * (size_t)i;
+  const float* q2 = p2 + 4 * (size_t)i;
+  cx::Params m1 = cx::Params{q1[0], q1[1], q1[2], q1[3]}, m2 = cx::Params{q2[0], q2[1], q2[2], q2[3]};
+  const float* c = con + 4 * (size_t)i;
+  cx::resolve_collision(x, m1, y, m2, cx::v2{c[0], c[1]}, cx::v2{c[2], c[3]});
+  a[2] = x.vx; a[3] = x.vy; a[5] = x.w;
+  b[2] = y.vx; b[3] = y.vy; b[5] = y.w;
+}
+__global__ void threefry_kernel(const uint32_t* k, const uint32_t* c, uint32_t* o, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  cx::key2 r = cx::threefry(cx::key2{k[2 * i], k[2 * i + 1]}, c[2 * i], c[2 * i + 1]);
+  o[2 * i] = r.a;
+  o[2 * i + 1] = r.b;
+}
+__global__ void split_kernel(const uint32_t* k, int n, int num, uint32_t* o) {
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)n * num) return;
+  int i = (int)(t / num), j = (int)(t % num);
+  cx::key2 r = cx::split_at(cx::key2{k[2 * i], k[2 * i + 1]}, (uint32_t)num, (uint32_t)j);
+  o[2 * t] = r.a;
+  o[2 * t + 1] = r.b;
+}
+// uniform(key, (count,)): word m of iota(count) counters, legacy layout
+__global__ void uniform_kernel(const uint32_t* k, int n, int count, float lo, float hi, float* o) {
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)n * count) return;
+  int i = (int)(t / count), m = (int)(t % count);
+  cx::key2 key = cx::key2{k[2 * i], k[2 * i + 1]};
+  int half = (count + 1) / 2;  // padded counter array split in two halves
+  uint32_t w = (m < half) ? cx::threefry(key, (uint32_t)m, (uint32_t)(m + half < count ? m + half : 0)).a
+                          : cx::threefry(key, (uint32_t)(m - half), (uint32_t)m).b;
+  // the odd pad counter is 0: block (half-1, pad) only feeds word half-1
+  o[t] = cx::fmax_(lo, cx::unit_float(w) * (hi - lo) + lo);
+}
+__global__ void order_cw_kernel(float* xy, int n, int nv) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v[2 * cx::MAXV];
+  for (int k = 0; k < 2 * nv; ++k) v[k] = xy[(size_t)i * 2 * nv + k];
+  cx::order_clockwise(v, nv);
+  for (int k = 0; k < 2 * nv; ++k) xy[(size_t)i * 2 * nv + k] = v[k];
+}
+__global__ void euler_kernel(float* dyn, int nb, int B, float dt) {
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)nb * B) return;
+  int b = (int)(t / B), g = (int)(t % B);
+  float* d = dyn + (size_t)b * 6 * B + g;
+  d[0] = d[0] + d[2 * (size_t)B] * dt;
+  d[(size_t)B] = d[(size_t)B] + d[3 * (size_t)B] * dt;
+  d[4 * (size_t)B] = d[4 * (size_t)B] + d[5 * (size_t)B] * dt;
+}
+__global__ void lunar_kernel(float* dyn, int B, cx::Params p0, cx::Params p1, cx::Params p2) {
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= B) return;
+  cx::Dyn d[3];
+  for (int b = 0; b < 3; ++b) {
+    float* q = dyn + (size_t)b * 6 * B + g;
+    d[b] = cx::Dyn{q[0], q[(size_t)B], q[2 * (size_t)B], q[3 * (size_t)B], q[4 * (size_t)B], q[5 * (size_t)B]};
+  }
+  cxk::lunar_constraints(d[0], d[1], d[2], p0, p1, p2);
+  for (int b = 0; b < 3; ++b) {
+    float* q = dyn + (size_t)b * 6 * B + g;
+    q[2 * (size_t)B] = d[b].vx;
+    q[3 * (size_t)B] = d[b].vy;
+    q[5 * (size_t)B] = d[b].w;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cotix_last_error(void) { return g_err.c_str(); }
+const char* cotix_version(void) { return "cotix_amd 0.1 (gfx950)"; }
+
+int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                       const int* part_type, const int* part_nverts, cotix_scene** out) {
+  if (!out) return fail("null argument");
+  cotix_scene* sc = new cotix_scene();
+  if (cxk::compile_scene(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, sc->host,
+                         sc->n_candidates, sc->fnset, g_err)) {
+    delete sc;
+    return -1;
+  }
+  *out = sc;
+  return 0;
+}
+
+int cotix_scene_destroy(cotix_scene* scene) {
+  if (!scene) return 0;
+  if (scene->dev) (void)hipFree(scene->dev);
+  delete scene;
+  return 0;
+}
+
+int cotix_scene_geom_floats(const cotix_scene* scene) { return scene ? scene->host.G : fail("null scene"); }
+
+int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, int* n_candidates, int* n_types) {
+  if (!scene) return fail("null scene");
+  if (n_contacts) *n_contacts = scene->host.nc;
+  if (n_cells) *n_cells = scene->host.nl;
+  if (n_candidates) *n_candidates = scene->n_candidates;
+  if (n_types) *n_types = scene->host.nt;
+  return 0;
+}
+
+// device copy of the scene tables, made on first use (so scenes compile on
+// hosts without a GPU; the first step is therefore not graph-capturable)
+static int scene_upload(cotix_scene* sc) {
+  if (sc->dev) return 0;
+  if (hip_check(hipMalloc(&sc->dev, sizeof(SceneDev)), "hipMalloc(scene)")) return -1;
+  return hip_check(hipMemcpy(sc->dev, &sc->host, sizeof(SceneDev), hipMemcpyHostToDevice), "hipMemcpy(scene)");
+}
+
+static int envs_per_block() {
+  const char* v = getenv("COTIX_ENVS_PER_BLOCK");
+  int e = v ? atoi(v) : 16;
+  return (e == 8 || e == 16 || e == 32) ? e : 16;
+}
+
+static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
+                     int geom_stride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                     const float* dyn_reset, uint32_t* resets, cotix_stream_t stream) {
+  if (!scene || !dyn || !keys || !err) return fail("null argument");
+  if ((stages & COTIX_STAGE_COLLIDER) && !geom) return fail("geometry required for the collider stage");
+  if (geom_stride != 0 && geom_stride < scene->host.G) return fail("geom_stride smaller than the scene geometry");
+  if (B <= 0 || n_steps <= 0) return B == 0 || n_steps == 0 ? 0 : fail("negative size");
+  if ((stages & COTIX_STAGE_LUNAR) && scene->host.nb < 3) return fail("LunarLander stage needs >= 3 bodies");
+  if (action && (action_body < 0 || action_body >= scene->host.nb)) return fail("action_body out of range");
+  if (scene_upload(scene)) return -1;
+  const int E = envs_per_block();
+  const size_t lds = (size_t)cxk::lds_words(scene->host) * E * 4;
+  if (lds > 160 * 1024) return fail("scene too large for the LDS tile");
+  dim3 grid((B + E - 1) / E), block(BLK);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const char* dbg = getenv("COTIX_DEBUG_SKIP");
+  cxk::KArgs ka{scene->dev, dyn,    keys,        err,       geom,   geom_stride,          B, n_steps, dt, stages,
+                action,     action_body, dyn_reset, resets, dbg ? atoi(dbg) : 0};
+  const int fs = scene->fnset;
+#define COTIX_LAUNCH(EE, FS) hipLaunchKernelGGL((step_kernel<EE, FS>), grid, block, lds, st, ka)
+#define COTIX_LAUNCH_E(FS)                \
+  if (E == 8) COTIX_LAUNCH(8, FS);        \
+  else if (E == 32) COTIX_LAUNCH(32, FS); \
+  else COTIX_LAUNCH(16, FS);
+  if ((fs & ~FNS_ANALYTIC) == 0) {
+    COTIX_LAUNCH_E(FNS_ANALYTIC)
+  } else if ((fs & FNS_CIRCLE_POLY) == 0) {
+    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX)
+  } else {
+    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY)
+  }
+#undef COTIX_LAUNCH_E
+#undef COTIX_LAUNCH
+  return hip_check(hipGetLastError(), "step_kernel launch");
+}
+
+int cotix_step(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
+               int B, int n_steps, float dt, int stages, const float* action, int action_body,
+               cotix_stream_t stream) {
+  return step_impl(scene, dyn, keys, err, geom, geom_stride, B, n_steps, dt, stages, action, action_body, nullptr,
+                   nullptr, stream);
+}
+
+int cotix_step_autoreset(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
+                         int geom_stride, int B, int n_steps, float dt, int stages, const float* dyn_reset,
+                         uint32_t* resets, cotix_stream_t stream) {
+  if (!dyn_reset) return fail("dyn_reset required");
+  return step_impl(scene, dyn, keys, err, geom, geom_stride, B, n_steps, dt, stages, nullptr, 0, dyn_reset, resets,
+                   stream);
+}
+
+int cotix_physics_euler(float* dyn, int n_bodies, int B, float dt, cotix_stream_t stream) {
+  if (!dyn) return fail("null argument");
+  long long n = (long long)n_bodies * B;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(euler_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), dyn, n_bodies, B, dt);
+  return hip_check(hipGetLastError(), "euler_kernel launch");
+}
+
+int cotix_collider_resolve(cotix_scene* scene, float* dyn, const uint32_t* keys, uint32_t* err, const float* geom,
+                           int geom_stride, int B, cotix_stream_t stream) {
+  // the fused kernel with the collider stage only; keys are read, not advanced
+  return cotix_step(scene, dyn, const_cast<uint32_t*>(keys), err, geom, geom_stride, B, 1, 0.0f,
+                    COTIX_STAGE_COLLIDER, nullptr, 0, stream);
+}
+
+int cotix_lunar_constraints(float* dyn, int B, cotix_stream_t stream) {
+  if (!dyn) return fail("null argument");
+  if (B <= 0) return 0;
+  // LunarLander body parameters (cotix/_lunar_lander.py:78-105)
+  cx::Params p0{30.0f, 30.0f, 1.0f, 0.1f}, p1{1.0f, 1.0f, 1.0f, 0.1f}, p2{1.0f, 1.0f, 1.0f, 0.1f};
+  hipLaunchKernelGGL(lunar_kernel, dim3((B + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dyn, B,
+                     p0, p1, p2);
+  return hip_check(hipGetLastError(), "lunar_kernel launch");
+}
+
+int cotix_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err, cotix_stream_t stream) {
+  if (!a || !b || !out) return fail("null argument");
+  if (fn < 0 || fn > 5) return fail("unknown contact function");
+  if (n <= 0) return 0;
+  float d0x, d0y;
+  uint32_t bx = 0xbd56c50bu, by = 0x3f7fa5d9u;
+  std::memcpy(&d0x, &bx, 4);
+  std::memcpy(&d0y, &by, 4);
+  hipLaunchKernelGGL(contacts_kernel, dim3((n + 127) / 128), dim3(128), 0, reinterpret_cast<hipStream_t>(stream), fn,
+                     n, a, b, out, err, d0x, d0y);
+  return hip_check(hipGetLastError(), "contacts_kernel launch");
+}
+
+int cotix_resolve(int n, float* dyn1, const float* par1, float* dyn2, const float* par2, const float* contact,
+                  cotix_stream_t stream) {
+  if (!dyn1 || !dyn2 || !par1 || !par2 || !contact) return fail("null argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n,
+                     dyn1, par1, dyn2, par2, contact);
+  return hip_check(hipGetLastError(), "resolve_kernel launch");
+}
+
+int cotix_threefry2x32(const uint32_t* keys, const uint32_t* ctr, uint32_t* out, int n, cotix_stream_t stream) {
+  if (!keys || !ctr || !out) return fail("null argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(threefry_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), keys,
+                     ctr, out, n);
+  return hip_check(hipGetLastError(), "threefry_kernel launch");
+}
+
+int cotix_random_split(const uint32_t* keys, int n, int num, uint32_t* out, cotix_stream_t stream) {
+  if (!keys || !out) return fail("null argument");
+  if (num <= 0) return fail("num must be positive");
+  long long t = (long long)n * num;
+  if (t <= 0) return 0;
+  hipLaunchKernelGGL(split_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), keys, n, num, out);
+  return hip_check(hipGetLastError(), "split_kernel launch");
+}
+
+int cotix_random_uniform(const uint32_t* keys, int n, int count, float lo, float hi, float* out,
+                         cotix_stream_t stream) {
+  if (!keys || !out) return fail("null argument");
+  if (count <= 0) return fail("count must be positive");
+  long long t = (long long)n * count;
+  if (t <= 0) return 0;
+  hipLaunchKernelGGL(uniform_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), keys, n, count, lo, hi, out);
+  return hip_check(hipGetLastError(), "uniform_kernel launch");
+}
+
+int cotix_order_clockwise(float* xy, int n, int nverts, cotix_stream_t stream) {
+  if (!xy) return fail("null argument");
+  if (nverts < 1 || nverts > cx::MAXV) return fail("nverts must be 1..8");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(order_cw_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), xy,
+                     n, nverts);
+  return hip_check(hipGetLastError(), "order_cw_kernel launch");
+}
+
+}  // extern "C"

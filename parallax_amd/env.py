@@ -1,0 +1,46 @@
+"""env.reset() / env.step() over a batched scenario (the north-star surface;
+the reference's intended env API is the non-functional
+AbstractEnvironment.eval, cotix/_envs.py:37-132).
+
+  env = BatchedEnv(RoboCupEnv(batch=4096, perturb=True))
+  env.reset()
+  env.step(n_steps=64)          # 64 driver steps fused in one launch
+  obs = env.observation()       # f32 [B, n_bodies, 6]
+"""
+import torch
+
+
+class BatchedEnv:
+    def __init__(self, scenario, dt=1e-2, autoreset=False):
+        self.scenario = scenario
+        self.world = scenario.world
+        self.dt = dt
+        self.autoreset = autoreset
+        self.resets = torch.zeros(self.world.B, dtype=torch.int32, device=self.world.device)
+        self._keys0 = self.world.keys.clone()
+
+    def reset(self):
+        self.world.dyn.copy_(self.scenario.dyn_reset)
+        self.world.keys.copy_(self._keys0)
+        self.world.err.zero_()
+        self.resets.zero_()
+        return self.observation()
+
+    def step(self, n_steps=1, action=None, action_body=None):
+        w = self.world
+        if self.autoreset:
+            if action is not None:
+                raise ValueError("autoreset and action are exclusive")
+            w.step(n_steps, self.dt, self.scenario.stages, dyn_reset=self.scenario.dyn_reset, resets=self.resets)
+        else:
+            body = len(w.bodies) - 1 if action_body is None else action_body
+            w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body)
+        return self.observation()
+
+    def observation(self):
+        """[B, n_bodies, 6] view-copy of (px, py, vx, vy, angle, angular_velocity)."""
+        return self.world.dyn.permute(2, 0, 1)
+
+    @property
+    def err(self):
+        return self.world.err

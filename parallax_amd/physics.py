@@ -1,0 +1,119 @@
+"""The reference's operator/plugin surface for the hot path, over Worlds.
+
+  ExplicitEulerPhysics.step(bodies, dt) -> (bodies, self)     cotix/_physics_solvers.py:16-33
+  RandomizedCollider.resolve(bodies, rkey) -> bodies          cotix/_colliders.py:74-351
+  SimpleConstraintSolver(loops).solve(bodies, constraints)    cotix/_constraint_solvers.py:4-17
+  contact_funcs[(Ta, Tb)](a, b) -> ContactInfo (batched)      cotix/_colliders.py:21-35
+  resolve_collision(b1, b2, contact) (batched)                cotix/_collision_resolution.py:52-151
+
+``bodies`` is a World (the batched body list); operators update it in place
+on the device and return it, so the reference's functional call sites
+(``new_bodies, _ = physics.step(bodies, dt)``) read the same.
+"""
+import torch
+
+from . import _ffi
+from .shapes import AABB, Circle, Polygon, Polygon4, Polygon6
+
+
+class AbstractPhysicsSolver:
+    def step(self, bodies, dt):
+        raise NotImplementedError
+
+
+class ExplicitEulerPhysics(AbstractPhysicsSolver):
+    def step(self, bodies, dt=1e-2):
+        bodies.euler(dt)
+        return bodies, self
+
+
+class AbstractCollider:
+    def resolve(self, bodies, *args, **kwargs):
+        raise NotImplementedError
+
+
+class RandomizedCollider(AbstractCollider):
+    def resolve(self, bodies, rkey=None, collision_callback=None):
+        """rkey: [B, 2] int32 keys (default: the world's own keys)."""
+        bodies.collide(rkey)
+        return bodies
+
+
+class SimpleConstraintSolver:
+    """No constraint class exists in the reference (grep: only
+    cotix/_constraint_solvers.py:8-16): with an empty list the solve is the
+    identity SoA round trip."""
+
+    def __init__(self, loops=1):
+        self.loops = loops
+
+    def solve(self, bodies, constraints):
+        for _ in range(self.loops):
+            for c in constraints:
+                bodies = c.apply(bodies)
+        return bodies
+
+
+class ContactInfo:
+    """Batched ContactInfo (cotix/_contacts.py:11-27): NaN contact_point = none."""
+
+    def __init__(self, penetration_vector, contact_point):
+        self.penetration_vector = penetration_vector
+        self.contact_point = contact_point
+
+    def isnan(self):
+        return torch.isnan(self.contact_point).any(-1)
+
+
+def shape_rows(shapes_geometry, kind, nverts=0):
+    """Pack world-frame geometry [n, k] into the [n, 18] operator layout."""
+    n = shapes_geometry.shape[0]
+    out = torch.zeros(n, 18, dtype=torch.float32, device=shapes_geometry.device)
+    out[:, 0] = kind
+    out[:, 1] = nverts
+    out[:, 2:2 + shapes_geometry.shape[1]] = shapes_geometry
+    return out
+
+
+KIND = {Circle: 0, AABB: 1}
+
+
+def run_contacts(fn, a_rows, b_rows):
+    """cotix_contacts over [n, 18] shape rows -> (ContactInfo, err[n])."""
+    n = a_rows.shape[0]
+    out = torch.empty(n, 4, dtype=torch.float32, device=a_rows.device)
+    err = torch.zeros(n, dtype=torch.int32, device=a_rows.device)
+    _ffi.check(_ffi.lib.cotix_contacts(fn, n, _ffi.ptr(a_rows.contiguous()), _ffi.ptr(b_rows.contiguous()),
+                                       _ffi.ptr(out), _ffi.ptr(err), _ffi.stream_ptr(a_rows.device)), "cotix_contacts")
+    return ContactInfo(out[:, 0:2], out[:, 2:4]), err
+
+
+# _contact_funcs registry (cotix/_colliders.py:21-35): (type, type) -> fn id
+contact_funcs = {
+    (AABB, AABB): _ffi.FN_AABB_AABB,
+    (Circle, Circle): _ffi.FN_CIRCLE_CIRCLE,
+    (Circle, AABB): _ffi.FN_CIRCLE_AABB,
+    (Polygon, Polygon): _ffi.FN_POLY_POLY,
+    (AABB, Polygon): _ffi.FN_AABB_POLY,
+    (Circle, Polygon): _ffi.FN_CIRCLE_POLY,
+    (Circle, Polygon4): _ffi.FN_CIRCLE_POLY,
+    (Circle, Polygon6): _ffi.FN_CIRCLE_POLY,
+    (AABB, Polygon4): _ffi.FN_AABB_POLY,
+    (AABB, Polygon6): _ffi.FN_AABB_POLY,
+    (Polygon4, Polygon4): _ffi.FN_POLY_POLY,
+    (Polygon4, Polygon6): _ffi.FN_POLY_POLY,
+    (Polygon6, Polygon6): _ffi.FN_POLY_POLY,
+}
+
+
+def resolve_collision(dyn1, par1, dyn2, par2, contact):
+    """Batched resolve_collision: dyn [n, 6] updated in place, par [n, 4]
+    (mass, inertia, elasticity, friction), contact [n, 4] (pen, cp)."""
+    n = dyn1.shape[0]
+    for t in (dyn1, dyn2):
+        if not t.is_contiguous():
+            raise ValueError("dyn tensors must be contiguous")
+    _ffi.check(_ffi.lib.cotix_resolve(n, _ffi.ptr(dyn1), _ffi.ptr(par1.contiguous()), _ffi.ptr(dyn2),
+                                      _ffi.ptr(par2.contiguous()), _ffi.ptr(contact.contiguous()),
+                                      _ffi.stream_ptr(dyn1.device)), "cotix_resolve")
+    return dyn1, dyn2

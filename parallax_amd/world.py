@@ -1,0 +1,135 @@
+"""A batched world: one compiled scene + SoA device state for B envs.
+
+Layout in HBM (DESIGN.md "Data layout"):
+  dyn   f32 [n_bodies][6][B]   px, py, vx, vy, angle, angular_velocity
+  keys  i32 [B][2]             collider PRNG key per env (uint32 bits)
+  err   i32 [B]                error bits (cotix/_contacts.py:105-107 trips)
+  geom  f32 [G] shared or [B][G] per env: local part geometry
+"""
+import torch
+
+from . import _ffi
+from .bodies import AnyBody, BodyView
+from .shapes import AbstractPolygon
+
+
+class Scene:
+    """cotix_scene_create: the collider's trace-time enumeration
+    (cotix/_colliders.py:86-131) compiled once into device tables."""
+
+    def __init__(self, bodies):
+        import ctypes
+        self.n_bodies = len(bodies)
+        params = torch.tensor([b.params() for b in bodies], dtype=torch.float32)
+        part_body, part_type, part_nv = [], [], []
+        for i, b in enumerate(bodies):
+            for p in b.shape.parts:
+                part_body.append(i)
+                part_type.append(p.type_id)
+                part_nv.append(p.vertices.shape[-2] if isinstance(p, AbstractPolygon) else 0)
+        self.parts = [p for b in bodies for p in b.shape.parts]
+        pb = torch.tensor(part_body, dtype=torch.int32)
+        pt = torch.tensor(part_type, dtype=torch.int32)
+        pn = torch.tensor(part_nv, dtype=torch.int32)
+        h = ctypes.c_void_p()
+        _ffi.check(_ffi.lib.cotix_scene_create(self.n_bodies, _ffi.ptr(params), len(part_body), _ffi.ptr(pb),
+                                               _ffi.ptr(pt), _ffi.ptr(pn), ctypes.byref(h)), "cotix_scene_create")
+        self.handle = h
+        self.geom_floats = _ffi.lib.cotix_scene_geom_floats(h)
+
+    def info(self):
+        import ctypes
+        v = [ctypes.c_int() for _ in range(4)]
+        _ffi.check(_ffi.lib.cotix_scene_info(self.handle, *[ctypes.byref(x) for x in v]), "cotix_scene_info")
+        return dict(zip(("contacts", "cells", "candidates", "types"), [x.value for x in v]))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and _ffi is not None and _ffi.lib is not None:
+            _ffi.lib.cotix_scene_destroy(h)
+            self.handle = None
+
+
+class World:
+    def __init__(self, bodies, batch=1, device="cuda", keys=None):
+        if not all(isinstance(b, AnyBody) for b in bodies):
+            raise TypeError("bodies must be AnyBody")
+        self.bodies = list(bodies)
+        self.B = int(batch)
+        self.device = torch.device(device)
+        self.scene = Scene(self.bodies)
+        self.geom = self._upload_geometry()
+        self.geom_stride = 0 if self.geom.dim() == 1 else self.geom.shape[1]
+        self.dyn = torch.stack([b.dyn_columns(self.B) for b in self.bodies], 0).to(self.device).contiguous()
+        self.keys = (keys if keys is not None else torch.zeros(self.B, 2, dtype=torch.int32)).to(
+            self.device, torch.int32).contiguous()
+        self.err = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+
+    # -- geometry ---------------------------------------------------------
+    def _upload_geometry(self):
+        cols, batched = [], False
+        for p in self.scene.parts:
+            g = p.local_geometry()
+            batched = batched or g.dim() == 2
+            cols.append(g)
+        if batched:
+            cols = [c.expand(self.B, -1) if c.dim() == 1 else c for c in cols]
+        geom = torch.cat(cols, dim=-1).to(self.device, torch.float32).contiguous()
+        # Polygon.__init__ sorts (cotix/_convex_shapes.py:143-144): do it on the device
+        off = 0
+        for p in self.scene.parts:
+            n = p.geom_floats()
+            if isinstance(p, AbstractPolygon) and not p.presorted:
+                sl = geom[..., off:off + n].contiguous()
+                nv = n // 2
+                _ffi.check(_ffi.lib.cotix_order_clockwise(_ffi.ptr(sl), sl.numel() // n, nv,
+                                                          _ffi.stream_ptr(self.device)), "cotix_order_clockwise")
+                geom[..., off:off + n] = sl
+            off += n
+        assert off == self.scene.geom_floats
+        return geom
+
+    # -- state access -----------------------------------------------------
+    def body(self, i):
+        return BodyView(self, i)
+
+    def set_dyn(self, dyn):
+        self.dyn.copy_(dyn)
+
+    # -- hot path ---------------------------------------------------------
+    def step(self, n_steps=1, dt=1e-2, stages=_ffi.STAGES_ROBOCUP, action=None, action_body=0,
+             dyn_reset=None, resets=None):
+        """Fused driver step (examples/test_viz.py:24-44 / :61-69), n_steps times."""
+        s = _ffi.stream_ptr(self.device)
+        if dyn_reset is not None:
+            _ffi.check(_ffi.lib.cotix_step_autoreset(
+                self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.keys), _ffi.ptr(self.err), _ffi.ptr(self.geom),
+                self.geom_stride, self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(dyn_reset),
+                _ffi.ptr(resets), s), "cotix_step_autoreset")
+            return self
+        if action is not None:
+            action = action.to(self.device, torch.float32).contiguous()
+            if action.shape != (n_steps, self.B, 2):
+                raise ValueError("action must be [n_steps, B, 2]")
+        _ffi.check(_ffi.lib.cotix_step(
+            self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.keys), _ffi.ptr(self.err), _ffi.ptr(self.geom),
+            self.geom_stride, self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(action), int(action_body), s),
+            "cotix_step")
+        return self
+
+    def euler(self, dt):
+        _ffi.check(_ffi.lib.cotix_physics_euler(_ffi.ptr(self.dyn), len(self.bodies), self.B, float(dt),
+                                                _ffi.stream_ptr(self.device)), "cotix_physics_euler")
+        return self
+
+    def collide(self, keys=None):
+        k = self.keys if keys is None else keys.to(self.device, torch.int32).contiguous()
+        _ffi.check(_ffi.lib.cotix_collider_resolve(
+            self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(k), _ffi.ptr(self.err), _ffi.ptr(self.geom),
+            self.geom_stride, self.B, _ffi.stream_ptr(self.device)), "cotix_collider_resolve")
+        return self
+
+    def lunar_constraints(self):
+        _ffi.check(_ffi.lib.cotix_lunar_constraints(_ffi.ptr(self.dyn), self.B, _ffi.stream_ptr(self.device)),
+                   "cotix_lunar_constraints")
+        return self

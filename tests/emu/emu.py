@@ -1,0 +1,62 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes front-end of the host emulation of the
+fused step kernel (tests/emu/cotix_emu.cpp)."""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+P_ = ctypes.c_void_p
+
+
+def load(asan=False):
+    path = os.path.join(HERE, "build", "libcotix_emu_asan.so" if asan else "libcotix_emu.so")
+    lib = ctypes.CDLL(path)
+    lib.emu_scene_create.argtypes = [ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.POINTER(P_)]
+    lib.emu_step.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                             ctypes.c_int, P_, ctypes.c_int, P_, P_, ctypes.c_int]
+    lib.emu_contacts.argtypes = [ctypes.c_int, ctypes.c_int, P_, P_, P_, P_]
+    lib.emu_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(P_)
+
+
+TYPE_ID = {"Circle": 0, "AABB": 1, "Polygon": 2, "Polygon3": 3, "Polygon4": 4, "Polygon5": 5, "Polygon6": 6}
+
+
+def oracle_scene(lib, bodies):
+    """Scene + local geometry from oracle Body objects."""
+    params = np.array([[b.mass, b.inertia, b.elasticity, b.friction_coefficient] for b in bodies], np.float32)
+    pb, pt, pn, geom = [], [], [], []
+    for i, b in enumerate(bodies):
+        for p in b.parts:
+            pb.append(i)
+            pt.append(TYPE_ID[p.kind])
+            if p.kind == "Circle":
+                pn.append(0)
+                geom += [p.radius, p.position[0], p.position[1], 0.0]
+            elif p.kind == "AABB":
+                pn.append(0)
+                geom += [p.lower[0], p.lower[1], p.upper[0], p.upper[1]]
+            else:
+                pn.append(len(p.vertices_))
+                for v in p.vertices_:
+                    geom += [v[0], v[1]]
+    pb, pt, pn = (np.array(x, np.int32) for x in (pb, pt, pn))
+    h = P_()
+    rc = lib.emu_scene_create(len(bodies), _p(params), len(pb), _p(pb), _p(pt), _p(pn), ctypes.byref(h))
+    if rc:
+        raise RuntimeError(lib.emu_last_error().decode())
+    return h, np.array(geom, np.float32)
+
+
+def step(lib, h, dyn, keys, err, geom, gstride, n_steps, stages, dt=1e-2, E=16, dyn_reset=None, resets=None):
+    """dyn f32 [nb, 6, B], keys u32 [B, 2], err u32 [B]: updated in place."""
+    B = dyn.shape[2]
+    for a in (dyn, keys, err, geom):
+        assert a.flags.c_contiguous
+    lib.emu_step(h, _p(dyn), _p(keys), _p(err), _p(geom), gstride, B, n_steps, dt, stages, None, 0,
+                 _p(dyn_reset), _p(resets), E)

@@ -1,0 +1,259 @@
+"""Generates the committed golden fixtures under tests/golden/ from the CPU
+oracle (oracle/cotix_oracle).  The oracle itself is pinned by the PRNG KATs
+and the reference's own test literals/properties (tests/test_oracle_*.py);
+these fixtures freeze its outputs so the GPU tests (which cannot import
+/root/reference) compare the HIP path against them bit for bit.
+
+    python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+
+from cotix_oracle import geometry as G  # noqa: E402
+from cotix_oracle import physics as P  # noqa: E402
+from cotix_oracle import prng  # noqa: E402
+
+F = np.float32
+D0 = prng.gjk_initial_direction()
+
+
+# ---------------------------------------------------------------------------
+# shape rows [18] = kind, nverts, d[16]  (the cotix_contacts operator layout)
+# ---------------------------------------------------------------------------
+def row(s):
+    r = np.zeros(18, F)
+    if s.kind == "Circle":
+        r[0], r[2], r[3], r[4] = 0, s.radius, s.position[0], s.position[1]
+    elif s.kind == "AABB":
+        r[0] = 1
+        r[2:6] = [s.lower[0], s.lower[1], s.upper[0], s.upper[1]]
+    else:
+        r[0], r[1] = 2, len(s.vertices_)
+        for k, v in enumerate(s.vertices_):
+            r[2 + 2 * k], r[3 + 2 * k] = v
+    return r
+
+
+def rand_circle(rng):
+    return G.Circle(F(rng.uniform(0.01, 5.0)), (F(rng.normal()), F(rng.normal())))
+
+
+def rand_aabb(rng, scale=1.0):
+    lo = np.array([rng.normal(), rng.normal()], F) * F(scale)
+    up = lo + np.array([rng.uniform(0.01, 5.0), rng.uniform(0.01, 5.0)], F)
+    return G.AABB(tuple(lo), tuple(up))
+
+
+def rand_poly(rng, n, spread=0.7):
+    c = rng.normal(size=2) * spread
+    ang = np.sort(rng.uniform(0, 2 * np.pi, n))
+    rad = rng.uniform(0.4, 1.2, n)
+    pts = [(F(c[0] + r * np.cos(a)), F(c[1] + r * np.sin(a))) for a, r in zip(ang, rad)]
+    rng.shuffle(pts)
+    return G.Polygon(pts, kind="Polygon%d" % n)
+
+
+CIRCLE_AABB_REF = [
+    (4.808976, (0.52343243, 0.38244677), (1.2948408, 1.4734308), (3.3397233, 6.3817973)),
+    (1.0, (1.0, 1.0), (-2.0, -2.0), (0.4, 0.7)),
+    (5.0, (0.0, 0.0), (-2.0, -2.0), (2.0, 2.0)),
+    (3.7427633, (-0.0277214, 1.0449156), (-0.6238362, -1.1297362), (1.3405488, -0.5544366)),
+    (0.5361439, (-0.4457733, 0.5882554), (-0.44587463, -0.73396504), (0.0717122, 3.0028129)),
+    (1.0, (0.0, 0.0), (-2.0, -2.0), (2.0, 2.0)),
+    (0.01, (0.0, 1.8), (-2.0, -2.0), (2.0, 2.0)),
+    (1.0, (0.1, 0.2), (-2.0, -2.3), (2.0, 2.0)),
+    (1.0, (-0.3, 0.05), (-2.1, -2.3), (2.0, 2.0)),
+    (1.0, (-0.12, -0.56), (-2.0, -2.0), (2.2, 2.3)),
+]
+
+
+def make_contacts():
+    rng = np.random.default_rng(2024)
+    cases = {}
+
+    def add(name, fn, pairs, func):
+        A, B, O, E = [], [], [], []
+        for a, b in pairs:
+            err = G.ErrorFlag()
+            pen, cp = func(a, b, err)
+            A.append(row(a))
+            B.append(row(b))
+            O.append([pen[0], pen[1], cp[0], cp[1]])
+            E.append(err.bits)
+        cases[name + "_a"] = np.array(A, F)
+        cases[name + "_b"] = np.array(B, F)
+        cases[name + "_out"] = np.array(O, F)
+        cases[name + "_err"] = np.array(E, np.int32)
+        cases[name + "_fn"] = np.array(fn, np.int32)
+
+    aa = [(rand_aabb(rng), rand_aabb(rng)) for _ in range(1500)]
+    # exact edge cases: touching faces (separated by <=), identical boxes
+    box = G.AABB((0.0, 0.0), (1.0, 1.0))
+    aa += [(box, G.AABB((1.0, 0.0), (2.0, 1.0))), (box, box), (box, G.AABB((0.5, 0.5), (0.75, 0.75))),
+           (G.AABB((F(np.nan), 0.0), (1.0, 1.0)), box)]
+    add("aabb_aabb", 0, aa, lambda a, b, e: G.aabb_vs_aabb(a, b, e))
+    cc = [(rand_circle(rng), rand_circle(rng)) for _ in range(1000)]
+    cc += [(G.Circle(1.0, (0.0, 0.0)), G.Circle(1.0, (0.0, 0.0))), (G.Circle(1.0, (0.0, 0.0)), G.Circle(0.5, (1.5, 0.0)))]
+    add("circle_circle", 1, cc, lambda a, b, e: G.circle_vs_circle(a, b, e))
+    ca = [(G.Circle(r, c), G.AABB(lo, up)) for r, c, lo, up in CIRCLE_AABB_REF]
+    ca += [(rand_circle(rng), rand_aabb(rng)) for _ in range(1500)]
+    # circle centre exactly on a corner (perfect_vertex) and far outside; NaN box (error_if trip)
+    ca += [(G.Circle(0.5, (1.0, 1.0)), box), (G.Circle(0.5, (3.0, 3.0)), box),
+           (G.Circle(0.5, (0.5, 0.5)), G.AABB((F(np.nan), 0.0), (1.0, 1.0)))]
+    add("circle_aabb", 2, ca, lambda a, b, e: G.circle_vs_aabb(a, b, e))
+    pp = []
+    for _ in range(400):
+        pp.append((rand_poly(rng, 4), rand_poly(rng, 6)))
+    for _ in range(300):
+        pp.append((rand_poly(rng, 4), rand_poly(rng, 4)))
+    for _ in range(150):
+        pp.append((rand_poly(rng, 3), rand_poly(rng, 5)))
+    for _ in range(100):
+        pp.append((rand_poly(rng, 6), rand_poly(rng, 6)))
+    p4 = rand_poly(rng, 4)
+    pp.append((p4, p4))  # self contact, as the collider's (2,2) cell does
+    add("poly_poly", 3, pp, lambda a, b, e: G.polygon_vs_polygon(a, b, D0, e))
+    ap = [(rand_aabb(rng, 0.6), rand_poly(rng, n)) for n in (4, 6, 5) for _ in range(150)]
+    add("aabb_poly", 4, ap, lambda a, b, e: G.aabb_vs_polygon(a, b, D0, e))
+    cp = [(G.Circle(F(rng.uniform(0.2, 1.5)), (F(rng.normal() * 0.7), F(rng.normal() * 0.7))), rand_poly(rng, n))
+          for n in (4, 6) for _ in range(60)]
+    add("circle_poly", 5, cp, lambda a, b, e: G.circle_vs_polygon(a, b, D0, e))
+    np.savez_compressed(os.path.join(HERE, "contacts.npz"), **cases)
+
+
+# ---------------------------------------------------------------------------
+# multi-step traces of the two scenarios
+# ---------------------------------------------------------------------------
+def robocup_perturb(B, seed=2):
+    """Oracle side of parallax_amd.scenarios.robocup_perturbation."""
+    keys = prng.split(prng.PRNGKey(seed), B)
+    out = []
+    for e in range(B):
+        kp, kv, kw = prng.split(keys[e], 3)
+        u = prng.uniform(kp, (2,))
+        lo = np.array([-4.4, -2.9], F)
+        hi = np.array([4.4, 2.9], F)
+        pos = np.maximum(lo, u * (hi - lo) + lo)
+        vel = prng.uniform(kv, (2,), -2.0, 2.0)
+        w = prng.uniform(kw, (), -10.0, 10.0)
+        out.append([pos[0], pos[1], vel[0], vel[1], F(0), F(w)])
+    out[0] = [F(0), F(0), F(1.0), F(0.01), F(0), F(10.0)]
+    return np.array(out, F)
+
+
+def trace(make_bodies, step_fn, keys, T, init=None):
+    B = len(keys)
+    dyn, ks, errs, chosen = [], [], [], []
+    envs = []
+    for e in range(B):
+        b = make_bodies(e)
+        if init is not None:
+            for i, d in enumerate(init[e]):
+                b[i].set_dyn(d)
+        envs.append(b)
+    cur = [np.array(k, np.uint32) for k in keys]
+    d_t = [[np.array([x.dyn() for x in envs[e]], F) for e in range(B)]]
+    k_t = [np.array(cur)]
+    for _ in range(T):
+        er_t, ch_t = [], []
+        for e in range(B):
+            err, tr = G.ErrorFlag(), {}
+            envs[e], cur[e] = step_fn(envs[e], cur[e], D0, err, tr)
+            er_t.append(err.bits)
+            ch_t.append(tr["chosen"])
+        d_t.append([np.array([x.dyn() for x in envs[e]], F) for e in range(B)])
+        k_t.append(np.array(cur))
+        errs.append(er_t)
+        chosen.append(ch_t)
+    return dict(dyn=np.array(d_t, F), keys=np.array(k_t, np.uint32), err=np.array(errs, np.int32),
+                chosen=np.array(chosen, np.int32))
+
+
+def make_robocup(B=8, T=12):
+    keys = prng.split(prng.PRNGKey(3), B)
+    pert = robocup_perturb(B)
+    init = []
+    for e in range(B):
+        d = [b.dyn() for b in P.robocup_bodies()]
+        d[4] = list(pert[e])
+        init.append(d)
+    tr = trace(lambda e: P.robocup_bodies(), P.robocup_step, keys, T, init)
+    np.savez_compressed(os.path.join(HERE, "robocup_trace.npz"), **tr)
+
+
+LL_DROP = [0.0, 6.0, 6.2, 6.4, 6.8, 7.5]
+
+
+def make_lunar(T=12):
+    B = len(LL_DROP)
+    tkeys = prng.split(prng.PRNGKey(0), B)
+    ckeys = prng.split(prng.PRNGKey(1), B)
+    init = []
+    for e in range(B):
+        d = [b.dyn() for b in P.lunar_lander_bodies(tkeys[e])]
+        for i in range(3):
+            d[i][1] = F(d[i][1] - F(LL_DROP[e]))
+            if e > 0:
+                d[i][3] = F(-0.3)  # falling: a resting contact has 0/0 drag (NaN) in the reference
+        init.append(d)
+    tr = trace(lambda e: P.lunar_lander_bodies(tkeys[e]), P.lunar_lander_step, ckeys, T, init)
+    tr["terrain_keys"] = np.array(tkeys, np.uint32)
+    tr["drop"] = np.array(LL_DROP, F)
+    tr["init"] = tr["dyn"][0]
+    np.savez_compressed(os.path.join(HERE, "lunar_trace.npz"), **tr)
+
+
+def box_world_bodies(e):
+    """A generic (non-reference) scene exercising every analytic contact with
+    finite outcomes: 3 static non-overlapping walls + 4 balls of finite mass."""
+    rng = np.random.default_rng(100 + e)
+    walls = [P.Body([G.AABB((-3.0, -3.2), (3.0, -2.0))], mass=np.inf, elasticity=0.8, friction_coefficient=0.3),
+             P.Body([G.AABB((-4.0, -1.9), (-3.0, 3.0))], mass=np.inf, elasticity=0.8, friction_coefficient=0.3),
+             P.Body([G.AABB((3.0, -1.9), (4.0, 3.0))], mass=np.inf, elasticity=0.8, friction_coefficient=0.3)]
+    balls = []
+    for k in range(4):
+        pos = (F(rng.uniform(-2.8, 2.8)), F(rng.uniform(-2.3, 1.0)))
+        vel = (F(rng.uniform(-3, 3)), F(rng.uniform(-3, 3)))
+        balls.append(P.Body([G.Circle(F(rng.uniform(0.3, 0.7)), (0.0, 0.0))], mass=F(rng.uniform(0.5, 2.0)),
+                            inertia=F(rng.uniform(0.2, 1.0)), position=pos, velocity=vel,
+                            angular_velocity=F(rng.uniform(-5, 5)), elasticity=F(rng.uniform(0.3, 1.0)),
+                            friction_coefficient=F(rng.uniform(0.1, 0.9))))
+    return walls + balls
+
+
+def box_world_step(bodies, key, d0, err=None, trace=None, dt=P.DT):
+    return P.robocup_step(bodies, key, d0, err, trace, dt)
+
+
+def make_box_world(B=6, T=40):
+    keys = prng.split(prng.PRNGKey(9), B)
+    tr = trace(box_world_bodies, box_world_step, keys, T)
+    np.savez_compressed(os.path.join(HERE, "box_world_trace.npz"), **tr)
+
+
+def make_prng():
+    rng = np.random.default_rng(5)
+    keys = rng.integers(0, 2 ** 32, size=(64, 2), dtype=np.uint64).astype(np.uint32)
+    ctr = rng.integers(0, 2 ** 32, size=(64, 2), dtype=np.uint64).astype(np.uint32)
+    blocks = np.array([np.concatenate(prng.threefry2x32(k, np.array([c[0]], np.uint32), np.array([c[1]], np.uint32)))
+                       for k, c in zip(keys, ctr)], np.uint32)
+    splits = np.array([prng.split(k, 5) for k in keys[:16]], np.uint32)
+    unif = np.array([prng.uniform(k, (7,), -3.0, 2.0) for k in keys[:16]], F)
+    unif1 = np.array([prng.uniform(k, (), 4.0, 8.0) for k in keys[:16]], F)
+    np.savez_compressed(os.path.join(HERE, "prng.npz"), keys=keys, ctr=ctr, blocks=blocks, splits=splits,
+                        uniform7=unif, uniform1=unif1)
+
+
+if __name__ == "__main__":
+    make_prng()
+    make_contacts()
+    make_robocup()
+    make_lunar()
+    make_box_world()
+    for f in sorted(os.listdir(HERE)):
+        print(f, os.path.getsize(os.path.join(HERE, f)))

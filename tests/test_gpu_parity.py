@@ -1,0 +1,314 @@
+"""GPU parity of the HIP hot path (through the C-ABI) against the oracle.
+
+Bar (DESIGN.md "Parity"): float32 results bit-identical to the oracle --
+equal bit patterns, and NaN exactly where the oracle has NaN (NaN payloads
+are not compared) -- plus identical error bits, keys and contact choices.
+This is stricter than north_star's 1e-5 relative tolerance.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def same_f32(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        return False
+    return np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+
+
+def diff_report(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    bad = ~((np.isnan(a) & np.isnan(b)) | (a.view(np.uint32) == b.view(np.uint32)))
+    idx = np.argwhere(bad)[:5]
+    return "first mismatches: " + "; ".join("%s: %r vs %r" % (tuple(i), a[tuple(i)], b[tuple(i)]) for i in idx)
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def u32_to_i32(x):
+    return np.asarray(x, np.uint32).view(np.int32)
+
+
+# ---------------------------------------------------------------------------
+# operators
+# ---------------------------------------------------------------------------
+def test_prng_kernels(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    g = np.load(os.path.join(GOLD, "prng.npz"))
+    keys = torch.tensor(u32_to_i32(g["keys"]), device="cuda")
+    ctr = torch.tensor(u32_to_i32(g["ctr"]), device="cuda")
+    out = pa.random.threefry2x32(keys, ctr).cpu().numpy().view(np.uint32)
+    assert np.array_equal(out, g["blocks"])
+    sp = pa.random.split(keys[:16], 5).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sp, g["splits"])
+    assert same_f32(pa.random.uniform(keys[:16], 7, -3.0, 2.0).cpu().numpy(), g["uniform7"])
+    assert same_f32(pa.random.uniform(keys[:16], None, 4.0, 8.0).cpu().numpy(), g["uniform1"])
+    # published: split(PRNGKey(0)) and uniform(PRNGKey(0), (3,))
+    k0 = pa.random.PRNGKey(0, "cuda")
+    assert pa.random.split(k0).cpu().numpy().view(np.uint32).tolist() == [[4146024105, 967050713],
+                                                                          [2718843009, 1272950319]]
+    assert same_f32(pa.random.uniform(k0, 3).cpu().numpy(), np.array([0.9653214, 0.31468165, 0.63302994], np.float32))
+
+
+@pytest.mark.parametrize("name", ["aabb_aabb", "circle_circle", "circle_aabb", "poly_poly", "aabb_poly",
+                                  "circle_poly"])
+def test_contact_operators(torch_cuda, name):
+    torch = torch_cuda
+    import parallax_amd as pa
+    g = np.load(os.path.join(GOLD, "contacts.npz"))
+    a = torch.tensor(g[name + "_a"], device="cuda")
+    b = torch.tensor(g[name + "_b"], device="cuda")
+    info, err = pa.run_contacts(int(g[name + "_fn"]), a, b)
+    got = torch.cat([info.penetration_vector, info.contact_point], 1).cpu().numpy()
+    assert same_f32(got, g[name + "_out"]), diff_report(got, g[name + "_out"])
+    assert np.array_equal(err.cpu().numpy(), g[name + "_err"])
+
+
+def test_resolve_operator(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import physics as P
+    rng = np.random.default_rng(3)
+    n = 400
+    d1 = rng.normal(size=(n, 6)).astype(np.float32)
+    d2 = rng.normal(size=(n, 6)).astype(np.float32)
+    p1 = np.abs(rng.normal(size=(n, 4))).astype(np.float32) + 0.1
+    p2 = np.abs(rng.normal(size=(n, 4))).astype(np.float32) + 0.1
+    p2[::7, 0] = np.inf  # static partner (mass inf) as in both scenarios
+    c = rng.normal(size=(n, 4)).astype(np.float32)
+    c[::11, 2] = np.nan  # no-contact rows are a no-op
+    want1, want2 = d1.copy(), d2.copy()
+    for k in range(n):
+        b1 = P.Body([], *p1[k, :2], elasticity=p1[k, 2], friction_coefficient=p1[k, 3])
+        b2 = P.Body([], *p2[k, :2], elasticity=p2[k, 2], friction_coefficient=p2[k, 3])
+        b1.set_dyn(d1[k])
+        b2.set_dyn(d2[k])
+        P.resolve_collision(b1, b2, ((c[k, 0], c[k, 1]), (c[k, 2], c[k, 3])))
+        want1[k], want2[k] = b1.dyn(), b2.dyn()
+    t1, t2 = torch.tensor(d1, device="cuda"), torch.tensor(d2, device="cuda")
+    pa.resolve_collision(t1, torch.tensor(p1, device="cuda"), t2, torch.tensor(p2, device="cuda"),
+                         torch.tensor(c, device="cuda"))
+    assert same_f32(t1.cpu().numpy(), want1), diff_report(t1.cpu().numpy(), want1)
+    assert same_f32(t2.cpu().numpy(), want2), diff_report(t2.cpu().numpy(), want2)
+
+
+def test_order_clockwise_operator(torch_cuda):
+    torch = torch_cuda
+    from cotix_oracle import geometry as G
+    import parallax_amd as pa
+    rng = np.random.default_rng(8)
+    for nv in (3, 4, 6, 8):
+        xy = rng.normal(size=(300, nv, 2)).astype(np.float32)
+        t = torch.tensor(xy, device="cuda")
+        pa._ffi.check(pa._ffi.lib.cotix_order_clockwise(pa._ffi.ptr(t), 300, nv, pa._ffi.stream_ptr()), "ocw")
+        want = np.array([G.order_clockwise([tuple(v) for v in p]) for p in xy], np.float32)
+        assert same_f32(t.cpu().numpy(), want)
+
+
+# ---------------------------------------------------------------------------
+# multi-step traces (fused kernel) vs the golden oracle traces
+# ---------------------------------------------------------------------------
+def _check_trace(world, tr, stages, T, per_step=True):
+    import torch
+    if per_step:
+        for t in range(T):
+            world.step(1, 1e-2, stages)
+            torch.cuda.synchronize()
+            dyn = world.dyn.permute(2, 0, 1).cpu().numpy()
+            assert same_f32(dyn, tr["dyn"][t + 1]), "step %d: %s" % (t, diff_report(dyn, tr["dyn"][t + 1]))
+            keys = world.keys.cpu().numpy().view(np.uint32)
+            assert np.array_equal(keys, tr["keys"][t + 1]), "step %d keys" % t
+            err = world.err.cpu().numpy()
+            want_err = np.bitwise_or.reduce(tr["err"][: t + 1], axis=0)
+            assert np.array_equal(err, want_err), "step %d err %s vs %s" % (t, err, want_err)
+    else:
+        world.step(T, 1e-2, stages)
+        torch.cuda.synchronize()
+        dyn = world.dyn.permute(2, 0, 1).cpu().numpy()
+        assert same_f32(dyn, tr["dyn"][T]), diff_report(dyn, tr["dyn"][T])
+        assert np.array_equal(world.keys.cpu().numpy().view(np.uint32), tr["keys"][T])
+
+
+@pytest.mark.parametrize("per_step", [True, False])
+def test_robocup_trace(torch_cuda, per_step):
+    torch = torch_cuda
+    import parallax_amd as pa
+    tr = np.load(os.path.join(GOLD, "robocup_trace.npz"))
+    T, B = tr["err"].shape
+    env = pa.RoboCupEnv(batch=B, device="cuda", keys=torch.tensor(u32_to_i32(tr["keys"][0]), device="cuda"),
+                        perturb=True)
+    assert same_f32(env.world.dyn.permute(2, 0, 1).cpu().numpy(), tr["dyn"][0]), "perturbed reset state"
+    _check_trace(env.world, tr, env.stages, T, per_step)
+
+
+@pytest.mark.parametrize("per_step", [True, False])
+def test_lunar_trace(torch_cuda, per_step):
+    torch = torch_cuda
+    import parallax_amd as pa
+    tr = np.load(os.path.join(GOLD, "lunar_trace.npz"))
+    T, B = tr["err"].shape
+    ll = pa.LunarLander(key=torch.tensor(u32_to_i32(tr["terrain_keys"]), device="cuda"), batch=B, device="cuda",
+                        collider_keys=torch.tensor(u32_to_i32(tr["keys"][0]), device="cuda"))
+    ll.world.dyn.copy_(torch.tensor(tr["init"], device="cuda").permute(1, 2, 0))
+    _check_trace(ll.world, tr, ll.stages, T, per_step)
+
+
+def test_lunar_terrain_matches_oracle(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    keys = prng.split(prng.PRNGKey(0), 16)
+    ll = pa.LunarLander(key=torch.tensor(u32_to_i32(keys), device="cuda"), batch=16, device="cuda")
+    geom = ll.world.geom.cpu().numpy()
+    for e in range(16):
+        ref = P.lunar_lander_bodies(keys[e])
+        want = np.concatenate([np.array(p.vertices_, np.float32).ravel() for b in ref for p in b.parts])
+        assert same_f32(geom[e], want), "env %d: %s" % (e, diff_report(geom[e], want))
+
+
+def test_box_world_trace(torch_cuda):
+    """Generic scene with finite dynamics (balls in a box)."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    sys_path = os.path.join(GOLD)
+    import sys
+    sys.path.insert(0, sys_path)
+    import make_golden as mg
+    tr = np.load(os.path.join(GOLD, "box_world_trace.npz"))
+    T, B = tr["err"].shape
+    for e in range(B):
+        ob = mg.box_world_bodies(e)
+        bodies = []
+        for b in ob:
+            parts = []
+            for p in b.parts:
+                if p.kind == "AABB":
+                    parts.append(pa.AABB(list(p.lower), list(p.upper)))
+                else:
+                    parts.append(pa.Circle(p.radius, list(p.position)))
+            bodies.append(pa.AnyBody(shape=pa.UniversalShape(*parts), mass=b.mass, inertia=b.inertia,
+                                     position=list(b.position), velocity=list(b.velocity), angle=b.angle,
+                                     angular_velocity=b.angular_velocity, elasticity=b.elasticity,
+                                     friction_coefficient=b.friction_coefficient))
+        w = pa.World(bodies, 1, "cuda", torch.tensor(u32_to_i32(tr["keys"][0][e:e + 1]), device="cuda"))
+        sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err")}
+        _check_trace(w, sub, pa._ffi.STAGES_ROBOCUP, T, per_step=True)
+
+
+# ---------------------------------------------------------------------------
+# operator composition == fused kernel (the reference's call sequence)
+# ---------------------------------------------------------------------------
+def test_operator_composition_matches_fused(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    tr = np.load(os.path.join(GOLD, "lunar_trace.npz"))
+    B = tr["err"].shape[1]
+    mk = lambda: pa.LunarLander(key=torch.tensor(u32_to_i32(tr["terrain_keys"]), device="cuda"),  # noqa: E731
+                                batch=B, device="cuda",
+                                collider_keys=torch.tensor(u32_to_i32(tr["keys"][0]), device="cuda"))
+    fused, ops = mk(), mk()
+    for x in (fused, ops):
+        x.world.dyn.copy_(torch.tensor(tr["init"], device="cuda").permute(1, 2, 0))
+    physics, collider = pa.ExplicitEulerPhysics(), pa.RandomizedCollider()
+    for t in range(6):
+        fused.world.step(1, 1e-2, fused.stages)
+        # examples/test_viz.py:24-44 composed from the operators
+        w, _ = physics.step(ops.world, dt=1e-2)
+        w.dyn[0, 3] += -0.002
+        w.dyn[0, 2] += 0.0
+        collider.resolve(w, w.keys)
+        w.keys.copy_(pa.random.split(w.keys)[:, 0])
+        ops.step()
+    torch.cuda.synchronize()
+    assert same_f32(ops.world.dyn.cpu().numpy(), fused.world.dyn.cpu().numpy())
+    assert torch.equal(ops.world.keys, fused.world.keys)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE sizes: 4096 envs -- sampled oracle parity + size-independent properties
+# ---------------------------------------------------------------------------
+def _oracle_envs(make_bodies, step_fn, init_dyn, keys, env_ids, T):
+    from cotix_oracle import geometry as G
+    from cotix_oracle import prng
+    d0 = prng.gjk_initial_direction()
+    out = []
+    for e in env_ids:
+        b = make_bodies(e)
+        for i in range(len(b)):
+            b[i].set_dyn(init_dyn[e][i])
+        k = np.array(keys[e], np.uint32)
+        err = G.ErrorFlag()
+        for _ in range(T):
+            b, k = step_fn(b, k, d0, err)
+        out.append((np.array([x.dyn() for x in b], np.float32), k, err.bits))
+    return out
+
+
+def test_robocup_4096_sampled_oracle_and_properties(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import physics as P
+    B, T = 4096, 6
+    env = pa.RoboCupEnv(batch=B, device="cuda", perturb=True)
+    init = env.world.dyn.permute(2, 0, 1).cpu().numpy().copy()
+    keys0 = env.world.keys.cpu().numpy().view(np.uint32).copy()
+    env.world.step(T, 1e-2, env.stages)
+    torch.cuda.synchronize()
+    dyn = env.world.dyn.permute(2, 0, 1).cpu().numpy()
+    err = env.world.err.cpu().numpy()
+    ids = [0, 1, 2, 777, 2048, 4095]
+    for e, (d, k, eb) in zip(ids, _oracle_envs(lambda e: P.robocup_bodies(), P.robocup_step, init, keys0, ids, T)):
+        assert same_f32(dyn[e], d), "env %d: %s" % (e, diff_report(dyn[e], d))
+        assert np.array_equal(env.world.keys[e].cpu().numpy().view(np.uint32), k)
+        assert err[e] == eb
+    # determinism + placement independence: the same envs, reversed order, in a fresh world
+    env2 = pa.RoboCupEnv(batch=B, device="cuda", keys=env.world.keys.new_tensor(keys0.view(np.int32)).flip(0))
+    env2.world.dyn.copy_(torch.tensor(init, device="cuda").flip(0).permute(1, 2, 0))
+    env2.world.step(T, 1e-2, env2.stages)
+    assert same_f32(env2.world.dyn.permute(2, 0, 1).flip(0).cpu().numpy(), dyn)
+    # fused T steps == T single-step launches
+    env3 = pa.RoboCupEnv(batch=B, device="cuda", perturb=True)
+    for _ in range(T):
+        env3.world.step(1, 1e-2, env3.stages)
+    assert same_f32(env3.world.dyn.cpu().numpy(), env.world.dyn.cpu().numpy())
+
+
+def test_lunar_4096_sampled_oracle(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    B, T = 4096, 4
+    tkeys = prng.split(prng.PRNGKey(0), B)
+    ll = pa.LunarLander(key=torch.tensor(u32_to_i32(tkeys), device="cuda"), batch=B, device="cuda")
+    # drop a quarter of the landers onto the ground so GJK/EPA contacts fire
+    drop = torch.zeros(B, device="cuda")
+    drop[::4] = 6.3
+    for i in range(3):
+        ll.world.dyn[i, 1] -= drop
+        ll.world.dyn[i, 3] = torch.where(drop > 0, torch.tensor(-0.3, device="cuda"), ll.world.dyn[i, 3])
+    init = ll.world.dyn.permute(2, 0, 1).cpu().numpy().copy()
+    keys0 = ll.world.keys.cpu().numpy().view(np.uint32).copy()
+    ll.world.step(T, 1e-2, ll.stages)
+    torch.cuda.synchronize()
+    dyn = ll.world.dyn.permute(2, 0, 1).cpu().numpy()
+    ids = [0, 4, 8, 1001, 2052, 4092, 4095]
+    res = _oracle_envs(lambda e: P.lunar_lander_bodies(tkeys[e]), P.lunar_lander_step, init, keys0, ids, T)
+    for e, (d, k, eb) in zip(ids, res):
+        assert same_f32(dyn[e], d), "env %d: %s" % (e, diff_report(dyn[e], d))

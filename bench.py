@@ -164,6 +164,18 @@ def main():
             "note": "VALU/latency-bound path (no dense contraction); HBM figure reported because north_star asks",
         },
     }
+    # HBM traffic per launch from the committed rocprofv3 PMC pass of the same
+    # workload (profiles/latest_pmc.json, tools/gpu_profile.sh); FETCH_SIZE
+    # doubled per MI355X_MICROARCH.md "HBM" (gfx950 reports half the bytes).
+    try:
+        pmc = json.load(open(os.path.join(ROOT, "profiles", "latest_pmc.json")))
+        c = pmc["config"]
+        if (c.get("envs_per_gpu") == B and c.get("substeps_per_launch") == a.substeps
+                and c.get("workload", "").split()[0] == out["config"]["workload"].split()[0]):
+            out["roofline"]["traffic"] = pmc["hbm_bytes_per_launch_corrected"]
+            out["roofline"]["traffic_source"] = "profiles/%s_summary.json" % pmc["tag"]
+    except (OSError, KeyError, ValueError):
+        pass
     if rank == 0 and a.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline(a.scenario, a.cpu_seconds)
     if rank == 0:

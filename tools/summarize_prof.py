@@ -1,0 +1,63 @@
+"""Summarize a tools/gpu_profile.sh run (gpurun_out/prof) into profiles/<tag>_*.
+
+Traffic per launch follows MI355X_MICROARCH.md "HBM": FETCH_SIZE/WRITE_SIZE are
+in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so
+the corrected figure doubles it (the guide calls other access widths
+uncalibrated: both raw and corrected values are recorded)."""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/prof"
+out = "profiles"
+K = "step_kernel"
+
+
+def pmc(d):
+    agg = defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(src, d, "run_counter_collection.csv"))):
+        if K in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+row = [r for r in stats if K in r["Name"]][0]
+avg_ns = float(row["AverageNs"])
+c = {}
+for d in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    c.update(pmc(d))
+bench = json.load(open(os.path.join(src, "trace_bench.json")))
+raw = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+corr = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+summary = {
+    "tag": tag,
+    "kernel": row["Name"],
+    "calls": int(row["Calls"]),
+    "avg_launch_ns": avg_ns,
+    "bench_event_launch_ms": bench["roofline"]["launch_ms"],
+    "bench_value": bench["value"],
+    "config": bench["config"],
+    "hbm_bytes_per_launch_raw": raw,
+    "hbm_bytes_per_launch_corrected": corr,
+    "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+    "counters_per_launch": c,
+    "valu_active_frac_of_wave_cycles": c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"],
+    "wait_frac_of_wave_cycles": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
+}
+os.makedirs(out, exist_ok=True)
+json.dump(summary, open(os.path.join(out, "%s_summary.json" % tag), "w"), indent=1)
+json.dump(summary, open(os.path.join(out, "latest_pmc.json"), "w"), indent=1)
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, "%s_kernel_stats.csv" % tag))
+for d in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    shutil.copy(os.path.join(src, d, "run_counter_collection.csv"), os.path.join(out, "%s_%s.csv" % (tag, d)))
+for f in os.listdir(src):
+    if f.startswith("sweep_"):
+        shutil.copy(os.path.join(src, f), os.path.join(out, "%s_%s" % (tag, f)))
+print(json.dumps({k: summary[k] for k in ("avg_launch_ns", "bench_event_launch_ms", "hbm_bytes_per_launch_raw",
+                                          "hbm_bytes_per_launch_corrected", "valu_active_frac_of_wave_cycles",
+                                          "wait_frac_of_wave_cycles")}, indent=1))

@@ -1,16 +1,17 @@
 // cotix_kernel.h -- the fused step as phase functions + the scene tables.
 //
-// Shared by the gfx950 kernel (cotix_step.hip: phases separated by
-// __syncthreads) and by the CPU emulation harness of the tests (tests/emu:
-// every phase run for all lanes in turn, under AddressSanitizer).
+// Shared by the gfx950 kernel (cotix_step.hip) and by the CPU emulation
+// harness of the tests (tests/emu: every phase run for all lanes of a wave in
+// turn, under AddressSanitizer).
 //
-// Design (DESIGN.md "Kernels"): one workgroup owns a tile of E environments
-// for all n_steps of a launch; the tile's state lives in LDS laid out
-// [word][env] (env fastest -> conflict-free, coalesced) and every phase of a
-// step is spread over the workgroup's lanes as (item, env) pairs with env
-// fastest, so the lanes of a wave run the same item (same contact function,
-// same cell) for consecutive envs:
-//   A  Euler (+gravity, +action), per-env key chain     (item = body)
+// Design (DESIGN.md "Kernels").  A workgroup is WPB independent waves; each
+// wave owns a tile of EW environments for all n_steps of a launch and syncs
+// only with itself (wave-local ordering, no workgroup barrier per phase), so
+// the serial phases of one wave overlap the other waves' work on the SIMD.
+// The tile's state lives in LDS laid out [word][env] (env fastest), next to
+// a per-workgroup LDS copy of the scene's hot tables.  Every phase is spread
+// over the wave's 64 lanes as (item, env) pairs with env fastest:
+//   A  Euler (+gravity, +action); per-env key chain     (item = body)
 //   T  part transforms + order_clockwise                  (item = part)
 //   B  distinct narrowphase contacts (+error bits)        (item = contact)
 //   C  per-cell "last passing candidate" RNG scan         (item = cell)
@@ -20,8 +21,9 @@
 // (cotix/_colliders.py:208-268) by an exact equivalent: for every cell
 // (i, j) only the LAST candidate (in scan order) whose contact is non-NaN
 // and whose bernoulli passes determines all_contacts[i, j], so each cell is
-// scanned backwards and stops at the first pass; duplicate contacts (the
-// same part pair repeated in the candidate lists) are evaluated once.
+// scanned backwards and stops at the first pass; a cell whose distinct
+// contacts are all NaN is skipped outright, and duplicate contacts (the same
+// part pair repeated in the candidate lists) are evaluated once.
 #pragma once
 #include "../../include/cotix_amd.h"
 #include "cotix_device.h"
@@ -29,17 +31,18 @@
 namespace cxk {
 
 constexpr int MAXB = 16, MAXP = 32, MAXC = 256, MAXL = 128, MAXT = 13, MAXCAND = 4096;
-constexpr int BLK = 256;
+constexpr int MAXHOT = 8192;
+constexpr int WAVE = 64;
 
+// Scene tables.  Everything the step reads per item is packed into hot[]
+// (word offsets below) and copied to LDS once per launch.
 struct SceneDev {
-  int nb, np, nc, nl, nt, G, W;  // bodies, parts, contacts, cells, types, geom floats, world floats
-  float d0x, d0y;                // GJK start direction (constant)
-  cx::Params par[MAXB];
-  int part_body[MAXP], part_kind[MAXP], part_n[MAXP], part_goff[MAXP], part_woff[MAXP];
-  int c_pa[MAXC], c_pb[MAXC], c_fn[MAXC];
-  int cell_i[MAXL], cell_j[MAXL], cell_beg[MAXL], cell_cnt[MAXL];
-  int type_n1[MAXT], type_n2[MAXT];
-  uint32_t cand[MAXCAND];
+  int nb, np, nc, nl, nt, G, W, ncand;  // bodies, parts, contacts, cells, types, geom/world floats, candidates
+  float d0x, d0y;                       // GJK start direction (constant)
+  int o_par, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
+  int o_ci, o_cj, o_cbeg, o_ccnt, o_dbeg, o_dcnt, o_tn1, o_tn2, o_cand, o_dist;
+  int nhot;
+  uint32_t hot[MAXHOT];
 };
 
 // kernel arguments (passed by value)
@@ -59,25 +62,31 @@ struct KArgs {
   int dbg_skip;            // debug only: bit k skips collider phase k (T=1,B=2,C=4,D=8)
 };
 
+// per-wave tile layout (words, each x EW envs)
 struct Lay {
-  int dyn, world, con, m, ch, key, sk0, skt, err, S;
+  int dyn, world, con, m, ch, key, sk0, skt, err, nres, S;
 };
-CX_DEV Lay layout(const SceneDev& s) {
+CX_DEV Lay layout(int nb, int W, int nc, int nt) {
   Lay L;
   L.dyn = 0;
-  L.world = L.dyn + s.nb * 6;
-  L.con = L.world + s.W;
-  L.m = L.con + s.nc * 4;
-  L.ch = L.m + s.nb * s.nb;
-  L.key = L.ch + s.nb;
+  L.world = L.dyn + nb * 6;
+  L.con = L.world + W;
+  L.m = L.con + nc * 4;
+  L.ch = L.m + nb * nb;
+  L.key = L.ch + nb;
   L.sk0 = L.key + 2;
   L.skt = L.sk0 + 2;
-  L.err = L.skt + 2 * s.nt;
-  L.S = L.err + 1;
+  L.err = L.skt + 2 * nt;
+  L.nres = L.err + 1;
+  L.S = L.nres + 1;
   return L;
 }
-static inline int lds_words(const SceneDev& s) {
-  return s.nb * 6 + s.W + s.nc * 4 + s.nb * s.nb + s.nb + 4 + 2 * s.nt + 1;
+static inline int tile_words(const SceneDev& s) {
+  return s.nb * 6 + s.W + s.nc * 4 + s.nb * s.nb + s.nb + 4 + 2 * s.nt + 2;
+}
+// LDS bytes of a workgroup of wpb waves x ew envs
+static inline size_t lds_bytes(const SceneDev& s, int wpb, int ew) {
+  return 4 * ((size_t)s.nhot + (size_t)tile_words(s) * ew * wpb);
 }
 
 CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, const cx::Params& pl,
@@ -132,36 +141,90 @@ CX_DEV cx::Contact run_contact_set(int fn, const cx::Shape& a, const cx::Shape& 
   return nan_contact();
 }
 
-// [word][env] LDS accessors
-template <int E>
+// jnp.cumsum via lax.associative_scan (CPU lowering), fully unrolled for a
+// compile-time length so the tree lives in registers.
+template <int N>
+CX_DEV void cumsum_fixed(const float* x, float* out) {
+  if constexpr (N < 2) {
+    if constexpr (N == 1) out[0] = x[0];
+  } else {
+    constexpr int M = N / 2;
+    float red[M], odd[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) red[k] = x[2 * k] + x[2 * k + 1];
+    cumsum_fixed<M>(red, odd);
+    constexpr int NE = (N % 2 == 0) ? M - 1 : M;
+    float even[M + 1];
+    even[0] = x[0];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) even[k + 1] = odd[k] + x[2 * k + 2];
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = (k % 2 == 0) ? even[k / 2] : odd[k / 2];
+  }
+}
+CX_DEV void cumsum_n(const float* x, int n, float* out) {
+  switch (n) {
+#define CXK_CS(k) \
+  case k:         \
+    cumsum_fixed<k>(x, out); \
+    break;
+    CXK_CS(1) CXK_CS(2) CXK_CS(3) CXK_CS(4) CXK_CS(5) CXK_CS(6) CXK_CS(7) CXK_CS(8)
+    CXK_CS(9) CXK_CS(10) CXK_CS(11) CXK_CS(12) CXK_CS(13) CXK_CS(14) CXK_CS(15) CXK_CS(16)
+#undef CXK_CS
+    default: break;
+  }
+}
+
+// wave-local ordering between phases: every lane's LDS traffic of the
+// previous phase is complete and visible to the wave before the next starts.
+CX_DEV void wave_sync() {
+#if defined(__HIP__) || defined(__HIPCC__)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
+
+// LDS views: scene hot tables + this wave's [word][env] tile
+template <int EW>
 struct Tile {
-  uint32_t* u;
-  CX_MF float& f(int off, int e) const { return reinterpret_cast<float*>(u)[off * E + e]; }
-  CX_MF uint32_t& w(int off, int e) const { return u[off * E + e]; }
+  uint32_t* u;          // tile base
+  const uint32_t* tb;   // hot tables
+  CX_MF float& f(int off, int e) const { return reinterpret_cast<float*>(u)[off * EW + e]; }
+  CX_MF uint32_t& w(int off, int e) const { return u[off * EW + e]; }
+  CX_MF int ti(int off) const { return (int)tb[off]; }
 };
 
-template <int E>
-CX_DEV void ph_load(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, int env0, int tid) {
-  for (int w = tid; w < sc.nb * 6 * E; w += BLK) {
-    int e = w % E, off = w / E, g = env0 + e;
-    t.f(L.dyn + off, e) = (g < a.B) ? a.dyn[(size_t)off * a.B + g] : 0.0f;
+struct Ctx {
+  int nb, np, nc, nl, nt;
+  const SceneDev* sc;
+  Lay L;
+};
+
+template <int EW>
+CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    int e = w % EW, off = w / EW, g = env0 + e;
+    t.f(c.L.dyn + off, e) = (g < a.B) ? a.dyn[(size_t)off * a.B + g] : 0.0f;
   }
-  for (int e = tid; e < E; e += BLK) {
+  for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
-    t.w(L.key, e) = (g < a.B) ? a.keys[2 * (size_t)g] : 0u;
-    t.w(L.key + 1, e) = (g < a.B) ? a.keys[2 * (size_t)g + 1] : 0u;
-    t.w(L.err, e) = (g < a.B) ? a.err[g] : 0u;
+    t.w(c.L.key, e) = (g < a.B) ? a.keys[2 * (size_t)g] : 0u;
+    t.w(c.L.key + 1, e) = (g < a.B) ? a.keys[2 * (size_t)g + 1] : 0u;
+    t.w(c.L.err, e) = (g < a.B) ? a.err[g] : 0u;
+    t.w(c.L.nres, e) = 0u;
   }
 }
 
 // phase A: Euler (cotix/_physics_solvers.py:16-33) + driver extras + key chain
-template <int E>
-CX_DEV void ph_A(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, int env0, int tid, int step) {
+template <int EW>
+CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   using namespace cx;
-  const int nb = sc.nb;
+  const int nb = c.nb;
+  const Lay& L = c.L;
   if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY)) {
-    for (int w = tid; w < nb * E; w += BLK) {
-      int e = w % E, b = w / E, g = env0 + e;
+    for (int w = lane; w < nb * EW; w += WAVE) {
+      int e = w % EW, b = w / EW, g = env0 + e;
       if (g >= a.B) continue;
       const int o = L.dyn + b * 6;
       if (a.stages & COTIX_STAGE_EULER) {
@@ -181,12 +244,12 @@ CX_DEV void ph_A(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, in
     }
   }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
-    for (int e = tid; e < E; e += BLK) {
+    for (int e = lane; e < EW; e += WAVE) {
       key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
       key2 s = split_at(k, 2u, 0u);  // cotix/_colliders.py:142 == next driver key
       t.w(L.sk0, e) = s.a;
       t.w(L.sk0 + 1, e) = s.b;
-      for (int q = 0; q < sc.nt; ++q) {  // :175, one split per type key
+      for (int q = 0; q < c.nt; ++q) {  // :175, one split per type key
         s = split_at(s, 2u, 0u);
         t.w(L.skt + 2 * q, e) = s.a;
         t.w(L.skt + 2 * q + 1, e) = s.b;
@@ -198,17 +261,18 @@ CX_DEV void ph_A(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, in
 }
 
 // phase T: shape.transform(body transformer) (cotix/_colliders.py:92-94)
-template <int E>
-CX_DEV void ph_T(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, int env0, int tid) {
+template <int EW, int FNSET>
+CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
-  for (int w = tid; w < sc.np * E; w += BLK) {
-    int e = w % E, p = w / E, g = env0 + e;
+  const SceneDev& sc = *c.sc;
+  for (int w = lane; w < c.np * EW; w += WAVE) {
+    int e = w % EW, p = w / EW, g = env0 + e;
     if (g >= a.B) continue;
-    const int b = sc.part_body[p], kind = sc.part_kind[p], n = sc.part_n[p];
-    const float* lg = a.geom + (a.gstride ? (size_t)g * a.gstride : (size_t)0) + sc.part_goff[p];
-    const int o = L.dyn + b * 6, wo = L.world + sc.part_woff[p];
+    const int b = t.ti(sc.o_pbody + p), kind = t.ti(sc.o_pkind + p);
+    const float* lg = a.geom + (a.gstride ? (size_t)g * a.gstride : (size_t)0) + t.ti(sc.o_pgoff + p);
+    const int o = c.L.dyn + b * 6, wo = c.L.world + t.ti(sc.o_pwoff + p);
     const float px = t.f(o + 0, e), py = t.f(o + 1, e);
-    if (kind != KIND_POLY) {
+    if (FNSET == FNS_ANALYTIC || kind != KIND_POLY) {
       // Circle (r, cx, cy, pad): translate only, cotix/_convex_shapes.py:37-41
       // AABB (lo.x, lo.y, up.x, up.y): translate only, :113-117
       // Branch-free on purpose: all four floats are loaded unconditionally
@@ -221,13 +285,14 @@ CX_DEV void ph_T(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, in
       t.f(wo + 2, e) = circ ? g2 + py : g2 + px;
       t.f(wo + 3, e) = circ ? g3 : g3 + py;
     } else {  // :181-187 forward_vector then re-sort (Polygon.__init__)
-      float s, c;
-      sincos32(t.f(o + 4, e), &s, &c);
+      const int n = t.ti(sc.o_pn + p);
+      float s, cs;
+      sincos32(t.f(o + 4, e), &s, &cs);
       float xy[2 * MAXV];
       for (int k = 0; k < n; ++k) {
         float x = lg[2 * k], y = lg[2 * k + 1];
-        float t0 = (c * x + (-s) * y) + px * 1.0f;
-        float t1 = (s * x + c * y) + py * 1.0f;
+        float t0 = (cs * x + (-s) * y) + px * 1.0f;
+        float t1 = (s * x + cs * y) + py * 1.0f;
         float t2 = (0.0f * x + 0.0f * y) + 1.0f * 1.0f;
         xy[2 * k] = t0 / t2;
         xy[2 * k + 1] = t1 / t2;
@@ -239,109 +304,151 @@ CX_DEV void ph_T(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, in
 }
 
 // phase B: distinct contacts (cotix/_colliders.py:149-173)
-template <int E, int FNSET>
-CX_DEV void ph_B(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, int env0, int tid) {
+template <int EW, int FNSET>
+CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
+  const SceneDev& sc = *c.sc;
   const v2 d0 = v2{sc.d0x, sc.d0y};
-  for (int w = tid; w < sc.nc * E; w += BLK) {
-    int e = w % E, c = w / E, g = env0 + e;
+  for (int w = lane; w < c.nc * EW; w += WAVE) {
+    int e = w % EW, ci = w / EW, g = env0 + e;
     if (g >= a.B) continue;
-    const int pa = sc.c_pa[c], pb = sc.c_pb[c];
+    const int pa = t.ti(sc.o_cpa + ci), pb = t.ti(sc.o_cpb + ci), fn = t.ti(sc.o_cfn + ci);
     Shape A, Bs;
-    A.kind = sc.part_kind[pa];
-    A.n = sc.part_n[pa];
-    Bs.kind = sc.part_kind[pb];
-    Bs.n = sc.part_n[pb];
-    const int na = A.kind == KIND_CIRCLE ? 3 : (A.kind == KIND_AABB ? 4 : 2 * A.n);
-    const int nbf = Bs.kind == KIND_CIRCLE ? 3 : (Bs.kind == KIND_AABB ? 4 : 2 * Bs.n);
-    for (int k = 0; k < na; ++k) A.d[k] = t.f(L.world + sc.part_woff[pa] + k, e);
-    for (int k = 0; k < nbf; ++k) Bs.d[k] = t.f(L.world + sc.part_woff[pb] + k, e);
+    A.kind = t.ti(sc.o_pkind + pa);
+    A.n = t.ti(sc.o_pn + pa);
+    Bs.kind = t.ti(sc.o_pkind + pb);
+    Bs.n = t.ti(sc.o_pn + pb);
+    const int wa = c.L.world + t.ti(sc.o_pwoff + pa), wb = c.L.world + t.ti(sc.o_pwoff + pb);
+    if (FNSET == FNS_ANALYTIC) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        A.d[k] = t.f(wa + k, e);
+        Bs.d[k] = t.f(wb + k, e);
+      }
+    } else {
+      const int na = A.kind == KIND_POLY ? 2 * A.n : 4;
+      const int nbf = Bs.kind == KIND_POLY ? 2 * Bs.n : 4;
+#pragma unroll
+      for (int k = 0; k < 2 * MAXV; ++k) {
+        A.d[k] = (k < na) ? t.f(wa + k, e) : 0.0f;
+        Bs.d[k] = (k < nbf) ? t.f(wb + k, e) : 0.0f;
+      }
+    }
     uint32_t er = 0u;
-    Contact ct = run_contact_set<FNSET>(sc.c_fn[c], A, Bs, d0, &er);
-    const int co = L.con + 4 * c;
+    Contact ct = run_contact_set<FNSET>(fn, A, Bs, d0, &er);
+    const int co = c.L.con + 4 * ci;
     t.f(co + 0, e) = ct.pen.x;
     t.f(co + 1, e) = ct.pen.y;
     t.f(co + 2, e) = ct.cp.x;
     t.f(co + 3, e) = ct.cp.y;
     if (er) {
 #if defined(__HIP__) || defined(__HIPCC__)
-      atomicOr(&t.w(L.err, e), er);
+      atomicOr(&t.w(c.L.err, e), er);
 #else
-      t.w(L.err, e) |= er;
+      t.w(c.L.err, e) |= er;
 #endif
     }
   }
 }
 
 // phase C: per cell, last passing candidate (cotix/_colliders.py:208-268)
-template <int E>
-CX_DEV void ph_C(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, int env0, int tid) {
+template <int EW>
+CX_DEV void ph_C(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
-  for (int w = tid; w < sc.nl * E; w += BLK) {
-    int e = w % E, l = w / E, g = env0 + e;
+  const SceneDev& sc = *c.sc;
+  const Lay& L = c.L;
+  for (int w = lane; w < c.nl * EW; w += WAVE) {
+    int e = w % EW, l = w / EW, g = env0 + e;
     if (g >= a.B) continue;
-    const int beg = sc.cell_beg[l], cnt = sc.cell_cnt[l];
-    int res = -1, lt = -1, li2 = -1;
-    key2 k2 = key2{0u, 0u};
-    for (int q = 0; q < cnt; ++q) {
-      const uint32_t cd = sc.cand[beg + q];
-      const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
+    int res = -1;
+    // fast path: a cell whose distinct contacts are all NaN never writes
+    const int dbeg = t.ti(sc.o_dbeg + l), dcnt = t.ti(sc.o_dcnt + l);
+    bool any = false;
+    for (int q = 0; q < dcnt; ++q) {
+      const int cid = t.ti(sc.o_dist + dbeg + q);
       const float cpx = t.f(L.con + 4 * cid + 2, e), cpy = t.f(L.con + 4 * cid + 3, e);
-      if (isn(cpx) || isn(cpy)) continue;  // a NaN candidate never writes
-      if (ty != lt || i2 != li2) {
-        key2 sk = key2{t.w(L.skt + 2 * ty, e), t.w(L.skt + 2 * ty + 1, e)};
-        k2 = split_at(sk, (uint32_t)sc.type_n2[ty], (uint32_t)i2);  // :264
-        lt = ty;
-        li2 = i2;
-      }
-      key2 k = split_at(k2, (uint32_t)sc.type_n1[ty], (uint32_t)i1);  // :254
-      key2 k1 = split_at(k, 2u, 0u);                                   // :222
-      if (bernoulli_half(k1)) {                                        // :223
-        res = cid;
-        break;
+      any = any || !(isn(cpx) || isn(cpy));
+    }
+    if (any) {
+      const int beg = t.ti(sc.o_cbeg + l), cnt = t.ti(sc.o_ccnt + l);
+      int lt = -1, li2 = -1;
+      key2 k2 = key2{0u, 0u};
+      for (int q = 0; q < cnt; ++q) {
+        const uint32_t cd = t.tb[sc.o_cand + beg + q];
+        const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
+        const float cpx = t.f(L.con + 4 * cid + 2, e), cpy = t.f(L.con + 4 * cid + 3, e);
+        if (isn(cpx) || isn(cpy)) continue;  // a NaN candidate never writes
+        if (ty != lt || i2 != li2) {
+          key2 sk = key2{t.w(L.skt + 2 * ty, e), t.w(L.skt + 2 * ty + 1, e)};
+          k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
+          lt = ty;
+          li2 = i2;
+        }
+        key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);  // :254
+        key2 k1 = split_at(k, 2u, 0u);                                        // :222
+        if (bernoulli_half(k1)) {                                             // :223
+          res = cid;
+          break;
+        }
       }
     }
-    t.w(L.m + sc.cell_i[l] * sc.nb + sc.cell_j[l], e) = (uint32_t)res;
+    t.w(L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = (uint32_t)res;
   }
 }
 
 // phase D: choose_random_contact (cotix/_colliders.py:274-295)
-template <int E>
-CX_DEV void ph_D(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, int env0, int tid) {
+template <int EW>
+CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
-  const int nb = sc.nb, nt = sc.nt;
-  for (int w = tid; w < nb * E; w += BLK) {
-    int e = w % E, i = w / E, g = env0 + e;
+  const int nb = c.nb, nt = c.nt;
+  const Lay& L = c.L;
+  for (int w = lane; w < nb * EW; w += WAVE) {
+    int e = w % EW, i = w / EW, g = env0 + e;
     if (g >= a.B) continue;
     int cnt = 0;
-    for (int j = 0; j < nb; ++j) cnt += ((int)t.w(L.m + i * nb + j, e) >= 0) ? 1 : 0;
+    uint32_t good = 0u;
+    for (int j = 0; j < nb; ++j)
+      if ((int)t.w(L.m + i * nb + j, e) >= 0) {
+        good |= 1u << j;
+        ++cnt;
+      }
     int ch = i;
     if (cnt > 0) {
-      float p[MAXB], c[MAXB];
+      float p[MAXB], cs[MAXB];
       const float fc = (float)cnt;
-      for (int j = 0; j < nb; ++j) p[j] = (((int)t.w(L.m + i * nb + j, e) >= 0) ? 1.0f : 0.0f) / fc;
-      cumsum_assoc(p, nb, c);
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j) p[j] = (((good >> j) & 1u) ? 1.0f : 0.0f) / fc;
+      cumsum_n(p, nb, cs);
       const int so = nt > 0 ? L.skt + 2 * (nt - 1) : L.sk0;
       key2 ck = split_at(key2{t.w(so, e), t.w(so + 1, e)}, (uint32_t)nb, (uint32_t)i);
       float u = unit_float(bits1(ck));
-      float r = c[nb - 1] * (1.0f - u);
+      float last = cs[0];
+#pragma unroll
+      for (int j = 1; j < MAXB; ++j)
+        if (j < nb) last = cs[j];
+      float r = last * (1.0f - u);
       ch = nb;
-      for (int j = 0; j < nb; ++j)
-        if (!(c[j] < r)) {
-          ch = j;
-          break;
-        }
+#pragma unroll
+      for (int j = MAXB - 1; j >= 0; --j)
+        if (j < nb && !(cs[j] < r)) ch = j;  // first j with r <= cumsum[j]
     }
     t.w(L.ch + i, e) = (uint32_t)ch;
   }
 }
 
+CX_DEV cx::Params load_par(const uint32_t* tb, int o) {
+  return cx::Params{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1]), __uint_as_float(tb[o + 2]),
+                    __uint_as_float(tb[o + 3])};
+}
+
 // phase E: sequential resolution (:310-336), joints, key update, restarts
-template <int E>
-CX_DEV void ph_E(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, int env0, int tid) {
+template <int EW>
+CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
-  const int nb = sc.nb;
-  for (int e = tid; e < E; e += BLK) {
+  const SceneDev& sc = *c.sc;
+  const int nb = c.nb;
+  const Lay& L = c.L;
+  for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g >= a.B) continue;
     if (a.stages & COTIX_STAGE_COLLIDER) {
@@ -353,8 +460,8 @@ CX_DEV void ph_E(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, in
         const int co = L.con + 4 * cid, oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
         Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), t.f(oi + 2, e), t.f(oi + 3, e), t.f(oi + 4, e), t.f(oi + 5, e)};
         Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), t.f(oj + 2, e), t.f(oj + 3, e), t.f(oj + 4, e), t.f(oj + 5, e)};
-        resolve_collision(bi, sc.par[i], bj, sc.par[j], v2{t.f(co, e), t.f(co + 1, e)},
-                          v2{t.f(co + 2, e), t.f(co + 3, e)});
+        resolve_collision(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
+                          v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)});
         t.f(oi + 2, e) = bi.vx;
         t.f(oi + 3, e) = bi.vy;
         t.f(oi + 5, e) = bi.w;
@@ -365,11 +472,14 @@ CX_DEV void ph_E(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, in
     }
     if ((a.stages & COTIX_STAGE_LUNAR) && nb >= 3) {
       Dyn d[3];
+#pragma unroll
       for (int b = 0; b < 3; ++b) {
         const int o = L.dyn + 6 * b;
         d[b] = Dyn{t.f(o, e), t.f(o + 1, e), t.f(o + 2, e), t.f(o + 3, e), t.f(o + 4, e), t.f(o + 5, e)};
       }
-      lunar_constraints(d[0], d[1], d[2], sc.par[0], sc.par[1], sc.par[2]);
+      lunar_constraints(d[0], d[1], d[2], load_par(t.tb, sc.o_par), load_par(t.tb, sc.o_par + 4),
+                        load_par(t.tb, sc.o_par + 8));
+#pragma unroll
       for (int b = 0; b < 3; ++b) {
         const int o = L.dyn + 6 * b;
         t.f(o + 2, e) = d[b].vx;
@@ -386,25 +496,50 @@ CX_DEV void ph_E(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, in
       // the env from its reset state; the key chain continues.
       for (int off = 0; off < nb * 6; ++off) t.f(L.dyn + off, e) = a.dyn_reset[(size_t)off * a.B + g];
       t.w(L.err, e) = 0u;
-      if (a.resets) a.resets[g] += 1u;
+      t.w(L.nres, e) = t.w(L.nres, e) + 1u;
     }
   }
 }
 
-template <int E>
-CX_DEV void ph_store(const KArgs& a, const SceneDev& sc, const Lay& L, Tile<E> t, int env0, int tid) {
-  for (int w = tid; w < sc.nb * 6 * E; w += BLK) {
-    int e = w % E, off = w / E, g = env0 + e;
-    if (g < a.B) a.dyn[(size_t)off * a.B + g] = t.f(L.dyn + off, e);
+template <int EW>
+CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    int e = w % EW, off = w / EW, g = env0 + e;
+    if (g < a.B) a.dyn[(size_t)off * a.B + g] = t.f(c.L.dyn + off, e);
   }
-  for (int e = tid; e < E; e += BLK) {
+  for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g < a.B) {
-      a.keys[2 * (size_t)g] = t.w(L.key, e);
-      a.keys[2 * (size_t)g + 1] = t.w(L.key + 1, e);
-      a.err[g] = t.w(L.err, e);
+      a.keys[2 * (size_t)g] = t.w(c.L.key, e);
+      a.keys[2 * (size_t)g + 1] = t.w(c.L.key + 1, e);
+      a.err[g] = t.w(c.L.err, e);
+      if (a.resets) a.resets[g] += t.w(c.L.nres, e);
     }
   }
+}
+
+// the whole launch for one wave (lane = 0..63), after the hot tables are in LDS
+template <int EW, int FNSET>
+CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  ph_load<EW>(a, c, t, env0, lane);
+  wave_sync();
+  for (int step = 0; step < a.n_steps; ++step) {
+    ph_A<EW>(a, c, t, env0, lane, step);
+    wave_sync();
+    if (a.stages & COTIX_STAGE_COLLIDER) {
+      if (!(a.dbg_skip & 1)) ph_T<EW, FNSET>(a, c, t, env0, lane);
+      wave_sync();
+      if (!(a.dbg_skip & 2)) ph_B<EW, FNSET>(a, c, t, env0, lane);
+      wave_sync();
+      if (!(a.dbg_skip & 4)) ph_C<EW>(a, c, t, env0, lane);
+      wave_sync();
+      if (!(a.dbg_skip & 8)) ph_D<EW>(a, c, t, env0, lane);
+      wave_sync();
+    }
+    ph_E<EW>(a, c, t, env0, lane);
+    wave_sync();
+  }
+  ph_store<EW>(a, c, t, env0, lane);
 }
 
 }  // namespace cxk

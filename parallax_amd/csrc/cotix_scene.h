@@ -50,32 +50,32 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   uint32_t bx = 0xbd56c50bu, by = 0x3f7fa5d9u;
   std::memcpy(&s.d0x, &bx, 4);
   std::memcpy(&s.d0y, &by, 4);
-  for (int b = 0; b < n_bodies; ++b)
-    s.par[b] = cx::Params{body_params[4 * b], body_params[4 * b + 1], body_params[4 * b + 2], body_params[4 * b + 3]};
+  std::vector<int> part_bodyv(n_parts), part_kindv(n_parts), part_nv(n_parts), part_goffv(n_parts),
+      part_woffv(n_parts);
   std::vector<std::vector<int>> parts_of(n_bodies);
   int goff = 0, woff = 0;
   for (int p = 0; p < n_parts; ++p) {
     int b = part_body[p], t = part_type[p];
     if (b < 0 || b >= n_bodies) return scene_fail(err, "part_body out of range");
     if (p > 0 && b < part_body[p - 1]) return scene_fail(err, "parts must be grouped by body in body order");
-    s.part_body[p] = b;
+    part_bodyv[p] = b;
     if (t == COTIX_CIRCLE) {
-      s.part_kind[p] = cx::KIND_CIRCLE;
-      s.part_n[p] = 0;
+      part_kindv[p] = cx::KIND_CIRCLE;
+      part_nv[p] = 0;
     } else if (t == COTIX_AABB) {
-      s.part_kind[p] = cx::KIND_AABB;
-      s.part_n[p] = 0;
+      part_kindv[p] = cx::KIND_AABB;
+      part_nv[p] = 0;
     } else if (t >= COTIX_POLYGON && t <= COTIX_POLYGON6) {
       int n = (t == COTIX_POLYGON) ? (part_nverts ? part_nverts[p] : 0) : t;
       if (n < 3 || n > cx::MAXV) return scene_fail(err, "polygon vertex count must be 3..8");
-      s.part_kind[p] = cx::KIND_POLY;
-      s.part_n[p] = n;
+      part_kindv[p] = cx::KIND_POLY;
+      part_nv[p] = n;
     } else {
       return scene_fail(err, "unknown part type");
     }
-    int nf = s.part_kind[p] == cx::KIND_CIRCLE ? 4 : (s.part_kind[p] == cx::KIND_AABB ? 4 : 2 * s.part_n[p]);
-    s.part_goff[p] = goff;
-    s.part_woff[p] = woff;
+    int nf = part_kindv[p] == cx::KIND_CIRCLE ? 4 : (part_kindv[p] == cx::KIND_AABB ? 4 : 2 * part_nv[p]);
+    part_goffv[p] = goff;
+    part_woffv[p] = woff;
     goff += nf;
     woff += nf;
     parts_of[b].push_back(p);
@@ -122,11 +122,12 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
     return c;
   };
   std::vector<std::tuple<int, int, int>> clist;
+  std::vector<int> tn1(s.nt), tn2(s.nt);
   for (int k = 0; k < s.nt; ++k) {
     int N1 = (int)l1[k].size(), N2 = (int)l2[k].size();
     if (N1 > 511 || N2 > 511) return scene_fail(err, "candidate list longer than 511");
-    s.type_n1[k] = N1;
-    s.type_n2[k] = N2;
+    tn1[k] = N1;
+    tn2[k] = N2;
     int fn = registry_fn(tkeys[k].first, tkeys[k].second);
     for (int i2 = 0; i2 < N2; ++i2)
       for (int i1 = 0; i1 < N1; ++i1) {
@@ -146,29 +147,77 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   }
   if ((int)clist.size() > MAXC || (int)clist.size() > 511) return scene_fail(err, "too many distinct contacts");
   s.nc = (int)clist.size();
-  for (int c = 0; c < s.nc; ++c) {
-    s.c_pa[c] = std::get<0>(clist[c]);
-    s.c_pb[c] = std::get<1>(clist[c]);
-    s.c_fn[c] = std::get<2>(clist[c]);
-  }
   if ((int)cells.size() > MAXL) return scene_fail(err, "too many cells");
   s.nl = (int)cells.size();
-  int nc_tot = 0, l = 0;
+  // pack the hot tables (word offsets into s.hot, copied to LDS per launch)
+  std::vector<uint32_t> hot;
+  auto put = [&](int& off, const std::vector<int>& v) {
+    off = (int)hot.size();
+    for (int x : v) hot.push_back((uint32_t)x);
+  };
+  {
+    s.o_par = (int)hot.size();
+    for (int q = 0; q < 4 * n_bodies; ++q) {
+      uint32_t u;
+      std::memcpy(&u, &body_params[q], 4);
+      hot.push_back(u);
+    }
+  }
+  put(s.o_pbody, part_bodyv);
+  put(s.o_pkind, part_kindv);
+  put(s.o_pn, part_nv);
+  put(s.o_pgoff, part_goffv);
+  put(s.o_pwoff, part_woffv);
+  std::vector<int> cpa(s.nc), cpb(s.nc), cfn(s.nc);
+  for (int c = 0; c < s.nc; ++c) {
+    cpa[c] = std::get<0>(clist[c]);
+    cpb[c] = std::get<1>(clist[c]);
+    cfn[c] = std::get<2>(clist[c]);
+  }
+  put(s.o_cpa, cpa);
+  put(s.o_cpb, cpb);
+  put(s.o_cfn, cfn);
+  std::vector<int> ci, cj, cbeg, ccnt, dbeg, dcnt, dist;
+  std::vector<int> candv;
   for (auto& ck : cell_order) {
     auto& v = cells[ck];
-    s.cell_i[l] = ck.first;
-    s.cell_j[l] = ck.second;
-    s.cell_beg[l] = nc_tot;
-    s.cell_cnt[l] = (int)v.size();
-    if (nc_tot + (int)v.size() > MAXCAND) return scene_fail(err, "too many candidates");
+    ci.push_back(ck.first);
+    cj.push_back(ck.second);
+    cbeg.push_back((int)candv.size());
+    ccnt.push_back((int)v.size());
     // types ascend, then (ind2, ind1) ascend in v: reverse = last write first
-    for (int q = (int)v.size() - 1; q >= 0; --q) s.cand[nc_tot++] = v[q];
-    ++l;
+    for (int q = (int)v.size() - 1; q >= 0; --q) candv.push_back((int)v[q]);
+    std::vector<int> d;
+    for (uint32_t cd : v) {
+      int c = (int)((cd >> 18) & 511u);
+      bool seen = false;
+      for (int x : d) seen = seen || x == c;
+      if (!seen) d.push_back(c);
+    }
+    dbeg.push_back((int)dist.size());
+    dcnt.push_back((int)d.size());
+    for (int x : d) dist.push_back(x);
   }
+  if ((int)candv.size() > MAXCAND) return scene_fail(err, "too many candidates");
+  put(s.o_ci, ci);
+  put(s.o_cj, cj);
+  put(s.o_cbeg, cbeg);
+  put(s.o_ccnt, ccnt);
+  put(s.o_dbeg, dbeg);
+  put(s.o_dcnt, dcnt);
+  put(s.o_tn1, tn1);
+  put(s.o_tn2, tn2);
+  put(s.o_cand, candv);
+  put(s.o_dist, dist);
+  if ((int)hot.size() > MAXHOT) return scene_fail(err, "scene tables too large");
+  s.nhot = (int)hot.size();
+  for (size_t q = 0; q < hot.size(); ++q) s.hot[q] = hot[q];
+  s.ncand = (int)candv.size();
+  int nc_tot = s.ncand;
   n_cand = nc_tot;
   fnset = 0;
   for (int c = 0; c < s.nc; ++c) {
-    int fn = s.c_fn[c];
+    int fn = cfn[c];
     fnset |= (fn == cx::FN_AABB_AABB || fn == cx::FN_CIRCLE_AABB || fn == cx::FN_CIRCLE_CIRCLE) ? FNS_ANALYTIC
              : (fn == cx::FN_CIRCLE_POLY ? FNS_CIRCLE_POLY : FNS_CONVEX);
   }

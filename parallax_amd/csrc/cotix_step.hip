@@ -13,7 +13,6 @@
 #include "cotix_kernel.h"
 #include "cotix_scene.h"
 
-using cxk::BLK;
 using cxk::FNS_ANALYTIC;
 using cxk::FNS_CIRCLE_POLY;
 using cxk::FNS_CONVEX;
@@ -41,34 +40,22 @@ struct cotix_scene {
 namespace {
 
 // ---------------------------------------------------------------------------
-// the fused step kernel: one workgroup = one tile of E envs, all n_steps
+// the fused step kernel: WPB independent waves per workgroup, EW envs per wave
 // ---------------------------------------------------------------------------
-template <int E, int FNSET>
-__global__ __launch_bounds__(BLK) void step_kernel(cxk::KArgs a) {
+constexpr int WPB = 4;
+template <int EW, int FNSET>
+__global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   extern __shared__ uint32_t lds[];
-  const SceneDev& sc = *a.sc;
-  const cxk::Lay L = cxk::layout(sc);
-  const cxk::Tile<E> t{lds};
-  const int tid = threadIdx.x, env0 = blockIdx.x * E;
-  cxk::ph_load<E>(a, sc, L, t, env0, tid);
+  const SceneDev* sc = a.sc;
+  const int nhot = sc->nhot;
+  for (int i = threadIdx.x; i < nhot; i += WPB * 64) lds[i] = sc->hot[i];
   __syncthreads();
-  for (int step = 0; step < a.n_steps; ++step) {
-    cxk::ph_A<E>(a, sc, L, t, env0, tid, step);
-    __syncthreads();
-    if (a.stages & COTIX_STAGE_COLLIDER) {
-      if (!(a.dbg_skip & 1)) cxk::ph_T<E>(a, sc, L, t, env0, tid);
-      __syncthreads();
-      if (!(a.dbg_skip & 2)) cxk::ph_B<E, FNSET>(a, sc, L, t, env0, tid);
-      __syncthreads();
-      if (!(a.dbg_skip & 4)) cxk::ph_C<E>(a, sc, L, t, env0, tid);
-      __syncthreads();
-      if (!(a.dbg_skip & 8)) cxk::ph_D<E>(a, sc, L, t, env0, tid);
-      __syncthreads();
-    }
-    cxk::ph_E<E>(a, sc, L, t, env0, tid);
-    __syncthreads();
-  }
-  cxk::ph_store<E>(a, sc, L, t, env0, tid);
+  const cxk::Ctx c{sc->nb, sc->np, sc->nc, sc->nl, sc->nt, sc, cxk::layout(sc->nb, sc->W, sc->nc, sc->nt)};
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int env0 = (blockIdx.x * WPB + wave) * EW;
+  if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
+  const cxk::Tile<EW> t{lds + nhot + wave * c.L.S * EW, lds};
+  cxk::run_wave<EW, FNSET>(a, c, t, env0, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -215,10 +202,10 @@ static int scene_upload(cotix_scene* sc) {
   return hip_check(hipMemcpy(sc->dev, &sc->host, sizeof(SceneDev), hipMemcpyHostToDevice), "hipMemcpy(scene)");
 }
 
-static int envs_per_block() {
-  const char* v = getenv("COTIX_ENVS_PER_BLOCK");
-  int e = v ? atoi(v) : 16;
-  return (e == 8 || e == 16 || e == 32) ? e : 16;
+static int envs_per_wave() {
+  const char* v = getenv("COTIX_ENVS_PER_WAVE");
+  int e = v ? atoi(v) : 4;  // measured best for both scenarios (profiles/r01_sweep_*)
+  return (e == 1 || e == 2 || e == 4 || e == 8) ? e : 4;
 }
 
 static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
@@ -231,10 +218,10 @@ static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* e
   if ((stages & COTIX_STAGE_LUNAR) && scene->host.nb < 3) return fail("LunarLander stage needs >= 3 bodies");
   if (action && (action_body < 0 || action_body >= scene->host.nb)) return fail("action_body out of range");
   if (scene_upload(scene)) return -1;
-  const int E = envs_per_block();
-  const size_t lds = (size_t)cxk::lds_words(scene->host) * E * 4;
+  const int EW = envs_per_wave();
+  const size_t lds = cxk::lds_bytes(scene->host, WPB, EW);
   if (lds > 160 * 1024) return fail("scene too large for the LDS tile");
-  dim3 grid((B + E - 1) / E), block(BLK);
+  dim3 grid((B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const char* dbg = getenv("COTIX_DEBUG_SKIP");
   cxk::KArgs ka{scene->dev, dyn,    keys,        err,       geom,   geom_stride,          B, n_steps, dt, stages,
@@ -242,9 +229,10 @@ static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* e
   const int fs = scene->fnset;
 #define COTIX_LAUNCH(EE, FS) hipLaunchKernelGGL((step_kernel<EE, FS>), grid, block, lds, st, ka)
 #define COTIX_LAUNCH_E(FS)                \
-  if (E == 8) COTIX_LAUNCH(8, FS);        \
-  else if (E == 32) COTIX_LAUNCH(32, FS); \
-  else COTIX_LAUNCH(16, FS);
+  if (EW == 1) COTIX_LAUNCH(1, FS);       \
+  else if (EW == 8) COTIX_LAUNCH(8, FS);  \
+  else if (EW == 2) COTIX_LAUNCH(2, FS);  \
+  else COTIX_LAUNCH(4, FS);
   if ((fs & ~FNS_ANALYTIC) == 0) {
     COTIX_LAUNCH_E(FNS_ANALYTIC)
   } else if ((fs & FNS_CIRCLE_POLY) == 0) {

@@ -20,29 +20,32 @@ struct EmuScene {
   int n_cand = 0, fnset = 0;
 };
 
-template <int E>
+// one wave at a time (waves are independent); within a wave every phase
+// runs for all 64 lanes before the next (what wave_sync() guarantees)
+template <int EW>
 void run_blocks(const cxk::KArgs& a) {
   const cxk::SceneDev& sc = *a.sc;
-  const cxk::Lay L = cxk::layout(sc);
-  const int nblk = (a.B + E - 1) / E;
-  std::vector<uint32_t> lds((size_t)cxk::lds_words(sc) * E);
-  const int BLK = cxk::BLK;
-  for (int b = 0; b < nblk; ++b) {
-    std::fill(lds.begin(), lds.end(), 0x7FBADBADu);  // poison (a NaN pattern)
-    const cxk::Tile<E> t{lds.data()};
-    const int env0 = b * E;
-    for (int tid = 0; tid < BLK; ++tid) cxk::ph_load<E>(a, sc, L, t, env0, tid);
+  const cxk::Ctx c{sc.nb, sc.np, sc.nc, sc.nl, sc.nt, &sc, cxk::layout(sc.nb, sc.W, sc.nc, sc.nt)};
+  const int nwaves = (a.B + EW - 1) / EW;
+  std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)c.L.S * EW);
+  for (int q = 0; q < sc.nhot; ++q) lds[q] = sc.hot[q];
+  const int W = cxk::WAVE;
+  for (int wv = 0; wv < nwaves; ++wv) {
+    std::fill(lds.begin() + sc.nhot, lds.end(), 0x7FBADBADu);  // poison (a NaN pattern)
+    const cxk::Tile<EW> t{lds.data() + sc.nhot, lds.data()};
+    const int env0 = wv * EW;
+    for (int l = 0; l < W; ++l) cxk::ph_load<EW>(a, c, t, env0, l);
     for (int step = 0; step < a.n_steps; ++step) {
-      for (int tid = 0; tid < BLK; ++tid) cxk::ph_A<E>(a, sc, L, t, env0, tid, step);
+      for (int l = 0; l < W; ++l) cxk::ph_A<EW>(a, c, t, env0, l, step);
       if (a.stages & COTIX_STAGE_COLLIDER) {
-        for (int tid = 0; tid < BLK; ++tid) cxk::ph_T<E>(a, sc, L, t, env0, tid);
-        for (int tid = 0; tid < BLK; ++tid) cxk::ph_B<E, 7>(a, sc, L, t, env0, tid);
-        for (int tid = 0; tid < BLK; ++tid) cxk::ph_C<E>(a, sc, L, t, env0, tid);
-        for (int tid = 0; tid < BLK; ++tid) cxk::ph_D<E>(a, sc, L, t, env0, tid);
+        for (int l = 0; l < W; ++l) cxk::ph_T<EW, 7>(a, c, t, env0, l);
+        for (int l = 0; l < W; ++l) cxk::ph_B<EW, 7>(a, c, t, env0, l);
+        for (int l = 0; l < W; ++l) cxk::ph_C<EW>(a, c, t, env0, l);
+        for (int l = 0; l < W; ++l) cxk::ph_D<EW>(a, c, t, env0, l);
       }
-      for (int tid = 0; tid < BLK; ++tid) cxk::ph_E<E>(a, sc, L, t, env0, tid);
+      for (int l = 0; l < W; ++l) cxk::ph_E<EW>(a, c, t, env0, l);
     }
-    for (int tid = 0; tid < BLK; ++tid) cxk::ph_store<E>(a, sc, L, t, env0, tid);
+    for (int l = 0; l < W; ++l) cxk::ph_store<EW>(a, c, t, env0, l);
   }
 }
 }  // namespace
@@ -72,9 +75,10 @@ int emu_step(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float
              uint32_t* resets, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
   cxk::KArgs a{&s->s, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, action, action_body, dyn_reset, resets, 0};
-  if (E == 8) run_blocks<8>(a);
-  else if (E == 32) run_blocks<32>(a);
-  else run_blocks<16>(a);
+  if (E == 1) run_blocks<1>(a);
+  else if (E == 4) run_blocks<4>(a);
+  else if (E == 8) run_blocks<8>(a);
+  else run_blocks<2>(a);
   return 0;
 }
 

@@ -1,0 +1,123 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes front-end of the C port of the oracle
+(oracle/c/cotix_oracle.c, built by `make -C oracle`).  Used by the tests as
+a fast checker and by bench.py as the timed CPU baseline ("kind": "port")."""
+import ctypes
+import os
+import time
+
+import numpy as np
+
+from . import physics as P
+from . import prng
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "..", "build", "libcotix_oracle.so")
+_P = ctypes.c_void_p
+TYPE_ID = {"Circle": 0, "AABB": 1, "Polygon": 2, "Polygon3": 3, "Polygon4": 4, "Polygon5": 5, "Polygon6": 6}
+STAGES_ROBOCUP = 1 | 4 | 16
+STAGES_LUNAR = 1 | 2 | 4 | 8 | 16
+
+
+def load():
+    lib = ctypes.CDLL(LIB)
+    lib.oracle_scene_size.restype = ctypes.c_int
+    lib.oracle_scene_init.argtypes = [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P, _P]
+    lib.oracle_step.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                ctypes.c_int, _P, _P, ctypes.c_int]
+    lib.oracle_contacts.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P]
+    return lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_P)
+
+
+class Scene:
+    """Scene description + local geometry (row) from oracle Body objects."""
+
+    def __init__(self, lib, bodies):
+        self.lib = lib
+        params = np.array([[b.mass, b.inertia, b.elasticity, b.friction_coefficient] for b in bodies], np.float32)
+        pb, pt, pn, geom = [], [], [], []
+        for i, b in enumerate(bodies):
+            for p in b.parts:
+                pb.append(i)
+                pt.append(TYPE_ID[p.kind])
+                if p.kind == "Circle":
+                    pn.append(0)
+                    geom += [p.radius, p.position[0], p.position[1], 0.0]
+                elif p.kind == "AABB":
+                    pn.append(0)
+                    geom += [p.lower[0], p.lower[1], p.upper[0], p.upper[1]]
+                else:
+                    pn.append(len(p.vertices_))
+                    for v in p.vertices_:
+                        geom += [v[0], v[1]]
+        self.n_bodies = len(bodies)
+        self.geom = np.array(geom, np.float32)
+        self.mem = ctypes.create_string_buffer(lib.oracle_scene_size())
+        args = [np.array(x, np.int32) for x in (pb, pt, pn)]
+        rc = lib.oracle_scene_init(self.mem, len(bodies), _p(params), len(pb), *[_p(a) for a in args])
+        if rc:
+            raise RuntimeError("oracle_scene_init failed (%d)" % rc)
+
+    def step(self, dyn, keys, err, n_steps, stages, geom=None, dyn_reset=None, resets=None, nthreads=0, dt=1e-2):
+        """dyn f32 [nb,6,B], keys u32 [B,2], err u32 [B] (in place); geom None
+        (shared, this scene's) or f32 [B,G] per env."""
+        B = dyn.shape[2]
+        g = self.geom if geom is None else np.ascontiguousarray(geom, np.float32)
+        gstride = 0 if geom is None else g.shape[1]
+        self.lib.oracle_step(self.mem, _p(dyn), _p(keys), _p(err), _p(g), gstride, B, n_steps, dt, stages,
+                             _p(dyn_reset), _p(resets), nthreads)
+
+
+def robocup_batch(B, seed_keys=3):
+    """The bench's RoboCup batch (perturbed ball per env, keys split(PRNGKey(3), B))."""
+    from . import geometry  # noqa: F401
+    keys = np.ascontiguousarray(prng.split(prng.PRNGKey(seed_keys), B)).astype(np.uint32)
+    base = np.array([b.dyn() for b in P.robocup_bodies()], np.float32)
+    dyn = np.repeat(base[:, :, None], B, axis=2)
+    pk = prng.split(prng.PRNGKey(2), B)
+    for e in range(1, B):
+        kp, kv, kw = prng.split(pk[e], 3)
+        u = prng.uniform(kp, (2,))
+        lo, hi = np.array([-4.4, -2.9], np.float32), np.array([4.4, 2.9], np.float32)
+        pos = np.maximum(lo, u * (hi - lo) + lo)
+        vel = prng.uniform(kv, (2,), -2.0, 2.0)
+        w = prng.uniform(kw, (), -10.0, 10.0)
+        dyn[4, :, e] = [pos[0], pos[1], vel[0], vel[1], 0.0, w]
+    return np.ascontiguousarray(dyn), keys
+
+
+def time_baseline(scenario, seconds=12.0, B=1024):
+    """Env-steps/s of the C port on this host's cores (OpenMP over envs),
+    over a bounded sample of the bench workload (autoreset, 4 steps/call)."""
+    lib = load()
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    if scenario == "robocup":
+        sc = Scene(lib, P.robocup_bodies())
+        dyn, keys = robocup_batch(B)
+        geom, stages = None, STAGES_ROBOCUP
+    else:
+        tk = prng.split(prng.PRNGKey(0), B)
+        sc = Scene(lib, P.lunar_lander_bodies(tk[0]))
+        rows = [Scene(lib, P.lunar_lander_bodies(k)).geom for k in tk]
+        geom = np.ascontiguousarray(np.stack(rows))
+        dyn = np.ascontiguousarray(np.repeat(np.array([b.dyn() for b in P.lunar_lander_bodies(tk[0])],
+                                                      np.float32)[:, :, None], B, axis=2))
+        keys = np.ascontiguousarray(prng.split(prng.PRNGKey(1), B)).astype(np.uint32)
+        stages = STAGES_LUNAR
+    reset = dyn.copy()
+    err = np.zeros(B, np.uint32)
+    resets = np.zeros(B, np.uint32)
+    n = 0
+    sc.step(dyn, keys, err, 1, stages, geom, reset, resets, nthreads)  # warm-up
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        sc.step(dyn, keys, err, 4, stages, geom, reset, resets, nthreads)
+        n += 4 * B
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
+            "sample": "%d env-steps (%d envs x %d steps, %s, autoreset) of the C oracle port "
+                      "(faithful N1xN2 collider scan), OpenMP %d threads, %.1f s"
+                      % (n, B, n // B, scenario, nthreads, dt)}

@@ -312,3 +312,68 @@ def test_lunar_4096_sampled_oracle(torch_cuda):
     res = _oracle_envs(lambda e: P.lunar_lander_bodies(tkeys[e]), P.lunar_lander_step, init, keys0, ids, T)
     for e, (d, k, eb) in zip(ids, res):
         assert same_f32(dyn[e], d), "env %d: %s" % (e, diff_report(dyn[e], d))
+
+
+# ---------------------------------------------------------------------------
+# BASELINE sizes, every env: HIP path vs the C port of the oracle
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def cport_lib():
+    from cotix_oracle import cport
+    if not os.path.exists(cport.LIB):
+        pytest.skip("oracle C port not built (make -C oracle)")
+    return cport, cport.load()
+
+
+def test_robocup_4096_all_envs_vs_cport_autoreset(torch_cuda, cport_lib):
+    """The bench workload itself: 4096 perturbed envs, 3 launches x 16 fused
+    steps with episode restarts, compared for every env."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import physics as P
+    cport, lib = cport_lib
+    B = 4096
+    env = pa.BatchedEnv(pa.RoboCupEnv(batch=B, device="cuda", perturb=True), autoreset=True)
+    env.reset()
+    dyn = np.ascontiguousarray(env.world.dyn.cpu().numpy())
+    keys = np.ascontiguousarray(env.world.keys.cpu().numpy().view(np.uint32))
+    reset = dyn.copy()
+    err = np.zeros(B, np.uint32)
+    resets = np.zeros(B, np.uint32)
+    sc = cport.Scene(lib, P.robocup_bodies())
+    for _ in range(3):
+        env.step(16)
+        sc.step(dyn, keys, err, 16, cport.STAGES_ROBOCUP, None, reset, resets, nthreads=8)
+    torch.cuda.synchronize()
+    assert same_f32(env.world.dyn.cpu().numpy(), dyn), diff_report(env.world.dyn.cpu().numpy(), dyn)
+    assert np.array_equal(env.world.keys.cpu().numpy().view(np.uint32), keys)
+    assert np.array_equal(env.world.err.cpu().numpy().view(np.uint32), err)
+    assert np.array_equal(env.resets.cpu().numpy().view(np.uint32), resets)
+    assert resets.sum() > 0
+
+
+def test_lunar_4096_all_envs_vs_cport(torch_cuda, cport_lib):
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    cport, lib = cport_lib
+    B, T = 4096, 8
+    tkeys = prng.split(prng.PRNGKey(0), B)
+    ll = pa.LunarLander(key=torch.tensor(u32_to_i32(tkeys), device="cuda"), batch=B, device="cuda")
+    drop = torch.zeros(B, device="cuda")
+    drop[::3] = 6.25
+    for i in range(3):
+        ll.world.dyn[i, 1] -= drop
+        ll.world.dyn[i, 3] = torch.where(drop > 0, torch.tensor(-0.3, device="cuda"), ll.world.dyn[i, 3])
+    dyn = np.ascontiguousarray(ll.world.dyn.cpu().numpy())
+    keys = np.ascontiguousarray(ll.world.keys.cpu().numpy().view(np.uint32))
+    geom = np.ascontiguousarray(ll.world.geom.cpu().numpy())
+    err = np.zeros(B, np.uint32)
+    ll.world.step(T, 1e-2, ll.stages)
+    sc = cport.Scene(lib, P.lunar_lander_bodies(tkeys[0]))
+    sc.step(dyn, keys, err, T, cport.STAGES_LUNAR, geom, nthreads=8)
+    torch.cuda.synchronize()
+    got = ll.world.dyn.cpu().numpy()
+    assert same_f32(got, dyn), diff_report(got, dyn)
+    assert np.array_equal(ll.world.keys.cpu().numpy().view(np.uint32), keys)

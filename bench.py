@@ -9,6 +9,12 @@ n_gpus / max-over-ranks wall time.
 
   python bench.py [--gpus N --steps K --warmup W --substeps S --scenario robocup|lunar]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+
+--mode grad (BASELINE config 5): one bench step = a differentiable --substeps
+(64) step RoboCup rollout from a fixed start state, forward (cotix_rollout)
++ backward (cotix_rollout_backward) -> d(sum_t ball x)/d(action) for every
+env; value = envs * substeps * steps * n_gpus / wall (env-steps with
+gradient per second).
 """
 import argparse
 import json
@@ -34,6 +40,7 @@ def parse():
     ap.add_argument("--scenario", default="robocup", choices=["robocup", "lunar"])
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--mode", default="step", choices=["step", "grad"])
     return ap.parse_args()
 
 
@@ -66,8 +73,40 @@ def cpu_baseline(scenario, seconds):
             "sample": "%d sequential env-steps of one %s env (python oracle, autoreset), %.1f s" % (n, scenario, dt)}
 
 
+def cpu_baseline_grad(T, seconds):
+    """Central finite differences (eps=1e-3) of the C oracle port (SURVEY.md
+    8(d) config 5): 4T perturbed rollouts per env, OpenMP over all of them.
+    Bounded sample sized from a short probe to ~`seconds`."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from cotix_oracle import cport
+    from cotix_oracle import physics as P
+    lib = cport.load()
+    sc = cport.Scene(lib, P.robocup_bodies())
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    w = np.zeros(30, np.float32)
+    w[24] = 1.0
+
+    def run(B):
+        dyn, keys = cport.robocup_batch(B)
+        acts = (np.random.default_rng(0).normal(size=(T, B, 2)) * 0.1).astype(np.float32)
+        t0 = time.perf_counter()
+        cport.fd_action_grad(sc, dyn, keys, acts, 4, w, cport.STAGES_ROBOCUP, eps=1e-3, nthreads=nthreads)
+        return time.perf_counter() - t0
+
+    B, dt = 8, run(8)
+    while dt < 0.5 * seconds and B < 4096:  # grow the sample to ~`seconds` of CPU work
+        B = int(min(4096, max(2 * B, B * seconds / max(dt, 1e-3))))
+        dt = run(B)
+    return {"value": B * T / dt, "unit": "env-steps/s (with d ret/d action)", "cores": nthreads, "kind": "port",
+            "sample": "%d RoboCup envs x %d-step rollout, gradient by central differences (%d perturbed rollouts "
+                      "per env) of the C oracle port, OpenMP %d threads, %.1f s" % (B, T, 4 * T, nthreads, dt)}
+
+
 def main():
     a = parse()
+    if a.mode == "grad":
+        return main_grad(a)
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -94,8 +133,15 @@ def main():
     env.reset()
     obs_all = torch.empty(world_size * B, len(scen.bodies), 6, device=dev) if dist else None
 
-    def one_step():
+    # HIP events around every step-kernel launch, on the stream it runs on
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+
+    def one_step(i=None):
+        if i is not None:
+            evs[i][0].record()
         env.step(a.substeps)
+        if i is not None:
+            evs[i][1].record()
         if dist is not None:  # north star: RCCL all-gather of the observation tensor
             dist.all_gather_into_tensor(obs_all, env.observation().contiguous())
 
@@ -105,18 +151,15 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(a.steps):
-        one_step()
-    ev1.record()
+    for i in range(a.steps):
+        one_step(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1)
+    ev_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs)
     tmax = torch.tensor([wall], device=dev, dtype=torch.float64)
     if dist:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -178,6 +221,116 @@ def main():
         pass
     if rank == 0 and a.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline(a.scenario, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def main_grad(a):
+    """BASELINE config 5: differentiable RoboCup rollout, forward + backward."""
+    import numpy as np
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world_size > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    import parallax_amd as pa
+    B, T = a.envs, a.substeps
+    keys = pa.random.split(pa.random.PRNGKey(3, dev), B * world_size)[rank * B:(rank + 1) * B].contiguous()
+    scen = pa.RoboCupEnv(batch=B, device=dev, keys=keys, perturb=True)
+    world = scen.world
+    dyn0, keys0 = world.dyn.clone(), world.keys.clone()
+    gen = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    actions = (torch.randn(T, B, 2, generator=gen) * 0.1).to(dev)  # SURVEY 8(d): ball dv ~ N(0, 0.1^2)
+    w = pa.rollout.ball_x_weights(5, 4)
+    evf = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    evb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    state = {}
+
+    def one_step(i=None):
+        world.dyn.copy_(dyn0)
+        world.keys.copy_(keys0)
+        world.err.zero_()
+        if i is not None:
+            evf[i][0].record()
+        ret, saved = pa.rollout_forward(world, actions, 4, w)
+        if i is not None:
+            evf[i][1].record()
+            evb[i][0].record()
+        ga, _ = pa.rollout_backward(world, saved)
+        if i is not None:
+            evb[i][1].record()
+        state["ret"], state["ga"] = ret, ga
+
+    for _ in range(a.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        one_step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    tmax = torch.tensor([wall], device=dev, dtype=torch.float64)
+    if dist:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    wall = float(tmax.item())
+    fwd_ms = sum(e0.elapsed_time(e1) for e0, e1 in evf) / a.steps
+    bwd_ms = sum(e0.elapsed_time(e1) for e0, e1 in evb) / a.steps
+    ga = state["ga"]
+    finite = float(torch.isfinite(ga).all(dim=2).all(dim=0).float().mean().item())
+    # algorithmic HBM bytes of the backward launch per env-step: saved state
+    # (5x6 f32) + key (2 u32) + action (2 f32) read, grad_action (2 f32) written
+    bwd_bytes = (5 * 6 * 4 + 8 + 8 + 8) * B * T
+    achieved = bwd_bytes / (bwd_ms * 1e-3) / 1e9
+    out = {
+        "metric": "differentiable 64-step RoboCup rollout, 4096 envs/GPU: env-steps/s with d(return)/d(action)",
+        "value": B * T * a.steps * world_size / wall,
+        "unit": "env-steps/s",
+        "n_gpus": world_size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": wall * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (RoboCup scene, per-env ball perturbation; actions N(0, 0.1^2) per step)",
+        "config": {
+            "workload": "RoboCup (cotix/_robocup.py) %d envs/GPU, %d-step rollout, grad of sum_t ball x "
+                        "w.r.t. per-step ball dv (BASELINE config 5)" % (B, T),
+            "envs_per_gpu": B,
+            "rollout_steps": T,
+            "fwd_ms": fwd_ms,
+            "bwd_ms": bwd_ms,
+            "finite_grad_env_fraction": finite,
+            "parallelism": "dp%d (independent env shards)" % world_size,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "step_kernel<4,1,true> (backward re-play)",
+            "launch_ms": bwd_ms,
+            "alg_bytes_per_launch": bwd_bytes,
+            "note": "VALU/latency-bound (the backward re-plays each step's forward); HBM figure for completeness",
+        },
+    }
+    if rank == 0 and a.cpu_baseline == "auto":
+        out["cpu_baseline"] = cpu_baseline_grad(T, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -109,6 +109,36 @@ int cotix_step_autoreset(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_
                          int geom_stride, int B, int n_steps, float dt, int stages, const float* dyn_reset,
                          uint32_t* resets, cotix_stream_t stream);
 
+/* Differentiable rollout (BASELINE config 5: grad(return)/d(action) through a
+ * fused n_steps RoboCup rollout).  The reference has no return or action
+ * (cotix/_envs.py:9-28 is abstract); SURVEY 8(d) defines them: action[t] is
+ * added to the velocity of body action_body after Euler (where the LL driver
+ * adds gravity, examples/test_viz.py:27-31), and
+ *   ret[env] += sum_{t=1..n_steps} sum_k ret_weights[k] * state_t[k]
+ * over the n_bodies*6 state words (terms with ret_weights[k] == 0 are
+ * skipped, so NaN bodies outside the return do not poison it).
+ *
+ * cotix_rollout runs the forward like cotix_step (no restarts) and saves the
+ * state and key before every step: saved_dyn device f32
+ * [n_steps][n_bodies][6][B], saved_keys device u32 [n_steps][B][2];
+ * ret_weights is HOST f32 [n_bodies*6]; ret device f32 [B] (accumulated).
+ *
+ * cotix_rollout_backward re-plays every step from the saved state (so each
+ * discrete choice -- contacts, RNG draws, branches -- is the forward's) and
+ * applies the reverse-mode derivative of the executed branch (jax.grad
+ * semantics through the reference's lax.cond branches, balanced ties for
+ * max/min/clip).  grad_action device f32 [n_steps][B][2] (nullable),
+ * grad_dyn0 device f32 [n_bodies][6][B] (nullable) = d ret / d initial state.
+ * Scenes with polygon parts (GJK/EPA) and the LunarLander stage are rejected. */
+int cotix_rollout(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
+                  int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                  const float* ret_weights, float* ret, float* saved_dyn, uint32_t* saved_keys,
+                  cotix_stream_t stream);
+int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uint32_t* saved_keys, const float* geom,
+                           int geom_stride, int B, int n_steps, float dt, int stages, const float* action,
+                           int action_body, const float* ret_weights, float* grad_action, float* grad_dyn0,
+                           cotix_stream_t stream);
+
 /* Operator-level entry points (batched over n independent items). */
 int cotix_physics_euler(float* dyn, int n_bodies, int B, float dt, cotix_stream_t stream);
 int cotix_collider_resolve(cotix_scene* scene, float* dyn, const uint32_t* keys, uint32_t* err,

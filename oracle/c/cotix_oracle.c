@@ -573,8 +573,9 @@ static void collider(const OScene* s, Dyn* d, const float* geom, K2 rkey, V2 d0,
 /* The driver (examples/test_viz.py), n_steps per env, OpenMP over envs.
  * dyn [nb][6][B]; keys u32 [B][2]; err u32 [B] (OR-ed); geom [G] or [B][gstride];
  * stages as include/cotix_amd.h; dyn_reset nullable (autoreset like the bench). */
-int oracle_step(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
-                int n_steps, float dt, int stages, const float* dyn_reset, uint32_t* resets, int nthreads) {
+static int drive(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
+                 int n_steps, float dt, int stages, const float* dyn_reset, uint32_t* resets, const float* action,
+                 int action_body, const float* ret_w, float* ret, int nthreads) {
   const OScene* s = (const OScene*)scene;
   const V2 d0 = {bitsf(0xbd56c50bu), bitsf(0x3f7fa5d9u)};
 #ifdef _OPENMP
@@ -602,6 +603,11 @@ int oracle_step(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, co
       if (stages & 1)
         for (int b = 0; b < nb; ++b) { d[b].px = d[b].px + d[b].vx * dt; d[b].py = d[b].py + d[b].vy * dt; d[b].a = d[b].a + d[b].w * dt; }
       if (stages & 2) { d[0].vx = d[0].vx + 0.0f; d[0].vy = d[0].vy + -0.002f; }
+      if (action) {  /* config 5: velocity += action after Euler */
+        const float* ac = action + ((size_t)t * B + g) * 2;
+        d[action_body].vx = d[action_body].vx + ac[0];
+        d[action_body].vy = d[action_body].vy + ac[1];
+      }
       if (stages & 4) collider(s, d, gg, key, d0, &e, &wk);
       if (stages & 8) lunar(&d[0], &d[1], &d[2], &s->par[0], &s->par[1], &s->par[2]);
       if (stages & 16) key = split0(key);
@@ -614,6 +620,16 @@ int oracle_step(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, co
         e = 0;
         if (resets) resets[g] += 1;
       }
+      if (ret) {  /* return: sum over steps of sum_k w_k * state_k (w_k != 0) */
+        float acc = ret[g];
+        for (int k = 0; k < nb * 6; ++k) {
+          if (ret_w[k] == 0.0f) continue;
+          const Dyn* q = &d[k / 6];
+          const float x[6] = {q->px, q->py, q->vx, q->vy, q->a, q->w};
+          acc = acc + ret_w[k] * x[k % 6];
+        }
+        ret[g] = acc;
+      }
     }
     for (int b = 0; b < nb; ++b) {
       float* q = dyn + (size_t)b * 6 * B + g;
@@ -625,6 +641,20 @@ int oracle_step(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, co
     free(wk.cur); free(wk.keys2); free(wk.keys1);
   }
   return 0;
+}
+
+int oracle_step(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
+                int n_steps, float dt, int stages, const float* dyn_reset, uint32_t* resets, int nthreads) {
+  return drive(scene, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, dyn_reset, resets, NULL, 0, NULL, NULL,
+               nthreads);
+}
+
+/* forward of the differentiable rollout: action [n_steps][B][2], ret [B] += */
+int oracle_rollout(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride,
+                   int B, int n_steps, float dt, int stages, const float* action, int action_body, const float* ret_w,
+                   float* ret, int nthreads) {
+  return drive(scene, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, NULL, NULL, action, action_body, ret_w,
+               ret, nthreads);
 }
 
 int oracle_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err) {

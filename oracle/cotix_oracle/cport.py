@@ -25,6 +25,8 @@ def load():
     lib.oracle_step.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                 ctypes.c_int, _P, _P, ctypes.c_int]
     lib.oracle_contacts.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P]
+    lib.oracle_rollout.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                   ctypes.c_int, _P, ctypes.c_int, _P, _P, ctypes.c_int]
     return lib
 
 
@@ -69,6 +71,38 @@ class Scene:
         gstride = 0 if geom is None else g.shape[1]
         self.lib.oracle_step(self.mem, _p(dyn), _p(keys), _p(err), _p(g), gstride, B, n_steps, dt, stages,
                              _p(dyn_reset), _p(resets), nthreads)
+
+
+    def rollout(self, dyn, keys, err, stages, actions, action_body, ret_w, geom=None, nthreads=0, dt=1e-2):
+        """Forward of the differentiable rollout; returns ret [B]."""
+        B = dyn.shape[2]
+        g = self.geom if geom is None else np.ascontiguousarray(geom, np.float32)
+        gstride = 0 if geom is None else g.shape[1]
+        ret = np.zeros(B, np.float32)
+        actions = np.ascontiguousarray(actions, np.float32)
+        ret_w = np.ascontiguousarray(ret_w, np.float32)
+        self.lib.oracle_rollout(self.mem, _p(dyn), _p(keys), _p(err), _p(g), gstride, B, actions.shape[0], dt, stages,
+                                _p(actions), action_body, _p(ret_w), _p(ret), nthreads)
+        return ret
+
+
+def fd_action_grad(sc, dyn0, keys0, actions, action_body, ret_w, stages, eps=1e-3, nthreads=0):
+    """Central finite differences d ret / d action [T, B, 2] of the C port:
+    4T perturbed rollouts per env, batched (OpenMP over all of them)."""
+    nb, _, B = dyn0.shape
+    T = actions.shape[0]
+    n = 4 * T
+    dyn = np.ascontiguousarray(np.repeat(dyn0[:, :, None, :], n, axis=2).reshape(nb, 6, n * B))
+    keys = np.ascontiguousarray(np.repeat(keys0[None], n, axis=0).reshape(n * B, 2))
+    acts = np.repeat(actions[:, None], n, axis=1).copy()  # [T, n, B, 2]
+    for q in range(n):
+        t, c, sgn = q // 4, (q // 2) % 2, 1.0 if q % 2 == 0 else -1.0
+        acts[t, q, :, c] += np.float32(sgn * eps)
+    acts = np.ascontiguousarray(acts.reshape(T, n * B, 2))
+    err = np.zeros(n * B, np.uint32)
+    ret = sc.rollout(dyn, keys, err, stages, acts, action_body, ret_w, nthreads=nthreads).reshape(n, B)
+    g = (ret[0::2].astype(np.float64) - ret[1::2]) / (2 * eps)  # [2T, B]
+    return g.reshape(T, 2, B).transpose(0, 2, 1)
 
 
 def robocup_batch(B, seed_keys=3):

@@ -1,0 +1,274 @@
+"""TEST INFRASTRUCTURE ONLY -- the checker of the differentiable rollout
+(BASELINE config 5).  Never imported by the product.
+
+jax.grad of the reference step differentiates the executed branch of every
+jax.lax.cond (cotix/_contacts.py:30-154, cotix/_collision_resolution.py:
+52-146, cotix/_colliders.py:333) with argmin/argmax and the RandomizedCollider
+choices as constants, and lax.max/min (jnp.clip) splitting ties 1/2-1/2.
+This module restates the continuous part of one step with torch float32
+autograd (torch.maximum/minimum have the same balanced tie rule), in the
+oracle's exact operation order, so its forward values are bit-identical to
+the oracle's and every branch/tie decision is the one the oracle took.  The
+discrete choices (which contact each body resolves, and which part pair
+produced it) come from the faithful oracle's trace (physics.collider_resolve
+trace["src"]).  Gradients of a T-step return are chained step by step:
+lambda_T = w; (lambda_t, dR/da_t) = VJP_t(lambda_{t+1}); lambda_t += w (t>=1).
+
+Return definition: action a_t (f32[2]) is added
+to the velocity of body `action_body` right after Euler; the return is
+R = sum_{t=1..T} sum_k w_k * state_t[k] over terms with w_k != 0.
+"""
+import warnings
+
+import numpy as np
+import torch
+
+from . import physics as P
+
+F32 = torch.float32
+# branch decisions read forward values of graph tensors (intended)
+warnings.filterwarnings("ignore", message="Converting a tensor with requires_grad=True to a scalar")
+
+
+def _t(x):
+    return torch.tensor(float(x), dtype=F32)
+
+
+def _fmax(a, b):
+    return torch.maximum(a, b)
+
+
+def _fmin(a, b):
+    return torch.minimum(a, b)
+
+
+def _clip(x, lo, hi):  # jnp.clip = minimum(maximum(x, lo), hi)
+    return _fmin(hi, _fmax(lo, x))
+
+
+def _dot(a, b):
+    return a[0] * b[0] + a[1] * b[1]
+
+
+class _Sqrt(torch.autograd.Function):
+    """Correctly rounded f32 sqrt (torch's CPU sqrt is not: it differs from
+    IEEE sqrt in ~0.5% of f32 inputs, machine-dependently); JAX's JVP
+    rule g * (0.5 / ans)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y = torch.tensor(np.sqrt(np.float32(x.item())), dtype=F32)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        return g * (0.5 / y)
+
+
+def _norm(a):
+    return _Sqrt.apply(a[0] * a[0] + a[1] * a[1])
+
+
+def _cross(a, b):
+    return a[0] * b[1] - a[1] * b[0]
+
+
+def _sub(a, b):
+    return (a[0] - b[0], a[1] - b[1])
+
+
+def _add(a, b):
+    return (a[0] + b[0], a[1] + b[1])
+
+
+def _isnan(v):
+    return bool(torch.isnan(v[0])) or bool(torch.isnan(v[1]))
+
+
+# ---- analytic contacts, contact branch (geometry.py / cotix/_contacts.py) ----
+def circle_vs_circle(a, b):  # a, b = (radius, (cx, cy))
+    ar, ap = a
+    br, bp = b
+    delta = _sub(ap, bp)
+    distance = _norm(delta)
+    if float(distance.detach()) == 0.0:
+        direction = (_t(1.0), _t(0.0))
+    else:
+        direction = (delta[0] / distance, delta[1] / distance)
+    m = _fmin(distance - (ar + br), _t(0.0))
+    pen = (direction[0] * m, direction[1] * m)
+    cp = ((bp[0] + direction[0] * (br - ar)) + ap[0], (bp[1] + direction[1] * (br - ar)) + ap[1])
+    cp = (cp[0] / 2.0, cp[1] / 2.0)
+    if not float(_dot(_sub(ap, cp), _sub(bp, cp))) <= 0:
+        d = _sub(bp, ap)  # Circle.contains (geometry.py): sumsq(p - c) <= r*r, r = radius + eps
+        r = np.float32(ar.item()) + np.float32(1e-6)
+        inside = float(d[0] * d[0] + d[1] * d[1]) <= float(r * r)
+        cp = bp if inside else ap
+    assert float(distance) <= float(ar + br), "not a contact"
+    return ((-pen[0], -pen[1]), cp)
+
+
+def aabb_vs_aabb(a, b, eps=1e-8):  # a, b = (lower, upper)
+    alo, aup = a
+    blo, bup = b
+    me = _t(-np.float32(eps))
+    depths = [_fmax(aup[1] - blo[1], me), _fmax(bup[1] - alo[1], me), _fmax(aup[0] - blo[0], me),
+              _fmax(bup[0] - alo[0], me)]
+    dirs = [(0, -1), (0, 1), (-1, 0), (1, 0)]
+    k = int(np.argmin([float(d) for d in depths]))
+    md = _fmax(_t(0.0), depths[k])
+    pen = (md * float(dirs[k][0]), md * float(dirs[k][1]))
+    mu = (_fmin(aup[0], bup[0]), _fmin(aup[1], bup[1]))
+    ml = (_fmax(alo[0], blo[0]), _fmax(alo[1], blo[1]))
+    return (pen, ((mu[0] + ml[0]) / 2.0, (mu[1] + ml[1]) / 2.0))
+
+
+def circle_vs_aabb(a, b, eps=1e-6):
+    r, ap = a
+    lo, up = b
+    bc = ((lo[0] + up[0]) / 2.0, (lo[1] + up[1]) / 2.0)
+    disp = _sub(ap, bc)
+    l = _sub(lo, bc)
+    h = _sub(up, bc)
+    ccp = _add(bc, (_clip(disp[0], l[0], h[0]), _clip(disp[1], l[1], h[1])))
+    vs = [lo, (lo[0], up[1]), up, (up[0], lo[1])]
+    perfect = any(float(_norm(_sub(v, ccp)).detach()) < np.float32(eps) for v in vs)
+    if perfect:
+        d = _sub(ccp, ap)
+        nd = _norm(d)
+        dn = (d[0] / nd, d[1] / nd)
+        q = _sub(_add(ap, (dn[0] * r, dn[1] * r)), ccp)
+        return ((-q[0], -q[1]), ccp)
+    shifts = [(ap[1] + r) - lo[1], up[1] - (ap[1] - r), (ap[0] + r) - lo[0], up[0] - (ap[0] - r)]
+    dirs = [(0, 1), (0, -1), (1, 0), (-1, 0)]
+    k = int(np.argmin([float(s) for s in shifts]))
+    ns = -shifts[k]
+    return ((ns * float(dirs[k][0]), ns * float(dirs[k][1])), ccp)
+
+
+CONTACTS = {"circle_vs_circle": circle_vs_circle, "aabb_vs_aabb": aabb_vs_aabb, "circle_vs_aabb": circle_vs_aabb}
+
+
+# ---- resolution (cotix/_collision_resolution.py:52-146) ----
+class _B:
+    def __init__(self, p, v, ang, w, body):
+        self.p, self.v, self.ang, self.w = p, v, ang, w
+        self.m, self.I = _t(body.mass), _t(body.inertia)
+        self.e, self.mu = _t(body.elasticity), _t(body.friction_coefficient)
+
+    def vel_at(self, pt):
+        r = _sub(pt, self.p)
+        return (self.v[0] + (-r[1]) * self.w, self.v[1] + r[0] * self.w)
+
+
+def _apply(b, imp, pt):
+    arm = _sub(pt, b.p)
+    torque = _cross(arm, imp)
+    b.v = (b.v[0] + imp[0] / b.m, b.v[1] + imp[1] / b.m)
+    b.w = b.w + torque / b.I
+
+
+def resolve(b1, b2, pen, cp):
+    v1, v2 = b1.vel_at(cp), b2.vel_at(cp)
+    relv = _sub(v2, v1)
+    pn = _norm(pen)
+    n = (pen[0] / pn, pen[1] / pn)
+    vn = _dot(relv, n)
+    e = _fmin(b1.e, b2.e)
+    r1, r2 = _sub(cp, b1.p), _sub(cp, b2.p)
+    lever1 = r1[0] * r1[0] + r1[1] * r1[1]
+    lever2 = r2[0] * r2[0] + r2[1] * r2[1]
+    ang = lever1 / b1.I + lever2 / b2.I
+    nim = (-(1.0 + e)) * vn - (_t(0.3) * _norm(pen)) / _t(0.01)
+    den = (1.0 / b1.m + 1.0 / b2.m) + ang
+    ni = nim / den
+    imp = (n[0] * ni, n[1] * ni)
+    mu = (b1.mu + b2.mu) / 2.0
+    vd = (relv[0] + vn * n[0], relv[1] + vn * n[1])
+    vdn = _norm(vd)
+    vdu = (vd[0] / vdn, vd[1] / vdn)
+    idr = (-vdn) / ((1.0 / b1.m + 1.0 / b2.m) + ang)
+    idr = _clip(idr, _t(0.0), ni * mu)
+    imp = (imp[0] + vdu[0] * idr, imp[1] + vdu[1] * idr)
+    if float(_dot(pen, relv)) < 0:
+        return False
+    _apply(b1, (-imp[0], -imp[1]), cp)
+    _apply(b2, imp, cp)
+    return True
+
+
+def _world_part(part, p):
+    if part.kind == "Circle":
+        return (_t(part.radius), (_t(part.position[0]) + p[0], _t(part.position[1]) + p[1]))
+    if part.kind == "AABB":
+        return ((_t(part.lower[0]) + p[0], _t(part.lower[1]) + p[1]),
+                (_t(part.upper[0]) + p[0], _t(part.upper[1]) + p[1]))
+    raise NotImplementedError("polygon contacts are not differentiated")
+
+
+def step_torch(S, a, bodies, trace, dt, action_body, gravity=False):
+    """One step's continuous map S_t [nb,6] -> S_{t+1} given the oracle's
+    discrete choices (trace of the same step)."""
+    nb = S.shape[0]
+    dt = float(np.float32(dt))
+    st = []
+    for b in range(nb):
+        p = (S[b, 0] + S[b, 2] * dt, S[b, 1] + S[b, 3] * dt)
+        st.append(_B(p, (S[b, 2], S[b, 3]), S[b, 4] + S[b, 5] * dt, S[b, 5], bodies[b]))
+    if gravity:
+        st[0].v = (st[0].v[0] + 0.0, st[0].v[1] + float(np.float32(P.LL_GRAVITY)))
+    if a is not None:
+        st[action_body].v = (st[action_body].v[0] + a[0], st[action_body].v[1] + a[1])
+    chosen, src = trace["chosen"], trace["src"]
+    for i in range(nb):
+        j = chosen[i]
+        if j == i:
+            continue
+        fname, (o1b, o1p), (o2b, o2p) = src[i][j]
+        s1 = _world_part(bodies[o1b].parts[o1p], st[o1b].p)
+        s2 = _world_part(bodies[o2b].parts[o2p], st[o2b].p)
+        pen, cp = CONTACTS[fname](s1, s2)
+        resolve(st[i], st[j], pen, cp)
+    rows = [torch.stack([b.p[0], b.p[1], b.v[0], b.v[1], b.ang, b.w]) for b in st]
+    return torch.stack(rows)
+
+
+def rollout_grad(make_bodies, S0, key0, actions, w, action_body, d0, dt=P.DT, step=P.robocup_step):
+    """Oracle forward (faithful, f32) + torch VJP chain.
+    S0 [nb,6] f32, key0 u32[2], actions [T,2] f32, w [nb*6] f32.
+    Returns (ret, grad_actions [T,2], grad_S0 [nb,6], states [T+1,nb,6])."""
+    T = actions.shape[0]
+    bodies = make_bodies()
+    for b, row in zip(bodies, S0):
+        b.set_dyn(row)
+    key = np.asarray(key0, np.uint32)
+    states, traces = [np.array([b.dyn() for b in bodies], np.float32)], []
+    for t in range(T):
+        tr = {}
+        bodies, key = step(bodies, key, d0, None, tr, dt, action=actions[t], action_body=action_body)
+        states.append(np.array([b.dyn() for b in bodies], np.float32))
+        traces.append(tr)
+    wm = np.asarray(w, np.float32).reshape(-1, 6)
+    ret = np.float32(0.0)
+    for t in range(1, T + 1):
+        for k in np.flatnonzero(wm.reshape(-1)):
+            ret = np.float32(ret + np.float32(wm.reshape(-1)[k]) * states[t].reshape(-1)[k])
+    lam = torch.tensor(wm, dtype=F32)
+    ga = np.zeros((T, 2), np.float32)
+    meta = make_bodies()
+    for t in range(T - 1, -1, -1):
+        S = torch.tensor(states[t], dtype=F32, requires_grad=True)
+        a = torch.tensor(actions[t], dtype=F32, requires_grad=True)
+        out = step_torch(S, a, meta, traces[t], dt, action_body, gravity=step is P.lunar_lander_step)
+        o = out.detach().numpy()
+        same = (o.view(np.uint32) == states[t + 1].view(np.uint32)) | (np.isnan(o) & np.isnan(states[t + 1]))
+        assert same.all(), "torch restatement diverged from the oracle at step %d: %s vs %s" % (
+            t, o[~same], states[t + 1][~same])
+        gS, gA = torch.autograd.grad(out, (S, a), lam, allow_unused=True)
+        ga[t] = gA.numpy() if gA is not None else 0.0
+        lam = gS.detach().clone()
+        if t >= 1:
+            lam = lam + torch.tensor(wm, dtype=F32)
+    return ret, ga, lam.numpy(), np.stack(states)

@@ -164,18 +164,23 @@ def collider_resolve(bodies, rkey, d0, err=None, trace=None):
 
     pen = [[(ZERO, ZERO) for _ in range(n)] for _ in range(n)]
     cp = [[(NAN, NAN) for _ in range(n)] for _ in range(n)]
+    src = [[None for _ in range(n)] for _ in range(n)]  # (contact fn, (body, part) of s1, of s2)
     skey = prng.split(rkey)[0]  # :142
     for key_t, (l1, l2) in type_to.items():
         N1, N2 = len(l1), len(l2)
         fname = CONTACT_FUNCS[key_t]
         # cross product of contacts :149-173
         cur = [[None] * N2 for _ in range(N1)]
+        srcs = {}
         for i1, (bi, pi) in enumerate(l1):
             for i2, (bj, pj) in enumerate(l2):
                 s1 = world[bi][pi]
                 s2 = world[bj][pj]
+                o1, o2 = (bi, pi), (bj, pj)
                 if (s1.kind, s2.kind) not in CONTACT_FUNCS:  # :155-157
                     s1, s2 = s2, s1
+                    o1, o2 = o2, o1
+                srcs[(i1, i2)] = (fname, o1, o2)
                 # the contact is evaluated for every pair (so error_if trips
                 # count for i < j too) and then masked by lax.cond(i < j) :163
                 c = run_contact(fname, s1, s2, d0, err)
@@ -193,6 +198,7 @@ def collider_resolve(bodies, rkey, d0, err=None, trace=None):
                     bi, bj = l1[i1][0], l2[i2][0]
                     pen[bi][bj] = c[0]
                     cp[bi][bj] = c[1]
+                    src[bi][bj] = srcs[(i1, i2)]
     # choose_random_contact :274-295
     ckeys = prng.split(skey, n)
     chosen = []
@@ -207,6 +213,7 @@ def collider_resolve(bodies, rkey, d0, err=None, trace=None):
     if trace is not None:
         trace["chosen"] = list(chosen)
         trace["contacts"] = [[(pen[i][j], cp[i][j]) for j in range(n)] for i in range(n)]
+        trace["src"] = src
     # sequential resolution :310-336
     for i in range(n):
         j = chosen[i]
@@ -334,19 +341,29 @@ DT = 1e-2
 LL_GRAVITY = -0.002
 
 
-def robocup_step(bodies, key, d0, err=None, trace=None, dt=DT):
+def apply_action(bodies, action, action_body):
+    """Config-5 action: velocity += action after Euler."""
+    if action is None:
+        return
+    v = bodies[action_body].velocity
+    bodies[action_body].velocity = (v[0] + F(action[0]), v[1] + F(action[1]))
+
+
+def robocup_step(bodies, key, d0, err=None, trace=None, dt=DT, action=None, action_body=None):
     """examples/test_viz.py:61-69: Euler -> collider -> (identity constraint
     pass) -> key = split(key)[0]."""
     euler_step(bodies, dt)
+    apply_action(bodies, action, action_body)
     collider_resolve(bodies, key, d0, err, trace)
     return bodies, prng.split(key)[0]
 
 
-def lunar_lander_step(bodies, key, d0, err=None, trace=None, dt=DT):
+def lunar_lander_step(bodies, key, d0, err=None, trace=None, dt=DT, action=None, action_body=None):
     """examples/test_viz.py:24-44."""
     euler_step(bodies, dt)
     v = bodies[0].velocity
     bodies[0].velocity = (v[0] + ZERO, v[1] + F(LL_GRAVITY))
+    apply_action(bodies, action, action_body)
     collider_resolve(bodies, key, d0, err, trace)
     nxt = prng.split(key)[0]
     lunar_lander_constraints(bodies)

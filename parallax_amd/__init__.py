@@ -9,6 +9,8 @@ from .bodies import AnyBody, BodyView  # noqa: F401
 from .env import BatchedEnv  # noqa: F401
 from .physics import (ContactInfo, ExplicitEulerPhysics, RandomizedCollider, SimpleConstraintSolver,  # noqa: F401
                       contact_funcs, resolve_collision, run_contacts)
+from .rollout import rollout as differentiable_rollout  # noqa: F401
+from .rollout import rollout_backward, rollout_forward  # noqa: F401
 from .scenarios import LunarLander, RoboCupEnv  # noqa: F401
 from .shapes import AABB, Circle, Polygon, Polygon3, Polygon4, Polygon5, Polygon6, UniversalShape  # noqa: F401
 from .world import Scene, World  # noqa: F401

@@ -28,6 +28,8 @@ SIGNATURES = {
     "cotix_scene_info": (_I, [_P, _P, _P, _P, _P]),
     "cotix_step": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P]),
     "cotix_step_autoreset": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
+    "cotix_rollout": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P, _P]),
+    "cotix_rollout_backward": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P]),
     "cotix_physics_euler": (_I, [_P, _I, _I, _F, _P]),
     "cotix_collider_resolve": (_I, [_P, _P, _P, _P, _P, _I, _I, _P]),
     "cotix_lunar_constraints": (_I, [_P, _I, _P]),

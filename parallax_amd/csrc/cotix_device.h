@@ -16,11 +16,13 @@
 #include <hip/hip_runtime.h>
 #define CX_DEV __device__ __forceinline__
 #define CX_MF __device__ __forceinline__  // member functions
+#define CX_HD __host__ __device__ inline   // host + device (layout arithmetic)
 #else
 // host build of the same code: used ONLY by the CPU emulation harness of the
 // test suite (tests/emu/), to run the kernel logic under AddressSanitizer.
 #define CX_DEV static inline
 #define CX_MF inline
+#define CX_HD static inline
 static inline float __uint_as_float(uint32_t u) {
   float f;
   memcpy(&f, &u, 4);
@@ -711,8 +713,8 @@ CX_DEV void apply_impulse(Dyn& b, const Params& m, v2 imp, v2 point) {  // :68-7
   b.vy = b.vy + imp.y / m.mass;
   b.w = b.w + torque / m.inertia;
 }
-CX_DEV void resolve_collision(Dyn& b1, const Params& m1, Dyn& b2, const Params& m2, v2 pen, v2 cp) {  // :52-151
-  if (vnan(cp)) return;
+CX_DEV bool resolve_collision(Dyn& b1, const Params& m1, Dyn& b2, const Params& m2, v2 pen, v2 cp) {  // :52-151
+  if (vnan(cp)) return false;
   v2 v1 = velocity_at(b1, cp), v2_ = velocity_at(b2, cp);
   v2 relv = sub(v2_, v1);
   float pn = nrm(pen);
@@ -732,9 +734,10 @@ CX_DEV void resolve_collision(Dyn& b1, const Params& m1, Dyn& b2, const Params& 
   float idr = (-vdn) / ((1.0f / m1.mass + 1.0f / m2.mass) + ang);
   idr = clip_(idr, 0.0f, ni * mu);
   imp = add(imp, scl(vdu, idr));
-  if (dot(pen, relv) < 0.0f) return;
+  if (dot(pen, relv) < 0.0f) return false;  // moving apart (:140-146)
   apply_impulse(b1, m1, neg(imp), cp);
   apply_impulse(b2, m2, imp, cp);
+  return true;
 }
 CX_DEV v2 rotate(v2 v, float ang) {  // _geometry_utils.py:81-88
   float s, c;

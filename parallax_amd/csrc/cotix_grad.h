@@ -1,0 +1,266 @@
+// cotix_grad.h -- reverse-mode derivatives (VJPs) of the continuous part of
+// the step, for the differentiable rollout (BASELINE config 5).
+//
+// Semantics are those of jax.grad through the reference: every branch in
+// the analytic contacts and in the resolution is a jax.lax.cond
+// (cotix/_contacts.py:30-154, cotix/_collision_resolution.py:52-65,140-146,
+// cotix/_colliders.py:333), so only the executed branch is differentiated;
+// argmin/argmax selections are constants; lax.max / lax.min (and jnp.clip,
+// built from them) send the cotangent to the operand equal to the result and
+// split it 1/2-1/2 on a tie (JAX's _balanced_eq JVP rule).  Each function
+// recomputes its forward values with the exact f32 code of cotix_device.h,
+// so branch decisions are those the forward step took.
+//
+// Shape gradients use the geometry layout of the forward path: circle
+// (r, cx, cy, pad) and AABB (lo.x, lo.y, up.x, up.y); the radius, masses,
+// inertias, elasticities and frictions are constants (not differentiated).
+#pragma once
+#include "cotix_device.h"
+
+namespace cx {
+
+CX_DEV void vjp_max(float x, float y, float g, float* gx, float* gy) {
+  const float z = fmax_(x, y);
+  const bool ex = x == z, ey = y == z;
+  *gx += ex ? (ey ? 0.5f * g : g) : 0.0f;
+  *gy += ey ? (ex ? 0.5f * g : g) : 0.0f;
+}
+CX_DEV void vjp_min(float x, float y, float g, float* gx, float* gy) {
+  const float z = fmin_(x, y);
+  const bool ex = x == z, ey = y == z;
+  *gx += ex ? (ey ? 0.5f * g : g) : 0.0f;
+  *gy += ey ? (ex ? 0.5f * g : g) : 0.0f;
+}
+// jnp.clip(x, lo, hi) = minimum(maximum(x, lo), hi)
+CX_DEV void vjp_clip(float x, float lo, float hi, float g, float* gx, float* glo, float* ghi) {
+  float gt = 0.0f;
+  vjp_min(fmax_(x, lo), hi, g, &gt, ghi);
+  vjp_max(x, lo, gt, gx, glo);
+}
+// d(v / |v|): cotangent g of the unit vector -> cotangent of v
+CX_DEV v2 vjp_unit(v2 v, v2 g) {
+  const float n = nrm(v);
+  const float gn = -dot(g, v) / (n * n);
+  return v2{g.x / n + gn * v.x / n, g.y / n + gn * v.y / n};
+}
+
+// aabb_vs_aabb (cotix/_contacts.py:61-96), contact branch
+CX_DEV void aabb_vs_aabb_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, float* ga, float* gb) {
+  const float alx = a.d[0], aly = a.d[1], aux = a.d[2], auy = a.d[3];
+  const float blx = b.d[0], bly = b.d[1], bux = b.d[2], buy = b.d[3];
+  const float me = -1e-8f;
+  const float X[4] = {auy - bly, buy - aly, aux - blx, bux - alx};
+  float dep[4];
+  for (int q = 0; q < 4; ++q) dep[q] = fmax_(X[q], me);
+  const float dx[4] = {0.0f, 0.0f, -1.0f, 1.0f}, dy[4] = {-1.0f, 1.0f, 0.0f, 0.0f};
+  const int k = argmin_first(dep, 4);
+  const float gmd = gpen.x * dx[k] + gpen.y * dy[k];
+  float gdep = 0.0f, gX = 0.0f, dummy = 0.0f;
+  vjp_max(0.0f, dep[k], gmd, &dummy, &gdep);  // jnp.clip(depth, a_min=0)
+  vjp_max(X[k], me, gdep, &gX, &dummy);
+  switch (k) {
+    case 0: ga[3] += gX; gb[1] -= gX; break;
+    case 1: gb[3] += gX; ga[1] -= gX; break;
+    case 2: ga[2] += gX; gb[0] -= gX; break;
+    default: gb[2] += gX; ga[0] -= gX; break;
+  }
+  const float hx = gcp.x / 2.0f, hy = gcp.y / 2.0f;  // cp = (min(up) + max(lo)) / 2
+  vjp_min(aux, bux, hx, &ga[2], &gb[2]);
+  vjp_min(auy, buy, hy, &ga[3], &gb[3]);
+  vjp_max(alx, blx, hx, &ga[0], &gb[0]);
+  vjp_max(aly, bly, hy, &ga[1], &gb[1]);
+}
+
+// circle_vs_circle (cotix/_contacts.py:30-58), contact branch
+CX_DEV void circle_vs_circle_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, float* ga, float* gb) {
+  const v2 ap = v2{a.d[1], a.d[2]}, bp = v2{b.d[1], b.d[2]};
+  const float ar = a.d[0], br = b.d[0];
+  const v2 delta = sub(ap, bp);
+  const float dist = nrm(delta);
+  const bool zero = dist == 0.0f;
+  const v2 dir = zero ? v2{1.0f, 0.0f} : divs(delta, dist);
+  const float mn = fmin_(dist - (ar + br), 0.0f);
+  const v2 cp0 = divs(add(add(bp, scl(dir, br - ar)), ap), 2.0f);
+  const bool sides = dot(sub(ap, cp0), sub(bp, cp0)) <= 0.0f;
+  v2 gap = v2{0.0f, 0.0f}, gbp = v2{0.0f, 0.0f};
+  const v2 gpr = neg(gpen);  // pen = -(dir * mn)
+  v2 gdir = scl(gpr, mn);
+  float gdist = 0.0f, dummy = 0.0f;
+  vjp_min(dist - (ar + br), 0.0f, dot(gpr, dir), &gdist, &dummy);
+  if (sides) {
+    const v2 h = divs(gcp, 2.0f);
+    gbp = add(gbp, h);
+    gap = add(gap, h);
+    gdir = add(gdir, scl(h, br - ar));
+  } else if (circle_contains(a, bp)) {
+    gbp = add(gbp, gcp);
+  } else {
+    gap = add(gap, gcp);
+  }
+  v2 gdelta = v2{0.0f, 0.0f};
+  if (!zero) {
+    gdelta = divs(gdir, dist);
+    gdist += -dot(gdir, delta) / (dist * dist);
+  }
+  gdelta = add(gdelta, scl(divs(delta, dist), gdist));  // d|delta|
+  gap = add(gap, gdelta);
+  gbp = sub(gbp, gdelta);
+  ga[1] += gap.x;
+  ga[2] += gap.y;
+  gb[1] += gbp.x;
+  gb[2] += gbp.y;
+}
+
+// circle_vs_aabb (cotix/_contacts.py:99-154), contact branch
+CX_DEV void circle_vs_aabb_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, float* ga, float* gb) {
+  const v2 ap = v2{a.d[1], a.d[2]};
+  const float r = a.d[0];
+  const v2 lo = v2{b.d[0], b.d[1]}, up = v2{b.d[2], b.d[3]};
+  const v2 bc = v2{(lo.x + up.x) / 2.0f, (lo.y + up.y) / 2.0f};
+  const v2 disp = sub(ap, bc);
+  const v2 l = sub(lo, bc), h = sub(up, bc);
+  const v2 ccp = add(bc, v2{clip_(disp.x, l.x, h.x), clip_(disp.y, l.y, h.y)});
+  const v2 vs[4] = {lo, v2{lo.x, up.y}, up, v2{up.x, lo.y}};
+  bool perfect = false;
+  for (int k = 0; k < 4; ++k) perfect = perfect || (nrm(sub(vs[k], ccp)) < 1e-6f);
+  v2 gap = v2{0.0f, 0.0f}, glo = v2{0.0f, 0.0f}, gup = v2{0.0f, 0.0f};
+  v2 gccp = gcp;
+  if (perfect) {  // pen = -(ap + r * unit(ccp - ap) - ccp)
+    const v2 d = sub(ccp, ap);
+    gap = sub(gap, gpen);
+    gccp = add(gccp, gpen);
+    const v2 gd = vjp_unit(d, scl(gpen, -r));
+    gccp = add(gccp, gd);
+    gap = sub(gap, gd);
+  } else {  // pen = -shift[k] * dir[k]
+    const float sh[4] = {(ap.y + r) - lo.y, up.y - (ap.y - r), (ap.x + r) - lo.x, up.x - (ap.x - r)};
+    const float dx[4] = {0.0f, 0.0f, 1.0f, -1.0f}, dy[4] = {1.0f, -1.0f, 0.0f, 0.0f};
+    const int k = argmin_first(sh, 4);
+    const float g = -(gpen.x * dx[k] + gpen.y * dy[k]);
+    switch (k) {
+      case 0: gap.y += g; glo.y -= g; break;
+      case 1: gup.y += g; gap.y -= g; break;
+      case 2: gap.x += g; glo.x -= g; break;
+      default: gup.x += g; gap.x -= g; break;
+    }
+  }
+  // ccp = bc + clip(ap - bc, lo - bc, up - bc)
+  v2 gbc = gccp, gdisp = v2{0.0f, 0.0f}, gl = v2{0.0f, 0.0f}, gh = v2{0.0f, 0.0f};
+  vjp_clip(disp.x, l.x, h.x, gccp.x, &gdisp.x, &gl.x, &gh.x);
+  vjp_clip(disp.y, l.y, h.y, gccp.y, &gdisp.y, &gl.y, &gh.y);
+  gap = add(gap, gdisp);
+  gbc = sub(sub(sub(gbc, gdisp), gl), gh);
+  glo = add(add(glo, gl), divs(gbc, 2.0f));
+  gup = add(add(gup, gh), divs(gbc, 2.0f));
+  ga[1] += gap.x;
+  ga[2] += gap.y;
+  gb[0] += glo.x;
+  gb[1] += glo.y;
+  gb[2] += gup.x;
+  gb[3] += gup.y;
+}
+
+// reverse of run_contact for the analytic contacts
+CX_DEV void contact_vjp(int fn, const Shape& a, const Shape& b, v2 gpen, v2 gcp, float* ga, float* gb) {
+  switch (fn) {
+    case FN_AABB_AABB: aabb_vs_aabb_vjp(a, b, gpen, gcp, ga, gb); break;
+    case FN_CIRCLE_CIRCLE: circle_vs_circle_vjp(a, b, gpen, gcp, ga, gb); break;
+    case FN_CIRCLE_AABB: circle_vs_aabb_vjp(a, b, gpen, gcp, ga, gb); break;
+    default: break;  // polygon contacts are not differentiated (rejected on the host)
+  }
+}
+
+// resolve_collision_notnan (cotix/_collision_resolution.py:76-146) in the
+// branch that applies the impulses.  In: the pre-resolution bodies, the
+// cotangents g1/g2 of the post-resolution bodies.  Out: g1/g2 become the
+// cotangents of the pre-resolution bodies; gpen/gcp those of the contact.
+CX_DEV void resolve_vjp(const Dyn& b1, const Params& m1, const Dyn& b2, const Params& m2, v2 pen, v2 cp, Dyn& g1,
+                        Dyn& g2, v2& gpen, v2& gcp) {
+  // forward values (cotix_device.h resolve_collision)
+  const v2 r1 = sub(cp, v2{b1.px, b1.py}), r2 = sub(cp, v2{b2.px, b2.py});
+  const v2 v1 = velocity_at(b1, cp), v2_ = velocity_at(b2, cp);
+  const v2 relv = sub(v2_, v1);
+  const float pn = nrm(pen);
+  const v2 n = v2{pen.x / pn, pen.y / pn};
+  const float vn = dot(relv, n);
+  const float e = fmin_(m1.elast, m2.elast);
+  const float lev1 = r1.x * r1.x + r1.y * r1.y, lev2 = r2.x * r2.x + r2.y * r2.y;
+  const float ang = lev1 / m1.inertia + lev2 / m2.inertia;
+  const float nim = (-(1.0f + e)) * vn - (0.3f * nrm(pen)) / 0.01f;
+  const float den = (1.0f / m1.mass + 1.0f / m2.mass) + ang;
+  const float ni = nim / den;
+  const float mu = (m1.fric + m2.fric) / 2.0f;
+  const v2 vd = v2{relv.x + vn * n.x, relv.y + vn * n.y};
+  const float vdn = nrm(vd);
+  const v2 vdu = v2{vd.x / vdn, vd.y / vdn};
+  const float idr0 = (-vdn) / den;
+  const float idr = clip_(idr0, 0.0f, ni * mu);
+  const v2 imp = add(scl(n, ni), scl(vdu, idr));
+
+  // apply_impulse(b1, -imp, cp); apply_impulse(b2, imp, cp)  (:68-73)
+  v2 gimp = v2{-g1.vx / m1.mass + g2.vx / m2.mass, -g1.vy / m1.mass + g2.vy / m2.mass};
+  v2 gr1 = v2{0.0f, 0.0f}, gr2 = v2{0.0f, 0.0f};
+  {
+    const float c1 = g1.w / m1.inertia;  // w1 += crs(r1, -imp) / I1
+    gr1 = add(gr1, scl(v2{-imp.y, imp.x}, c1));
+    gimp = add(gimp, scl(v2{r1.y, -r1.x}, c1));
+    const float c2 = g2.w / m2.inertia;  // w2 += crs(r2, imp) / I2
+    gr2 = add(gr2, scl(v2{imp.y, -imp.x}, c2));
+    gimp = add(gimp, scl(v2{-r2.y, r2.x}, c2));
+  }
+  // imp = n * ni + vdu * idr
+  v2 gn = scl(gimp, ni);
+  float gni = dot(gimp, n);
+  v2 gvdu = scl(gimp, idr);
+  const float gidr = dot(gimp, vdu);
+  // idr = clip(idr0, 0, ni * mu)
+  float gidr0 = 0.0f, glo = 0.0f, ghi = 0.0f;
+  vjp_clip(idr0, 0.0f, ni * mu, gidr, &gidr0, &glo, &ghi);
+  gni += ghi * mu;
+  // idr0 = -vdn / den
+  float gvdn = -gidr0 / den;
+  float gden = gidr0 * vdn / (den * den);
+  // vdu = vd / vdn ; vdn = |vd|
+  v2 gvd = divs(gvdu, vdn);
+  gvdn += -dot(gvdu, vd) / (vdn * vdn);
+  gvd = add(gvd, scl(divs(vd, vdn), gvdn));
+  // vd = relv + vn * n
+  v2 grelv = gvd;
+  float gvn = dot(gvd, n);
+  gn = add(gn, scl(gvd, vn));
+  // ni = nim / den ; den = 1/m1 + 1/m2 + ang ; ang = lev1/I1 + lev2/I2
+  const float gnim = gni / den;
+  gden += -gni * nim / (den * den);
+  gr1 = add(gr1, scl(r1, 2.0f * (gden / m1.inertia)));
+  gr2 = add(gr2, scl(r2, 2.0f * (gden / m2.inertia)));
+  // nim = -(1 + e) * vn - 0.3 * |pen| / 0.01
+  gvn += -(1.0f + e) * gnim;
+  float gpn = -(0.3f / 0.01f) * gnim;
+  // vn = relv . n
+  grelv = add(grelv, scl(n, gvn));
+  gn = add(gn, scl(relv, gvn));
+  // n = pen / |pen|
+  gpen = add(gpen, vjp_unit(pen, gn));
+  gpen = add(gpen, scl(divs(pen, pn), gpn));
+  // relv = velocity_at(b2, cp) - velocity_at(b1, cp); velocity_at = v + perp(cp - p) * w
+  const v2 gv2c = grelv, gv1c = neg(grelv);
+  Dyn o1 = g1, o2 = g2;  // pass-through of every field
+  o1.vx += gv1c.x;
+  o1.vy += gv1c.y;
+  o1.w += -r1.y * gv1c.x + r1.x * gv1c.y;
+  gr1 = add(gr1, v2{gv1c.y * b1.w, -gv1c.x * b1.w});
+  o2.vx += gv2c.x;
+  o2.vy += gv2c.y;
+  o2.w += -r2.y * gv2c.x + r2.x * gv2c.y;
+  gr2 = add(gr2, v2{gv2c.y * b2.w, -gv2c.x * b2.w});
+  // r = cp - p
+  gcp = add(gcp, add(gr1, gr2));
+  o1.px -= gr1.x;
+  o1.py -= gr1.y;
+  o2.px -= gr2.x;
+  o2.py -= gr2.y;
+  g1 = o1;
+  g2 = o2;
+}
+
+}  // namespace cx

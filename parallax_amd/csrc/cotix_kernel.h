@@ -27,6 +27,7 @@
 #pragma once
 #include "../../include/cotix_amd.h"
 #include "cotix_device.h"
+#include "cotix_grad.h"
 
 namespace cxk {
 
@@ -60,13 +61,21 @@ struct KArgs {
   const float* dyn_reset;  // [nb][6][B] or null
   uint32_t* resets;        // [B] or null
   int dbg_skip;            // debug only: bit k skips collider phase k (T=1,B=2,C=4,D=8)
+  // differentiable rollout (cotix_rollout / cotix_rollout_backward)
+  float* save_dyn;         // [n_steps][nb*6][B]: state before each step, or null
+  uint32_t* save_keys;     // [n_steps][B][2]
+  float* ret;              // [B] += sum_t sum_k ret_w[k] * state_{t+1}[k] (terms with ret_w[k] == 0 skipped)
+  float* grad_action;      // backward: [n_steps][B][2] d ret / d action
+  float* grad_dyn;         // backward: [nb*6][B] d ret / d initial state, or null
+  float ret_w[MAXB * 6];
 };
 
 // per-wave tile layout (words, each x EW envs)
 struct Lay {
-  int dyn, world, con, m, ch, key, sk0, skt, err, nres, S;
+  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, S;
 };
-CX_DEV Lay layout(int nb, int W, int nc, int nt) {
+constexpr int REC_W = 7;  // per resolution: applied flag, v/w of body i, v/w of body j (pre-resolution)
+CX_HD Lay layout(int nb, int W, int nc, int nt) {
   Lay L;
   L.dyn = 0;
   L.world = L.dyn + nb * 6;
@@ -78,12 +87,13 @@ CX_DEV Lay layout(int nb, int W, int nc, int nt) {
   L.skt = L.sk0 + 2;
   L.err = L.skt + 2 * nt;
   L.nres = L.err + 1;
-  L.S = L.nres + 1;
+  L.ret = L.nres + 1;
+  L.adj = L.ret + 1;
+  L.rec = L.adj + nb * 6;
+  L.S = L.rec + nb * REC_W;
   return L;
 }
-static inline int tile_words(const SceneDev& s) {
-  return s.nb * 6 + s.W + s.nc * 4 + s.nb * s.nb + s.nb + 4 + 2 * s.nt + 2;
-}
+static inline int tile_words(const SceneDev& s) { return layout(s.nb, s.W, s.nc, s.nt).S; }
 // LDS bytes of a workgroup of wpb waves x ew envs
 static inline size_t lds_bytes(const SceneDev& s, int wpb, int ew) {
   return 4 * ((size_t)s.nhot + (size_t)tile_words(s) * ew * wpb);
@@ -441,8 +451,10 @@ CX_DEV cx::Params load_par(const uint32_t* tb, int o) {
                     __uint_as_float(tb[o + 3])};
 }
 
-// phase E: sequential resolution (:310-336), joints, key update, restarts
-template <int EW>
+// phase E: sequential resolution (:310-336), joints, key update, restarts.
+// REC (backward re-play only): record, per resolution, whether the impulses
+// were applied and the pre-resolution velocities of the two bodies.
+template <int EW, bool REC = false>
 CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
   const SceneDev& sc = *c.sc;
@@ -453,6 +465,7 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     if (g >= a.B) continue;
     if (a.stages & COTIX_STAGE_COLLIDER) {
       for (int i = 0; i < nb; ++i) {
+        if (REC) t.w(L.rec + REC_W * i, e) = 0u;
         const int j = (int)t.w(L.ch + i, e);
         if (j == i || j < 0 || j >= nb) continue;
         const int cid = (int)t.w(L.m + i * nb + j, e);
@@ -460,8 +473,19 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
         const int co = L.con + 4 * cid, oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
         Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), t.f(oi + 2, e), t.f(oi + 3, e), t.f(oi + 4, e), t.f(oi + 5, e)};
         Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), t.f(oj + 2, e), t.f(oj + 3, e), t.f(oj + 4, e), t.f(oj + 5, e)};
-        resolve_collision(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
-                          v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)});
+        if (REC) {
+          const int ro = L.rec + REC_W * i;
+          t.f(ro + 1, e) = bi.vx;
+          t.f(ro + 2, e) = bi.vy;
+          t.f(ro + 3, e) = bi.w;
+          t.f(ro + 4, e) = bj.vx;
+          t.f(ro + 5, e) = bj.vy;
+          t.f(ro + 6, e) = bj.w;
+        }
+        const bool applied =
+            resolve_collision(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
+                              v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)});
+        if (REC) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
         t.f(oi + 2, e) = bi.vx;
         t.f(oi + 3, e) = bi.vy;
         t.f(oi + 5, e) = bi.w;
@@ -514,32 +538,208 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
       a.keys[2 * (size_t)g + 1] = t.w(c.L.key + 1, e);
       a.err[g] = t.w(c.L.err, e);
       if (a.resets) a.resets[g] += t.w(c.L.nres, e);
+      if (a.ret) a.ret[g] += t.f(c.L.ret, e);
     }
   }
 }
 
-// the whole launch for one wave (lane = 0..63), after the hot tables are in LDS
-template <int EW, int FNSET>
-CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
-  ph_load<EW>(a, c, t, env0, lane);
-  wave_sync();
-  for (int step = 0; step < a.n_steps; ++step) {
-    ph_A<EW>(a, c, t, env0, lane, step);
-    wave_sync();
-    if (a.stages & COTIX_STAGE_COLLIDER) {
-      if (!(a.dbg_skip & 1)) ph_T<EW, FNSET>(a, c, t, env0, lane);
-      wave_sync();
-      if (!(a.dbg_skip & 2)) ph_B<EW, FNSET>(a, c, t, env0, lane);
-      wave_sync();
-      if (!(a.dbg_skip & 4)) ph_C<EW>(a, c, t, env0, lane);
-      wave_sync();
-      if (!(a.dbg_skip & 8)) ph_D<EW>(a, c, t, env0, lane);
-      wave_sync();
-    }
-    ph_E<EW>(a, c, t, env0, lane);
-    wave_sync();
+// ---------------------------------------------------------------------------
+// differentiable rollout: forward saves, return, backward re-play
+// ---------------------------------------------------------------------------
+// state before step `step` -> save_dyn[step], save_keys[step]
+template <int EW>
+CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+  const size_t base = (size_t)step * c.nb * 6 * a.B;
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    int e = w % EW, off = w / EW, g = env0 + e;
+    if (g < a.B) a.save_dyn[base + (size_t)off * a.B + g] = t.f(c.L.dyn + off, e);
   }
-  ph_store<EW>(a, c, t, env0, lane);
+  for (int e = lane; e < EW; e += WAVE) {
+    int g = env0 + e;
+    if (g < a.B) {
+      a.save_keys[2 * ((size_t)step * a.B + g)] = t.w(c.L.key, e);
+      a.save_keys[2 * ((size_t)step * a.B + g) + 1] = t.w(c.L.key + 1, e);
+    }
+  }
+}
+
+// return accumulation after a step: ret += sum_k w_k * state_k (w_k != 0)
+template <int EW>
+CX_DEV void ph_ret(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  for (int e = lane; e < EW; e += WAVE) {
+    if (env0 + e >= a.B) continue;
+    float acc = t.f(c.L.ret, e);
+    for (int k = 0; k < c.nb * 6; ++k)
+      if (a.ret_w[k] != 0.0f) acc = acc + a.ret_w[k] * t.f(c.L.dyn + k, e);
+    t.f(c.L.ret, e) = acc;
+  }
+}
+
+// backward: state before step `step` from the saved trajectory
+template <int EW>
+CX_DEV void ph_restore(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+  const size_t base = (size_t)step * c.nb * 6 * a.B;
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    int e = w % EW, off = w / EW, g = env0 + e;
+    t.f(c.L.dyn + off, e) = (g < a.B) ? a.save_dyn[base + (size_t)off * a.B + g] : 0.0f;
+  }
+  for (int e = lane; e < EW; e += WAVE) {
+    int g = env0 + e;
+    t.w(c.L.key, e) = (g < a.B) ? a.save_keys[2 * ((size_t)step * a.B + g)] : 0u;
+    t.w(c.L.key + 1, e) = (g < a.B) ? a.save_keys[2 * ((size_t)step * a.B + g) + 1] : 0u;
+    t.w(c.L.err, e) = 0u;
+  }
+}
+
+template <int EW>
+CX_DEV void ph_adj_init(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    int e = w % EW, off = w / EW;
+    t.f(c.L.adj + off, e) = a.ret_w[off];  // d ret / d state_T
+  }
+}
+
+// phase G: reverse of one step (one lane per env).  Entry: adj = d ret /
+// d state_{step+1}; the tile holds the re-played step (post-Euler positions,
+// contacts, choices, recorded pre-resolution velocities).  Exit: adj = d ret
+// / d state_step, grad_action[step] written.
+template <int EW>
+CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+  using namespace cx;
+  const SceneDev& sc = *c.sc;
+  const int nb = c.nb;
+  const Lay& L = c.L;
+  for (int e = lane; e < EW; e += WAVE) {
+    const int g = env0 + e;
+    if (g >= a.B) continue;
+    if (a.stages & COTIX_STAGE_COLLIDER) {
+      for (int i = nb - 1; i >= 0; --i) {  // resolutions in reverse order
+        const int ro = L.rec + REC_W * i;
+        if (t.w(ro, e) == 0u) continue;
+        const int j = (int)t.w(L.ch + i, e);
+        const int cid = (int)t.w(L.m + i * nb + j, e);
+        const int co = L.con + 4 * cid, oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
+        const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), t.f(ro + 1, e), t.f(ro + 2, e), t.f(oi + 4, e), t.f(ro + 3, e)};
+        const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), t.f(ro + 4, e), t.f(ro + 5, e), t.f(oj + 4, e), t.f(ro + 6, e)};
+        const int ai = L.adj + 6 * i, aj = L.adj + 6 * j;
+        Dyn gi = Dyn{t.f(ai, e), t.f(ai + 1, e), t.f(ai + 2, e), t.f(ai + 3, e), t.f(ai + 4, e), t.f(ai + 5, e)};
+        Dyn gj = Dyn{t.f(aj, e), t.f(aj + 1, e), t.f(aj + 2, e), t.f(aj + 3, e), t.f(aj + 4, e), t.f(aj + 5, e)};
+        v2 gpen = v2{0.0f, 0.0f}, gcp = v2{0.0f, 0.0f};
+        resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
+                    v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp);
+        // the contact: fn(world(part pa), world(part pb)); world = local + body position
+        const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
+        const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
+        Shape SA, SB;
+        SA.kind = ka;
+        SB.kind = kb;
+        SA.n = SB.n = 0;
+        const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
+        for (int k = 0; k < 4; ++k) {
+          SA.d[k] = t.f(wa + k, e);
+          SB.d[k] = t.f(wb + k, e);
+        }
+        float ga[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        contact_vjp(fn, SA, SB, gpen, gcp, ga, gb);
+        t.f(ai, e) = gi.px;
+        t.f(ai + 1, e) = gi.py;
+        t.f(ai + 2, e) = gi.vx;
+        t.f(ai + 3, e) = gi.vy;
+        t.f(ai + 4, e) = gi.a;
+        t.f(ai + 5, e) = gi.w;
+        t.f(aj, e) = gj.px;
+        t.f(aj + 1, e) = gj.py;
+        t.f(aj + 2, e) = gj.vx;
+        t.f(aj + 3, e) = gj.vy;
+        t.f(aj + 4, e) = gj.a;
+        t.f(aj + 5, e) = gj.w;
+        const int qa = L.adj + 6 * t.ti(sc.o_pbody + pa), qb = L.adj + 6 * t.ti(sc.o_pbody + pb);
+        if (ka == KIND_CIRCLE) {
+          t.f(qa, e) = t.f(qa, e) + ga[1];
+          t.f(qa + 1, e) = t.f(qa + 1, e) + ga[2];
+        } else {
+          t.f(qa, e) = t.f(qa, e) + (ga[0] + ga[2]);
+          t.f(qa + 1, e) = t.f(qa + 1, e) + (ga[1] + ga[3]);
+        }
+        if (kb == KIND_CIRCLE) {
+          t.f(qb, e) = t.f(qb, e) + gb[1];
+          t.f(qb + 1, e) = t.f(qb + 1, e) + gb[2];
+        } else {
+          t.f(qb, e) = t.f(qb, e) + (gb[0] + gb[2]);
+          t.f(qb + 1, e) = t.f(qb + 1, e) + (gb[1] + gb[3]);
+        }
+      }
+    }
+    if (a.action != nullptr && a.grad_action != nullptr) {  // v[action_body] += action[step]
+      const int o = L.adj + 6 * a.action_body;
+      a.grad_action[2 * ((size_t)step * a.B + g)] = t.f(o + 2, e);
+      a.grad_action[2 * ((size_t)step * a.B + g) + 1] = t.f(o + 3, e);
+    }
+    for (int b = 0; b < nb; ++b) {
+      const int o = L.adj + 6 * b;
+      if (a.stages & COTIX_STAGE_EULER) {  // p += v dt, angle += w dt
+        t.f(o + 2, e) = t.f(o + 2, e) + t.f(o + 0, e) * a.dt;
+        t.f(o + 3, e) = t.f(o + 3, e) + t.f(o + 1, e) * a.dt;
+        t.f(o + 5, e) = t.f(o + 5, e) + t.f(o + 4, e) * a.dt;
+      }
+      if (step > 0)
+        for (int k = 0; k < 6; ++k) t.f(o + k, e) = t.f(o + k, e) + a.ret_w[6 * b + k];
+    }
+  }
+}
+
+template <int EW>
+CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  if (a.grad_dyn == nullptr) return;
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    int e = w % EW, off = w / EW, g = env0 + e;
+    if (g < a.B) a.grad_dyn[(size_t)off * a.B + g] = t.f(c.L.adj + off, e);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// the wave programs.  R runs one phase over the wave's lanes and orders it
+// before the next: on the GPU R = this lane + wave_sync(); in the CPU
+// emulation of the tests R loops over the 64 lanes.
+// ---------------------------------------------------------------------------
+template <int EW, int FNSET, class R>
+CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
+  if (!(a.dbg_skip & 1)) run([&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
+  if (!(a.dbg_skip & 2)) run([&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
+  if (!(a.dbg_skip & 4)) run([&](int l) { ph_C<EW>(a, c, t, env0, l); });
+  if (!(a.dbg_skip & 8)) run([&](int l) { ph_D<EW>(a, c, t, env0, l); });
+}
+
+// forward: n_steps fused steps (+ optional trajectory save and return)
+template <int EW, int FNSET, class R>
+CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
+  run([&](int l) {
+    ph_load<EW>(a, c, t, env0, l);
+    for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
+  });
+  for (int step = 0; step < a.n_steps; ++step) {
+    if (a.save_dyn != nullptr) run([&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
+    run([&](int l) { ph_A<EW>(a, c, t, env0, l, step); });
+    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET>(a, c, t, env0, run);
+    run([&](int l) { ph_E<EW>(a, c, t, env0, l); });
+    if (a.ret != nullptr) run([&](int l) { ph_ret<EW>(a, c, t, env0, l); });
+  }
+  run([&](int l) { ph_store<EW>(a, c, t, env0, l); });
+}
+
+// backward: steps n_steps-1 .. 0, each re-played from the saved state (so
+// every discrete choice is the forward's) and then reversed by phase G
+template <int EW, int FNSET, class R>
+CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
+  run([&](int l) { ph_adj_init<EW>(a, c, t, env0, l); });
+  for (int step = a.n_steps - 1; step >= 0; --step) {
+    run([&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });
+    run([&](int l) { ph_A<EW>(a, c, t, env0, l, step); });
+    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET>(a, c, t, env0, run);
+    run([&](int l) { ph_E<EW, true>(a, c, t, env0, l); });
+    run([&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
+  }
+  run([&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });
 }
 
 }  // namespace cxk

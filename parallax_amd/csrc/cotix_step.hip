@@ -43,7 +43,16 @@ namespace {
 // the fused step kernel: WPB independent waves per workgroup, EW envs per wave
 // ---------------------------------------------------------------------------
 constexpr int WPB = 4;
-template <int EW, int FNSET>
+// one phase on this lane, then wave-local ordering before the next phase
+struct WaveRun {
+  int lane;
+  template <class F>
+  __device__ __forceinline__ void operator()(F f) const {
+    f(lane);
+    cxk::wave_sync();
+  }
+};
+template <int EW, int FNSET, bool BWD>
 __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   extern __shared__ uint32_t lds[];
   const SceneDev* sc = a.sc;
@@ -55,7 +64,10 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   const int env0 = (blockIdx.x * WPB + wave) * EW;
   if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
   const cxk::Tile<EW> t{lds + nhot + wave * c.L.S * EW, lds};
-  cxk::run_wave<EW, FNSET>(a, c, t, env0, lane);
+  if (BWD)
+    cxk::run_wave_backward<EW, FNSET>(a, c, t, env0, WaveRun{lane});
+  else
+    cxk::run_wave<EW, FNSET>(a, c, t, env0, WaveRun{lane});
 }
 
 // ---------------------------------------------------------------------------
@@ -208,41 +220,71 @@ static int envs_per_wave() {
   return (e == 1 || e == 2 || e == 4 || e == 8) ? e : 4;
 }
 
-static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
-                     int geom_stride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
-                     const float* dyn_reset, uint32_t* resets, cotix_stream_t stream) {
-  if (!scene || !dyn || !keys || !err) return fail("null argument");
+static int check_step_args(const cotix_scene* scene, const float* dyn, const uint32_t* keys, const float* geom,
+                           int geom_stride, int B, int n_steps, int stages, const float* action, int action_body) {
+  if (!scene || !dyn || !keys) return fail("null argument");
   if ((stages & COTIX_STAGE_COLLIDER) && !geom) return fail("geometry required for the collider stage");
   if (geom_stride != 0 && geom_stride < scene->host.G) return fail("geom_stride smaller than the scene geometry");
-  if (B <= 0 || n_steps <= 0) return B == 0 || n_steps == 0 ? 0 : fail("negative size");
+  if (B < 0 || n_steps < 0) return fail("negative size");
   if ((stages & COTIX_STAGE_LUNAR) && scene->host.nb < 3) return fail("LunarLander stage needs >= 3 bodies");
   if (action && (action_body < 0 || action_body >= scene->host.nb)) return fail("action_body out of range");
+  return 0;
+}
+
+// launch the fused step kernel (forward, or backward re-play when bwd)
+static int launch(cotix_scene* scene, const cxk::KArgs& ka0, bool bwd, cotix_stream_t stream) {
   if (scene_upload(scene)) return -1;
   const int EW = envs_per_wave();
   const size_t lds = cxk::lds_bytes(scene->host, WPB, EW);
   if (lds > 160 * 1024) return fail("scene too large for the LDS tile");
-  dim3 grid((B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  cxk::KArgs ka = ka0;
+  ka.sc = scene->dev;
   const char* dbg = getenv("COTIX_DEBUG_SKIP");
-  cxk::KArgs ka{scene->dev, dyn,    keys,        err,       geom,   geom_stride,          B, n_steps, dt, stages,
-                action,     action_body, dyn_reset, resets, dbg ? atoi(dbg) : 0};
+  ka.dbg_skip = dbg ? atoi(dbg) : 0;
+  dim3 grid((ka.B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int fs = scene->fnset;
-#define COTIX_LAUNCH(EE, FS) hipLaunchKernelGGL((step_kernel<EE, FS>), grid, block, lds, st, ka)
-#define COTIX_LAUNCH_E(FS)                \
-  if (EW == 1) COTIX_LAUNCH(1, FS);       \
-  else if (EW == 8) COTIX_LAUNCH(8, FS);  \
-  else if (EW == 2) COTIX_LAUNCH(2, FS);  \
-  else COTIX_LAUNCH(4, FS);
-  if ((fs & ~FNS_ANALYTIC) == 0) {
-    COTIX_LAUNCH_E(FNS_ANALYTIC)
+#define COTIX_LAUNCH(EE, FS, BW) hipLaunchKernelGGL((step_kernel<EE, FS, BW>), grid, block, lds, st, ka)
+#define COTIX_LAUNCH_E(FS, BW)                \
+  if (EW == 1) COTIX_LAUNCH(1, FS, BW);       \
+  else if (EW == 8) COTIX_LAUNCH(8, FS, BW);  \
+  else if (EW == 2) COTIX_LAUNCH(2, FS, BW);  \
+  else COTIX_LAUNCH(4, FS, BW);
+  if (bwd) {
+    COTIX_LAUNCH_E(FNS_ANALYTIC, true)  // the host admits analytic scenes only
+  } else if ((fs & ~FNS_ANALYTIC) == 0) {
+    COTIX_LAUNCH_E(FNS_ANALYTIC, false)
   } else if ((fs & FNS_CIRCLE_POLY) == 0) {
-    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX)
+    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX, false)
   } else {
-    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY)
+    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, false)
   }
 #undef COTIX_LAUNCH_E
 #undef COTIX_LAUNCH
   return hip_check(hipGetLastError(), "step_kernel launch");
+}
+
+static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
+                     int geom_stride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                     const float* dyn_reset, uint32_t* resets, cotix_stream_t stream) {
+  if (check_step_args(scene, dyn, keys, geom, geom_stride, B, n_steps, stages, action, action_body)) return -1;
+  if (!err) return fail("null argument");
+  if (B == 0 || n_steps == 0) return 0;
+  cxk::KArgs ka{};
+  ka.dyn = dyn;
+  ka.keys = keys;
+  ka.err = err;
+  ka.geom = geom;
+  ka.gstride = geom_stride;
+  ka.B = B;
+  ka.n_steps = n_steps;
+  ka.dt = dt;
+  ka.stages = stages;
+  ka.action = action;
+  ka.action_body = action_body;
+  ka.dyn_reset = dyn_reset;
+  ka.resets = resets;
+  return launch(scene, ka, false, stream);
 }
 
 int cotix_step(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
@@ -258,6 +300,63 @@ int cotix_step_autoreset(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_
   if (!dyn_reset) return fail("dyn_reset required");
   return step_impl(scene, dyn, keys, err, geom, geom_stride, B, n_steps, dt, stages, nullptr, 0, dyn_reset, resets,
                    stream);
+}
+
+int cotix_rollout(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
+                  int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                  const float* ret_weights, float* ret, float* saved_dyn, uint32_t* saved_keys, cotix_stream_t stream) {
+  if (check_step_args(scene, dyn, keys, geom, geom_stride, B, n_steps, stages, action, action_body)) return -1;
+  if (!err || !ret_weights || !ret || !saved_dyn || !saved_keys) return fail("null argument");
+  if (B == 0 || n_steps == 0) return 0;
+  cxk::KArgs ka{};
+  ka.dyn = dyn;
+  ka.keys = keys;
+  ka.err = err;
+  ka.geom = geom;
+  ka.gstride = geom_stride;
+  ka.B = B;
+  ka.n_steps = n_steps;
+  ka.dt = dt;
+  ka.stages = stages;
+  ka.action = action;
+  ka.action_body = action_body;
+  ka.save_dyn = saved_dyn;
+  ka.save_keys = saved_keys;
+  ka.ret = ret;
+  for (int k = 0; k < scene->host.nb * 6; ++k) ka.ret_w[k] = ret_weights[k];
+  return launch(scene, ka, false, stream);
+}
+
+int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uint32_t* saved_keys, const float* geom,
+                           int geom_stride, int B, int n_steps, float dt, int stages, const float* action,
+                           int action_body, const float* ret_weights, float* grad_action, float* grad_dyn0,
+                           cotix_stream_t stream) {
+  if (check_step_args(scene, saved_dyn, saved_keys, geom, geom_stride, B, n_steps, stages, action, action_body))
+    return -1;
+  if (!ret_weights) return fail("null argument");
+  if (grad_action && !action) return fail("grad_action needs the action the rollout was run with");
+  if (scene->fnset & ~FNS_ANALYTIC)
+    return fail("differentiable rollout: polygon contacts (GJK/EPA) are not differentiated; circle/AABB scenes only");
+  if (stages & COTIX_STAGE_LUNAR) return fail("differentiable rollout: the LunarLander joint stage is not supported");
+  if (B == 0 || n_steps == 0) return 0;
+  cxk::KArgs ka{};
+  ka.dyn = nullptr;
+  ka.keys = nullptr;
+  ka.err = nullptr;
+  ka.geom = geom;
+  ka.gstride = geom_stride;
+  ka.B = B;
+  ka.n_steps = n_steps;
+  ka.dt = dt;
+  ka.stages = stages;
+  ka.action = action;
+  ka.action_body = action_body;
+  ka.save_dyn = const_cast<float*>(saved_dyn);
+  ka.save_keys = const_cast<uint32_t*>(saved_keys);
+  ka.grad_action = grad_action;
+  ka.grad_dyn = grad_dyn0;
+  for (int k = 0; k < scene->host.nb * 6; ++k) ka.ret_w[k] = ret_weights[k];
+  return launch(scene, ka, true, stream);
 }
 
 int cotix_physics_euler(float* dyn, int n_bodies, int B, float dt, cotix_stream_t stream) {

@@ -1,0 +1,92 @@
+"""Differentiable fused rollout (BASELINE config 5): grad(return)/d(action)
+through an n-step rollout, forward and backward as HIP kernels
+(cotix_rollout / cotix_rollout_backward, include/cotix_amd.h).
+
+The reference defines neither action nor return (cotix/_envs.py:9-28 is
+abstract); SURVEY.md 8(d) fixes them: action[t] (f32[B,2]) is added to the
+velocity of `action_body` right after Euler -- where the LunarLander driver
+adds gravity (examples/test_viz.py:27-31) -- and the return is
+    R[env] = sum_{t=1..T} sum_k w[k] * state_t[k]      (terms with w[k] == 0 skipped)
+over the n_bodies*6 state words (default: the ball's x position, body 4 of
+RoboCup).  Derivatives are jax.grad's through the reference: the executed
+branch of every lax.cond, RandomizedCollider choices held fixed, balanced
+ties for max/min/clip.  Circle/AABB scenes only (no GJK/EPA derivative).
+"""
+import numpy as np
+import torch
+
+from . import _ffi
+
+
+def ball_x_weights(n_bodies, body=4, coord=0):
+    w = np.zeros(n_bodies * 6, np.float32)
+    w[body * 6 + coord] = 1.0
+    return w
+
+
+def _weights(world, w):
+    nb = len(world.bodies)
+    w = ball_x_weights(nb, nb - 1) if w is None else np.ascontiguousarray(np.asarray(w, np.float32).reshape(-1))
+    if w.shape != (nb * 6,):
+        raise ValueError("return weights must have n_bodies*6 entries")
+    return w
+
+
+def _check_actions(world, actions):
+    actions = actions.to(world.device, torch.float32).contiguous()
+    if actions.dim() != 3 or actions.shape[1:] != (world.B, 2):
+        raise ValueError("actions must be [T, B, 2]")
+    return actions
+
+
+def rollout_forward(world, actions, action_body=None, ret_weights=None, dt=1e-2, stages=_ffi.STAGES_ROBOCUP):
+    """Run T = actions.shape[0] fused steps (world state advanced in place)
+    and save the trajectory.  Returns (ret [B], saved) for rollout_backward."""
+    actions = _check_actions(world, actions)
+    nb, B, T = len(world.bodies), world.B, actions.shape[0]
+    action_body = nb - 1 if action_body is None else int(action_body)
+    w = _weights(world, ret_weights)
+    saved_dyn = torch.empty(T, nb, 6, B, device=world.device, dtype=torch.float32)
+    saved_keys = torch.empty(T, B, 2, device=world.device, dtype=torch.int32)
+    ret = torch.zeros(B, device=world.device, dtype=torch.float32)
+    _ffi.check(_ffi.lib.cotix_rollout(
+        world.scene.handle, _ffi.ptr(world.dyn), _ffi.ptr(world.keys), _ffi.ptr(world.err), _ffi.ptr(world.geom),
+        world.geom_stride, B, T, float(dt), int(stages), _ffi.ptr(actions), action_body,
+        w.ctypes.data_as(_ffi._P), _ffi.ptr(ret), _ffi.ptr(saved_dyn), _ffi.ptr(saved_keys),
+        _ffi.stream_ptr(world.device)), "cotix_rollout")
+    saved = dict(dyn=saved_dyn, keys=saved_keys, actions=actions, action_body=action_body, w=w, dt=float(dt),
+                 stages=int(stages))
+    return ret, saved
+
+
+def rollout_backward(world, saved, want_dyn0=False):
+    """d ret / d actions [T, B, 2] (and d ret / d initial state [nb, 6, B])."""
+    nb, B = len(world.bodies), world.B
+    T = saved["actions"].shape[0]
+    ga = torch.empty(T, B, 2, device=world.device, dtype=torch.float32)
+    gd = torch.empty(nb, 6, B, device=world.device, dtype=torch.float32) if want_dyn0 else None
+    _ffi.check(_ffi.lib.cotix_rollout_backward(
+        world.scene.handle, _ffi.ptr(saved["dyn"]), _ffi.ptr(saved["keys"]), _ffi.ptr(world.geom),
+        world.geom_stride, B, T, saved["dt"], saved["stages"], _ffi.ptr(saved["actions"]), saved["action_body"],
+        saved["w"].ctypes.data_as(_ffi._P), _ffi.ptr(ga), _ffi.ptr(gd), _ffi.stream_ptr(world.device)),
+        "cotix_rollout_backward")
+    return ga, gd
+
+
+class _Rollout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, actions, world, action_body, ret_weights, dt, stages):
+        ret, saved = rollout_forward(world, actions.detach(), action_body, ret_weights, dt, stages)
+        ctx.world, ctx.saved = world, saved
+        return ret
+
+    @staticmethod
+    def backward(ctx, g_ret):
+        ga, _ = rollout_backward(ctx.world, ctx.saved)
+        return ga * g_ret.to(ga.dtype)[None, :, None], None, None, None, None, None
+
+
+def rollout(world, actions, action_body=None, ret_weights=None, dt=1e-2, stages=_ffi.STAGES_ROBOCUP):
+    """R[env] (differentiable w.r.t. actions via torch.autograd); advances
+    `world` by T steps in place."""
+    return _Rollout.apply(actions, world, action_body, ret_weights, dt, stages)

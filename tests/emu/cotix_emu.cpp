@@ -20,33 +20,38 @@ struct EmuScene {
   int n_cand = 0, fnset = 0;
 };
 
-// one wave at a time (waves are independent); within a wave every phase
-// runs for all 64 lanes before the next (what wave_sync() guarantees)
+// a phase runs for all 64 lanes of the wave before the next starts (what
+// wave_sync() guarantees on the GPU)
+struct HostRun {
+  template <class F>
+  void operator()(F f) const {
+    for (int l = 0; l < cxk::WAVE; ++l) f(l);
+  }
+};
+
+// one wave at a time (waves are independent), through the kernel's own
+// wave programs (cxk::run_wave / run_wave_backward)
 template <int EW>
-void run_blocks(const cxk::KArgs& a) {
+void run_blocks(const cxk::KArgs& a, bool bwd) {
   const cxk::SceneDev& sc = *a.sc;
   const cxk::Ctx c{sc.nb, sc.np, sc.nc, sc.nl, sc.nt, &sc, cxk::layout(sc.nb, sc.W, sc.nc, sc.nt)};
   const int nwaves = (a.B + EW - 1) / EW;
   std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)c.L.S * EW);
   for (int q = 0; q < sc.nhot; ++q) lds[q] = sc.hot[q];
-  const int W = cxk::WAVE;
   for (int wv = 0; wv < nwaves; ++wv) {
     std::fill(lds.begin() + sc.nhot, lds.end(), 0x7FBADBADu);  // poison (a NaN pattern)
     const cxk::Tile<EW> t{lds.data() + sc.nhot, lds.data()};
-    const int env0 = wv * EW;
-    for (int l = 0; l < W; ++l) cxk::ph_load<EW>(a, c, t, env0, l);
-    for (int step = 0; step < a.n_steps; ++step) {
-      for (int l = 0; l < W; ++l) cxk::ph_A<EW>(a, c, t, env0, l, step);
-      if (a.stages & COTIX_STAGE_COLLIDER) {
-        for (int l = 0; l < W; ++l) cxk::ph_T<EW, 7>(a, c, t, env0, l);
-        for (int l = 0; l < W; ++l) cxk::ph_B<EW, 7>(a, c, t, env0, l);
-        for (int l = 0; l < W; ++l) cxk::ph_C<EW>(a, c, t, env0, l);
-        for (int l = 0; l < W; ++l) cxk::ph_D<EW>(a, c, t, env0, l);
-      }
-      for (int l = 0; l < W; ++l) cxk::ph_E<EW>(a, c, t, env0, l);
-    }
-    for (int l = 0; l < W; ++l) cxk::ph_store<EW>(a, c, t, env0, l);
+    if (bwd)
+      cxk::run_wave_backward<EW, 7>(a, c, t, wv * EW, HostRun{});
+    else
+      cxk::run_wave<EW, 7>(a, c, t, wv * EW, HostRun{});
   }
+}
+void run_any(const cxk::KArgs& a, int E, bool bwd) {
+  if (E == 1) run_blocks<1>(a, bwd);
+  else if (E == 4) run_blocks<4>(a, bwd);
+  else if (E == 8) run_blocks<8>(a, bwd);
+  else run_blocks<2>(a, bwd);
 }
 }  // namespace
 
@@ -75,10 +80,59 @@ int emu_step(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float
              uint32_t* resets, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
   cxk::KArgs a{&s->s, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, action, action_body, dyn_reset, resets, 0};
-  if (E == 1) run_blocks<1>(a);
-  else if (E == 4) run_blocks<4>(a);
-  else if (E == 8) run_blocks<8>(a);
-  else run_blocks<2>(a);
+  run_any(a, E, false);
+  return 0;
+}
+
+int emu_rollout(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
+                int n_steps, float dt, int stages, const float* action, int action_body, const float* ret_w, float* ret,
+                float* saved_dyn, uint32_t* saved_keys, int E) {
+  EmuScene* s = static_cast<EmuScene*>(scene);
+  cxk::KArgs a{};
+  a.sc = &s->s;
+  a.dyn = dyn;
+  a.keys = keys;
+  a.err = err;
+  a.geom = geom;
+  a.gstride = gstride;
+  a.B = B;
+  a.n_steps = n_steps;
+  a.dt = dt;
+  a.stages = stages;
+  a.action = action;
+  a.action_body = action_body;
+  a.save_dyn = saved_dyn;
+  a.save_keys = saved_keys;
+  a.ret = ret;
+  for (int k = 0; k < s->s.nb * 6; ++k) a.ret_w[k] = ret_w[k];
+  run_any(a, E, false);
+  return 0;
+}
+
+int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* saved_keys, const float* geom,
+                         int gstride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                         const float* ret_w, float* grad_action, float* grad_dyn0, int E) {
+  EmuScene* s = static_cast<EmuScene*>(scene);
+  if (s->fnset & ~1) {
+    g_err = "differentiable rollout: circle/AABB scenes only";
+    return -1;
+  }
+  cxk::KArgs a{};
+  a.sc = &s->s;
+  a.geom = geom;
+  a.gstride = gstride;
+  a.B = B;
+  a.n_steps = n_steps;
+  a.dt = dt;
+  a.stages = stages;
+  a.action = action;
+  a.action_body = action_body;
+  a.save_dyn = const_cast<float*>(saved_dyn);
+  a.save_keys = const_cast<uint32_t*>(saved_keys);
+  a.grad_action = grad_action;
+  a.grad_dyn = grad_dyn0;
+  for (int k = 0; k < s->s.nb * 6; ++k) a.ret_w[k] = ret_w[k];
+  run_any(a, E, true);
   return 0;
 }
 

@@ -16,6 +16,10 @@ def load(asan=False):
     lib.emu_step.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                              ctypes.c_int, P_, ctypes.c_int, P_, P_, ctypes.c_int]
     lib.emu_contacts.argtypes = [ctypes.c_int, ctypes.c_int, P_, P_, P_, P_]
+    lib.emu_rollout.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, ctypes.c_int]
+    lib.emu_rollout_backward.argtypes = [P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                         ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.c_int]
     lib.emu_last_error.restype = ctypes.c_char_p
     return lib
 
@@ -60,3 +64,30 @@ def step(lib, h, dyn, keys, err, geom, gstride, n_steps, stages, dt=1e-2, E=16, 
         assert a.flags.c_contiguous
     lib.emu_step(h, _p(dyn), _p(keys), _p(err), _p(geom), gstride, B, n_steps, dt, stages, None, 0,
                  _p(dyn_reset), _p(resets), E)
+
+
+def rollout(lib, h, dyn, keys, err, geom, gstride, stages, actions, action_body, w, dt=1e-2, E=4):
+    """Forward of the differentiable rollout; returns (ret [B], saved_dyn
+    [T,nb,6,B], saved_keys [T,B,2]); dyn/keys/err advanced in place."""
+    T, B = actions.shape[0], dyn.shape[2]
+    ret = np.zeros(B, np.float32)
+    sd = np.zeros((T,) + dyn.shape, np.float32)
+    sk = np.zeros((T, B, 2), np.uint32)
+    actions = np.ascontiguousarray(actions, np.float32)
+    w = np.ascontiguousarray(w, np.float32)
+    lib.emu_rollout(h, _p(dyn), _p(keys), _p(err), _p(geom), gstride, B, T, dt, stages, _p(actions), action_body,
+                    _p(w), _p(ret), _p(sd), _p(sk), E)
+    return ret, sd, sk
+
+
+def rollout_backward(lib, h, sd, sk, geom, gstride, stages, actions, action_body, w, dt=1e-2, E=4):
+    T, B = actions.shape[0], sd.shape[3]
+    ga = np.zeros((T, B, 2), np.float32)
+    gd = np.zeros(sd.shape[1:], np.float32)
+    actions = np.ascontiguousarray(actions, np.float32)
+    w = np.ascontiguousarray(w, np.float32)
+    rc = lib.emu_rollout_backward(h, _p(sd), _p(sk), _p(geom), gstride, B, T, dt, stages, _p(actions), action_body,
+                                  _p(w), _p(ga), _p(gd), E)
+    if rc:
+        raise RuntimeError(lib.emu_last_error().decode())
+    return ga, gd

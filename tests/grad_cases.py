@@ -1,0 +1,76 @@
+"""Shared cases for the differentiable-rollout tests (CPU emulation and GPU).
+
+box world: one scene (tests/golden/make_golden.box_world_bodies(0): three
+static walls + four finite-mass balls), each env with its own random ball
+states, so circle-circle, circle-AABB contacts and sustained resolutions are
+exercised.  robocup: the bench batch (cotix/_robocup.py scene)."""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(HERE, "golden"), os.path.join(HERE, "..", "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import make_golden as mg  # noqa: E402
+from cotix_oracle import grad as G  # noqa: E402
+from cotix_oracle import physics as P  # noqa: E402
+from cotix_oracle import prng  # noqa: E402
+
+D0 = prng.gjk_initial_direction()
+
+
+def box_case(B, T, seed=0):
+    make = lambda: mg.box_world_bodies(0)  # noqa: E731
+    base = np.array([b.dyn() for b in make()], np.float32)
+    rng = np.random.default_rng(seed)
+    S0 = np.repeat(base[None], B, axis=0)
+    for e in range(B):
+        for b in range(3, 7):
+            S0[e, b] = [rng.uniform(-2.5, 2.5), rng.uniform(-1.6, 1.6), rng.uniform(-3, 3), rng.uniform(-3, 3),
+                        rng.uniform(-1, 1), rng.uniform(-5, 5)]
+    keys = np.asarray(prng.split(prng.PRNGKey(11 + seed), B), np.uint32)
+    actions = (rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32)
+    w = np.zeros(7 * 6, np.float32)
+    w[6 * 6 + 0] = 1.0   # ball 6: x
+    w[5 * 6 + 3] = 0.5   # ball 5: vy
+    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=6, step=P.robocup_step)
+
+
+def robocup_case(B, T, seed=0):
+    from cotix_oracle import cport
+    dyn, keys = cport.robocup_batch(B)
+    rng = np.random.default_rng(seed)
+    actions = (rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32)
+    w = np.zeros(5 * 6, np.float32)
+    w[4 * 6 + 0] = 1.0   # return = sum_t ball x
+    return dict(make=P.robocup_bodies, S0=np.ascontiguousarray(dyn.transpose(2, 0, 1)), keys=keys,
+                actions=actions, w=w, ab=4, step=P.robocup_step)
+
+
+def oracle(case, envs=None):
+    """Per env: (ret, grad_actions [T,2], grad_S0 [nb,6]) from the torch VJP chain."""
+    B = case["S0"].shape[0]
+    envs = range(B) if envs is None else envs
+    out = {}
+    for e in envs:
+        ret, ga, gS, _ = G.rollout_grad(case["make"], case["S0"][e], case["keys"][e], case["actions"][:, e],
+                                        case["w"], case["ab"], D0, step=case["step"])
+        out[e] = (ret, ga, gS)
+    return out
+
+
+def close(got, want, rtol=2e-4):
+    """Gradient agreement: same NaN pattern, |got-want| <= rtol*(|want| + max|want|*0.1)."""
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    ng, nw = np.isnan(got), np.isnan(want)
+    if not np.array_equal(ng, nw):
+        return False, "NaN pattern differs (%d vs %d)" % (ng.sum(), nw.sum())
+    g, w = got[~nw], want[~nw]
+    if g.size == 0:
+        return True, ""
+    scale = np.abs(w) + 0.1 * np.max(np.abs(w)) + 1e-12
+    err = np.max(np.abs(g - w) / scale)
+    return err <= rtol, "max scaled err %.3g" % err

@@ -377,3 +377,102 @@ def test_lunar_4096_all_envs_vs_cport(torch_cuda, cport_lib):
     got = ll.world.dyn.cpu().numpy()
     assert same_f32(got, dyn), diff_report(got, dyn)
     assert np.array_equal(ll.world.keys.cpu().numpy().view(np.uint32), keys)
+
+
+# ---------------------------------------------------------------------------
+# differentiable rollout (BASELINE config 5)
+# ---------------------------------------------------------------------------
+def _gpu_rollout(torch, case, bodies_pa, want_dyn0=True):
+    import parallax_amd as pa
+    B = case["S0"].shape[0]
+    w = pa.World(bodies_pa, B, "cuda", torch.tensor(u32_to_i32(case["keys"]), device="cuda"))
+    w.dyn.copy_(torch.tensor(case["S0"], device="cuda").permute(1, 2, 0))
+    acts = torch.tensor(case["actions"], device="cuda")
+    ret, saved = pa.rollout_forward(w, acts, case["ab"], case["w"])
+    ga, gd = pa.rollout_backward(w, saved, want_dyn0=want_dyn0)
+    torch.cuda.synchronize()
+    return w, ret.cpu().numpy(), ga.cpu().numpy(), (gd.cpu().numpy() if gd is not None else None), saved
+
+
+def _pa_bodies(pa, oracle_bodies):
+    out = []
+    for b in oracle_bodies:
+        parts = [pa.AABB(list(p.lower), list(p.upper)) if p.kind == "AABB" else pa.Circle(p.radius, list(p.position))
+                 for p in b.parts]
+        out.append(pa.AnyBody(shape=pa.UniversalShape(*parts), mass=b.mass, inertia=b.inertia,
+                              position=list(b.position), velocity=list(b.velocity), angle=b.angle,
+                              angular_velocity=b.angular_velocity, elasticity=b.elasticity,
+                              friction_coefficient=b.friction_coefficient))
+    return out
+
+
+def test_rollout_grad_box_world_vs_oracle(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    case = GC.box_case(6, 32, seed=1)
+    _, ret, ga, gd, _ = _gpu_rollout(torch, case, _pa_bodies(pa, case["make"]()))
+    orc = GC.oracle(case)
+    for e in orc:
+        r, oga, ogS = orc[e]
+        assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)
+        ok, msg = GC.close(ga[:, e], oga)
+        assert ok, "env %d grad_action %s" % (e, msg)
+        ok, msg = GC.close(gd[:, :, e], ogS)
+        assert ok, "env %d grad_dyn0 %s" % (e, msg)
+
+
+def test_rollout_grad_robocup_vs_oracle(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    case = GC.robocup_case(16, 8)
+    _, ret, ga, _, _ = _gpu_rollout(torch, case, pa.scenarios.robocup_bodies())
+    orc = GC.oracle(case)
+    for e in orc:
+        r, oga, _ = orc[e]
+        assert (np.isnan(ret[e]) and np.isnan(r)) or np.float32(ret[e]).view(np.uint32) == np.float32(r).view(
+            np.uint32), (e, ret[e], r)
+        ok, msg = GC.close(ga[:, e], oga)
+        assert ok, "env %d %s" % (e, msg)
+
+
+def test_rollout_config5_full_size_vs_emulation(torch_cuda):
+    """BASELINE config 5 at full size (4096 envs x 64 steps): forward state,
+    return and every gradient equal the host emulation of the same kernel
+    code bit for bit (the emulation is pinned to the oracle by
+    tests/test_grad_cpu.py); then autograd through pa.differentiable_rollout."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    sys_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu")
+    import sys
+    sys.path.insert(0, sys_path)
+    import emu
+    lib = emu.load()
+    B, T = 4096, 64
+    case = GC.robocup_case(B, T)
+    w, ret, ga, gd, saved = _gpu_rollout(torch, case, pa.scenarios.robocup_bodies())
+    h, geom = emu.oracle_scene(lib, case["make"]())
+    dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
+    keys = np.array(case["keys"], np.uint32, copy=True)
+    err = np.zeros(B, np.uint32)
+    eret, esd, esk = emu.rollout(lib, h, dyn, keys, err, geom, 0, 21, case["actions"], case["ab"], case["w"])
+    ega, egd = emu.rollout_backward(lib, h, esd, esk, geom, 0, 21, case["actions"], case["ab"], case["w"])
+    assert same_f32(w.dyn.cpu().numpy(), dyn)
+    assert same_f32(saved["dyn"].cpu().numpy(), esd)
+    assert same_f32(ret, eret)
+    assert same_f32(ga, ega), diff_report(ga, ega)
+    assert same_f32(gd, egd), diff_report(gd, egd)
+    fin = np.isfinite(ga).all(axis=(0, 2))
+    assert fin.any()
+    # autograd surface: d(sum_env g_env * R_env)/d action = g_env * dR_env/d action
+    w2 = pa.World(pa.scenarios.robocup_bodies(), B, "cuda", torch.tensor(u32_to_i32(case["keys"]), device="cuda"))
+    w2.dyn.copy_(torch.tensor(case["S0"], device="cuda").permute(1, 2, 0))
+    acts = torch.tensor(case["actions"], device="cuda", requires_grad=True)
+    R = pa.differentiable_rollout(w2, acts, case["ab"], case["w"])
+    g = torch.linspace(0.5, 1.5, B, device="cuda")
+    (R[torch.isfinite(R)] * g[torch.isfinite(R)]).sum().backward()
+    got = acts.grad.cpu().numpy()[:, fin]
+    want = (ga * g.cpu().numpy()[None, :, None])[:, fin]
+    assert np.allclose(got, want, rtol=1e-6, atol=0)

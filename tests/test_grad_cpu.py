@@ -1,0 +1,108 @@
+"""Differentiable rollout (BASELINE config 5) on CPU: the kernel's forward
+and backward wave programs (host emulation, tests/emu) against the torch
+float32 VJP chain of the oracle (oracle/cotix_oracle/grad.py), itself
+checked against central finite differences of the faithful oracle."""
+import os
+
+import numpy as np
+import pytest
+
+import grad_cases as GC
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def emu_lib():
+    import subprocess
+    import sys
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "emu"), "build/libcotix_emu.so"], check=True)
+    sys.path.insert(0, os.path.join(HERE, "emu"))
+    import emu
+    return emu, emu.load()
+
+
+def _emu_run(emu, lib, case, E=4):
+    h, geom = emu.oracle_scene(lib, case["make"]())
+    dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
+    keys = np.array(case["keys"], np.uint32, copy=True)  # the kernel advances keys in place
+    err = np.zeros(dyn.shape[2], np.uint32)
+    ret, sd, sk = emu.rollout(lib, h, dyn, keys, err, geom, 0, 1 | 4 | 16, case["actions"], case["ab"], case["w"],
+                              E=E)
+    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, 1 | 4 | 16, case["actions"], case["ab"], case["w"], E=E)
+    return ret, ga, gd, dyn
+
+
+def test_oracle_grad_vs_finite_differences():
+    """The checker itself: torch VJP chain vs central differences of the
+    faithful f32 oracle (box world, no discrete flips at eps=1e-2)."""
+    case = GC.box_case(2, 10, seed=3)
+    orc = GC.oracle(case)
+    P = GC.P
+    for e in range(2):
+        ga = orc[e][1]
+        for (t, c) in [(0, 0), (0, 1), (4, 0), (9, 1)]:
+            vals = []
+            for s in (1, -1):
+                a = case["actions"][:, e].copy()
+                a[t, c] += s * 1e-2
+                bodies = case["make"]()
+                for b, row in zip(bodies, case["S0"][e]):
+                    b.set_dyn(row)
+                key = case["keys"][e]
+                tot = 0.0
+                for tt in range(10):
+                    bodies, key = P.robocup_step(bodies, key, GC.D0, action=a[tt], action_body=case["ab"])
+                    tot += float(bodies[6].position[0]) + 0.5 * float(bodies[5].velocity[1])
+                vals.append(tot)
+            fd = (vals[0] - vals[1]) / 2e-2
+            assert abs(fd - ga[t, c]) <= 2e-3 * (1 + abs(fd)), (e, t, c, fd, ga[t, c])
+
+
+@pytest.mark.parametrize("E", [1, 4])
+def test_emu_rollout_box_world(emu_lib, E):
+    emu, lib = emu_lib
+    B, T = 6, 40
+    case = GC.box_case(B, T, seed=1)
+    ret, ga, gd, dyn = _emu_run(emu, lib, case, E)
+    orc = GC.oracle(case)
+    for e in range(B):
+        r, oga, ogS = orc[e]
+        assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)  # bit-exact
+        ok, msg = GC.close(ga[:, e], oga)
+        assert ok, "env %d grad_action: %s" % (e, msg)
+        ok, msg = GC.close(gd[:, :, e], ogS)
+        assert ok, "env %d grad_dyn0: %s" % (e, msg)
+    assert np.abs(ga).max() > 0
+
+
+def test_emu_rollout_robocup(emu_lib):
+    """The config-5 scene itself (short horizon): ball x return, NaN-propagation
+    pattern included (most RoboCup envs go NaN at step 1 in the reference)."""
+    emu, lib = emu_lib
+    B, T = 8, 6
+    case = GC.robocup_case(B, T)
+    ret, ga, gd, _ = _emu_run(emu, lib, case)
+    orc = GC.oracle(case)
+    finite = 0
+    for e in range(B):
+        r, oga, ogS = orc[e]
+        same = (np.isnan(ret[e]) and np.isnan(r)) or np.float32(ret[e]).view(np.uint32) == np.float32(r).view(
+            np.uint32)
+        assert same, (e, ret[e], r)
+        ok, msg = GC.close(ga[:, e], oga)
+        assert ok, "env %d: %s" % (e, msg)
+        finite += int(np.isfinite(oga).all())
+    assert finite >= 1
+
+
+def test_backward_rejects_polygon_scenes(emu_lib):
+    emu, lib = emu_lib
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    h, geom = emu.oracle_scene(lib, P.lunar_lander_bodies(prng.PRNGKey(0)))
+    sd = np.zeros((1, 4, 6, 1), np.float32)
+    sk = np.zeros((1, 1, 2), np.uint32)
+    with pytest.raises(RuntimeError, match="circle/AABB"):
+        emu.rollout_backward(lib, h, sd, sk, geom, 0, 1 | 4 | 16, np.zeros((1, 1, 2), np.float32), 0,
+                             np.zeros(24, np.float32))

@@ -148,14 +148,17 @@ CX_DEV key2 threefry(key2 k, uint32_t x0, uint32_t x1) {
   return key2{x0, x1};
 }
 #undef CX_RND
-// word m of the flat output of split(key, num) (counters iota(2*num)).
+// word m of the flat output of split(key, num) (counters iota(2*num)): the
+// y0 of block (m, num+m) when m < num, else the y1 of block (m-num, m).
+// Branch-free (one block per word even when lanes diverge on m < num).
 CX_DEV uint32_t split_word(key2 k, uint32_t num, uint32_t m) {
-  if (m < num) return threefry(k, m, num + m).a;
-  return threefry(k, m - num, m).b;
+  const bool lo = m < num;
+  const key2 r = threefry(k, lo ? m : m - num, lo ? num + m : m);
+  return lo ? r.a : r.b;
 }
-// split(key, num)[idx]: two threefry blocks (one when num == 1).
+// split(key, num)[idx]: two blocks (for num == 1 both words come from block
+// (0, 1), which the same formula yields).
 CX_DEV key2 split_at(key2 k, uint32_t num, uint32_t idx) {
-  if (num == 1u) return threefry(k, 0u, 1u);
   return key2{split_word(k, num, 2u * idx), split_word(k, num, 2u * idx + 1u)};
 }
 // the single 32-bit word of random_bits(key, ()) (odd count -> zero pad).

@@ -41,7 +41,10 @@ struct SceneDev {
   int nb, np, nc, nl, nt, G, W, ncand;  // bodies, parts, contacts, cells, types, geom/world floats, candidates
   float d0x, d0y;                       // GJK start direction (constant)
   int o_par, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
-  int o_ci, o_cj, o_cbeg, o_ccnt, o_dbeg, o_dcnt, o_tn1, o_tn2, o_cand, o_dist;
+  int o_ci, o_cj, o_cbeg, o_ccnt, o_tn1, o_tn2, o_cand;
+  int o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts
+  int o_cmask;  // per cell nmw words: bitmask of the cell's distinct contacts
+  int nmw;      // contact-mask words = ceil(nc / 32)
   int nhot;
   uint32_t hot[MAXHOT];
 };
@@ -60,7 +63,7 @@ struct KArgs {
   int action_body;
   const float* dyn_reset;  // [nb][6][B] or null
   uint32_t* resets;        // [B] or null
-  int dbg_skip;            // debug only: bit k skips collider phase k (T=1,B=2,C=4,D=8)
+  int dbg_skip;            // timing only: skip phase T=1, B=2, C=4, D=8, A's key splits=16, E=32
   // differentiable rollout (cotix_rollout / cotix_rollout_backward)
   float* save_dyn;         // [n_steps][nb*6][B]: state before each step, or null
   uint32_t* save_keys;     // [n_steps][B][2]
@@ -72,7 +75,7 @@ struct KArgs {
 
 // per-wave tile layout (words, each x EW envs)
 struct Lay {
-  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, S;
+  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, S;
 };
 constexpr int REC_W = 7;  // per resolution: applied flag, v/w of body i, v/w of body j (pre-resolution)
 CX_HD Lay layout(int nb, int W, int nc, int nt) {
@@ -90,13 +93,19 @@ CX_HD Lay layout(int nb, int W, int nc, int nt) {
   L.ret = L.nres + 1;
   L.adj = L.ret + 1;
   L.rec = L.adj + nb * 6;
-  L.S = L.rec + nb * REC_W;
+  L.vm = L.rec + nb * REC_W;        // bit c: contact c has a contact point this step
+  L.rst = L.vm + (nc + 31) / 32;    // restart state (autoreset), staged once per launch
+  L.S = L.rst + nb * 6;
   return L;
 }
 static inline int tile_words(const SceneDev& s) { return layout(s.nb, s.W, s.nc, s.nt).S; }
+// per-wave scratch of phase C (words, not per env): pass flags, keep flags,
+// active count, two item lists (double buffer), per-item scan positions
+enum : int { WS_FLAG = 0, WS_KEEP = 64, WS_N = 128, WS_LIST = 129 };
+CX_HD int ws_words(int nl, int ew) { return WS_LIST + 3 * nl * ew; }
 // LDS bytes of a workgroup of wpb waves x ew envs
 static inline size_t lds_bytes(const SceneDev& s, int wpb, int ew) {
-  return 4 * ((size_t)s.nhot + (size_t)tile_words(s) * ew * wpb);
+  return 4 * ((size_t)s.nhot + ((size_t)tile_words(s) * ew + (size_t)ws_words(s.nl, ew)) * wpb);
 }
 
 CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, const cx::Params& pl,
@@ -195,11 +204,29 @@ CX_DEV void wave_sync() {
 #endif
 }
 
+// 64-bit ballot of flags[lane] != 0 over the wave.  Called convergently (all
+// 64 lanes, top level of a phase) after the flags were written by the
+// previous phase; the host emulation rebuilds it from the LDS flags.
+CX_DEV uint64_t wave_ballot(const uint32_t* flags, int lane) {
+#if defined(__HIP__) || defined(__HIPCC__)
+  return (uint64_t)__ballot(flags[lane] != 0u);
+#else
+  (void)lane;
+  uint64_t m = 0;
+  for (int l = 0; l < WAVE; ++l)
+    if (flags[l] != 0u) m |= 1ull << l;
+  return m;
+#endif
+}
+CX_DEV int popc64(uint64_t m) { return __builtin_popcountll(m); }
+CX_DEV uint64_t lanes_below(int lane) { return lane == 0 ? 0ull : ((1ull << lane) - 1ull); }
+
 // LDS views: scene hot tables + this wave's [word][env] tile
 template <int EW>
 struct Tile {
   uint32_t* u;          // tile base
   const uint32_t* tb;   // hot tables
+  uint32_t* ws;         // wave scratch (ws_words)
   CX_MF float& f(int off, int e) const { return reinterpret_cast<float*>(u)[off * EW + e]; }
   CX_MF uint32_t& w(int off, int e) const { return u[off * EW + e]; }
   CX_MF int ti(int off) const { return (int)tb[off]; }
@@ -217,6 +244,11 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
     int e = w % EW, off = w / EW, g = env0 + e;
     t.f(c.L.dyn + off, e) = (g < a.B) ? a.dyn[(size_t)off * a.B + g] : 0.0f;
   }
+  if (a.dyn_reset != nullptr)
+    for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+      int e = w % EW, off = w / EW, g = env0 + e;
+      t.f(c.L.rst + off, e) = (g < a.B) ? a.dyn_reset[(size_t)off * a.B + g] : 0.0f;
+    }
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     t.w(c.L.key, e) = (g < a.B) ? a.keys[2 * (size_t)g] : 0u;
@@ -255,16 +287,19 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
     for (int e = lane; e < EW; e += WAVE) {
-      key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
-      key2 s = split_at(k, 2u, 0u);  // cotix/_colliders.py:142 == next driver key
-      t.w(L.sk0, e) = s.a;
-      t.w(L.sk0 + 1, e) = s.b;
-      for (int q = 0; q < c.nt; ++q) {  // :175, one split per type key
-        s = split_at(s, 2u, 0u);
-        t.w(L.skt + 2 * q, e) = s.a;
-        t.w(L.skt + 2 * q + 1, e) = s.b;
+      if (!(a.dbg_skip & 16)) {
+        key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
+        key2 s = split_at(k, 2u, 0u);  // cotix/_colliders.py:142 == next driver key
+        t.w(L.sk0, e) = s.a;
+        t.w(L.sk0 + 1, e) = s.b;
+        for (int q = 0; q < c.nt; ++q) {  // :175, one split per type key
+          s = split_at(s, 2u, 0u);
+          t.w(L.skt + 2 * q, e) = s.a;
+          t.w(L.skt + 2 * q + 1, e) = s.b;
+        }
       }
       for (int q = 0; q < nb * nb; ++q) t.w(L.m + q, e) = 0xFFFFFFFFu;
+      for (int q = 0; q < c.sc->nmw; ++q) t.w(L.vm + q, e) = 0u;
       for (int q = 0; q < nb; ++q) t.w(L.ch + q, e) = (uint32_t)q;
     }
   }
@@ -322,13 +357,14 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int w = lane; w < c.nc * EW; w += WAVE) {
     int e = w % EW, ci = w / EW, g = env0 + e;
     if (g >= a.B) continue;
-    const int pa = t.ti(sc.o_cpa + ci), pb = t.ti(sc.o_cpb + ci), fn = t.ti(sc.o_cfn + ci);
+    const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
+    const int fn = (int)((d0w >> 20) & 7u);
     Shape A, Bs;
-    A.kind = t.ti(sc.o_pkind + pa);
-    A.n = t.ti(sc.o_pn + pa);
-    Bs.kind = t.ti(sc.o_pkind + pb);
-    Bs.n = t.ti(sc.o_pn + pb);
-    const int wa = c.L.world + t.ti(sc.o_pwoff + pa), wb = c.L.world + t.ti(sc.o_pwoff + pb);
+    A.kind = (int)((d0w >> 23) & 3u);
+    Bs.kind = (int)((d0w >> 25) & 3u);
+    A.n = (int)(d1w & 255u);
+    Bs.n = (int)((d1w >> 8) & 255u);
+    const int wa = c.L.world + (int)(d0w & 1023u), wb = c.L.world + (int)((d0w >> 10) & 1023u);
     if (FNSET == FNS_ANALYTIC) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -351,6 +387,13 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     t.f(co + 1, e) = ct.pen.y;
     t.f(co + 2, e) = ct.cp.x;
     t.f(co + 3, e) = ct.cp.y;
+    if (!(isn(ct.cp.x) || isn(ct.cp.y))) {
+#if defined(__HIP__) || defined(__HIPCC__)
+      atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
+#else
+      t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
+#endif
+    }
     if (er) {
 #if defined(__HIP__) || defined(__HIPCC__)
       atomicOr(&t.w(c.L.err, e), er);
@@ -361,49 +404,108 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   }
 }
 
-// phase C: per cell, last passing candidate (cotix/_colliders.py:208-268)
+// phase C: per cell, last passing candidate (cotix/_colliders.py:208-268).
+// The reference scans N2 x N1 candidates forward, each non-NaN one writing
+// its cell when its bernoulli draw passes, so a cell ends with its LAST
+// passing candidate: we scan each cell's candidates in reverse and stop at
+// the first pass.  The scan is wave-cooperative: active (env, cell) items
+// are compacted into a list, and every round gives each remaining item
+// G = 64 / n lanes that draw G consecutive candidates at once; a ballot
+// picks each item's first passing one, unresolved items advance by G.
+// C0: activity (a cell whose distinct contacts are all NaN never writes).
 template <int EW>
-CX_DEV void ph_C(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void ph_C0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int chunk) {
   using namespace cx;
   const SceneDev& sc = *c.sc;
-  const Lay& L = c.L;
-  for (int w = lane; w < c.nl * EW; w += WAVE) {
-    int e = w % EW, l = w / EW, g = env0 + e;
-    if (g >= a.B) continue;
-    int res = -1;
-    // fast path: a cell whose distinct contacts are all NaN never writes
-    const int dbeg = t.ti(sc.o_dbeg + l), dcnt = t.ti(sc.o_dcnt + l);
-    bool any = false;
-    for (int q = 0; q < dcnt; ++q) {
-      const int cid = t.ti(sc.o_dist + dbeg + q);
-      const float cpx = t.f(L.con + 4 * cid + 2, e), cpy = t.f(L.con + 4 * cid + 3, e);
-      any = any || !(isn(cpx) || isn(cpy));
-    }
-    if (any) {
-      const int beg = t.ti(sc.o_cbeg + l), cnt = t.ti(sc.o_ccnt + l);
-      int lt = -1, li2 = -1;
-      key2 k2 = key2{0u, 0u};
-      for (int q = 0; q < cnt; ++q) {
-        const uint32_t cd = t.tb[sc.o_cand + beg + q];
-        const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
-        const float cpx = t.f(L.con + 4 * cid + 2, e), cpy = t.f(L.con + 4 * cid + 3, e);
-        if (isn(cpx) || isn(cpy)) continue;  // a NaN candidate never writes
-        if (ty != lt || i2 != li2) {
-          key2 sk = key2{t.w(L.skt + 2 * ty, e), t.w(L.skt + 2 * ty + 1, e)};
-          k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
-          lt = ty;
-          li2 = i2;
-        }
-        key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);  // :254
-        key2 k1 = split_at(k, 2u, 0u);                                        // :222
-        if (bernoulli_half(k1)) {                                             // :223
-          res = cid;
-          break;
-        }
+  const int id = chunk * WAVE + lane;
+  uint32_t flag = 0u;
+  if (id < c.nl * EW) {
+    const int e = id % EW, l = id / EW;
+    if (env0 + e < a.B) {
+      bool any = false;
+      for (int q = 0; q < sc.nmw; ++q) any = any || (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
+      if (any) {
+        flag = 1u;
+        t.ws[WS_LIST + 2 * c.nl * EW + id] = 0u;  // scan position
       }
     }
-    t.w(L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = (uint32_t)res;
   }
+  t.ws[WS_FLAG + lane] = flag;
+}
+// C0b: append this chunk's active items to list 0
+template <int EW>
+CX_DEV void ph_C0b(const Ctx& c, Tile<EW> t, int lane, int chunk) {
+  const uint64_t mask = wave_ballot(t.ws + WS_FLAG, lane);
+  const uint32_t base = chunk == 0 ? 0u : t.ws[WS_N];
+  if (t.ws[WS_FLAG + lane] != 0u) t.ws[WS_LIST + base + popc64(mask & lanes_below(lane))] = (uint32_t)(chunk * WAVE + lane);
+  if (lane == WAVE - 1) t.ws[WS_N] = base + (uint32_t)popc64(mask);  // last lane: the host emulation runs it last
+  (void)c;
+}
+// R1: every lane draws one candidate of its item
+template <int EW>
+CX_DEV void ph_C1(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int par) {
+  using namespace cx;
+  const SceneDev& sc = *c.sc;
+  const int NI = c.nl * EW;
+  const uint32_t* list = t.ws + WS_LIST + par * NI;
+  const int n = (int)t.ws[WS_N], np = n < WAVE ? n : WAVE, G = WAVE / np;
+  const int slot = lane / G, q = lane % G;
+  uint32_t pass = 0u;
+  if (slot < np) {
+    const int id = (int)list[slot], e = id % EW, l = id / EW;
+    const int idx = (int)t.ws[WS_LIST + 2 * NI + id] + q;
+    if (idx < t.ti(sc.o_ccnt + l)) {
+      const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
+      const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
+      const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
+      if (!(isn(cpx) || isn(cpy))) {  // a NaN candidate never writes
+        const key2 sk = key2{t.w(c.L.skt + 2 * ty, e), t.w(c.L.skt + 2 * ty + 1, e)};
+        const key2 k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
+        const key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);   // :254
+        pass = bernoulli_half(split_at(k, 2u, 0u)) ? 1u : 0u;                      // :222-223
+      }
+    }
+  }
+  (void)a;
+  t.ws[WS_FLAG + lane] = pass;
+  t.ws[WS_KEEP + lane] = 0u;
+}
+// R2: per item, the first passing draw writes the cell; else advance
+template <int EW>
+CX_DEV void ph_C2(const Ctx& c, Tile<EW> t, int lane, int par) {
+  const SceneDev& sc = *c.sc;
+  const uint64_t mask = wave_ballot(t.ws + WS_FLAG, lane);
+  const int NI = c.nl * EW;
+  const uint32_t* list = t.ws + WS_LIST + par * NI;
+  const int n = (int)t.ws[WS_N], np = n < WAVE ? n : WAVE, G = WAVE / np;
+  const int slot = lane / G, q = lane % G;
+  if (q == 0 && slot < np) {
+    const int id = (int)list[slot], e = id % EW, l = id / EW;
+    const uint64_t gm = G == WAVE ? ~0ull : ((1ull << G) - 1ull);
+    const uint64_t bits = (mask >> (slot * G)) & gm;
+    uint32_t& pos = t.ws[WS_LIST + 2 * NI + id];
+    if (bits != 0ull) {
+      const int idx = (int)pos + __builtin_ctzll(bits);
+      const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
+      t.w(c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = (cd >> 18) & 511u;
+    } else {
+      pos = pos + (uint32_t)G;
+      t.ws[WS_KEEP + slot] = (int)pos < t.ti(sc.o_ccnt + l) ? 1u : 0u;
+    }
+  }
+}
+// R3: compact the unresolved items into the other list
+template <int EW>
+CX_DEV void ph_C3(const Ctx& c, Tile<EW> t, int lane, int par) {
+  const uint64_t mask = wave_ballot(t.ws + WS_KEEP, lane);
+  const int NI = c.nl * EW;
+  const uint32_t* cur = t.ws + WS_LIST + par * NI;
+  uint32_t* nxt = t.ws + WS_LIST + (1 - par) * NI;
+  const int n = (int)t.ws[WS_N];
+  const int kept = popc64(mask);
+  if (t.ws[WS_KEEP + lane] != 0u) nxt[popc64(mask & lanes_below(lane))] = cur[lane];
+  for (int s2 = WAVE + lane; s2 < n; s2 += WAVE) nxt[kept + s2 - WAVE] = cur[s2];  // not drawn this round
+  if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)(kept + (n > WAVE ? n - WAVE : 0));
 }
 
 // phase D: choose_random_contact (cotix/_colliders.py:274-295)
@@ -518,14 +620,14 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     if (a.dyn_reset != nullptr && t.w(L.err, e) != 0u) {
       // episode end on an error_if trip (the reference raises here): restart
       // the env from its reset state; the key chain continues.
-      for (int off = 0; off < nb * 6; ++off) t.f(L.dyn + off, e) = a.dyn_reset[(size_t)off * a.B + g];
+      for (int off = 0; off < nb * 6; ++off) t.f(L.dyn + off, e) = t.f(L.rst + off, e);
       t.w(L.err, e) = 0u;
       t.w(L.nres, e) = t.w(L.nres, e) + 1u;
     }
   }
 }
 
-template <int EW>
+template <int EW, bool ROLL = false>
 CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
@@ -538,7 +640,7 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
       a.keys[2 * (size_t)g + 1] = t.w(c.L.key + 1, e);
       a.err[g] = t.w(c.L.err, e);
       if (a.resets) a.resets[g] += t.w(c.L.nres, e);
-      if (a.ret) a.ret[g] += t.f(c.L.ret, e);
+      if (ROLL) a.ret[g] += t.f(c.L.ret, e);
     }
   }
 }
@@ -700,46 +802,61 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // ---------------------------------------------------------------------------
 // the wave programs.  R runs one phase over the wave's lanes and orders it
 // before the next: on the GPU R = this lane + wave_sync(); in the CPU
-// emulation of the tests R loops over the 64 lanes.
+// emulation of the tests R loops over the 64 lanes.  The phase id is used
+// only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
+enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
+             PH_RESTORE, PH_G, PH_ADJ, PH_COUNT };
 // ---------------------------------------------------------------------------
 template <int EW, int FNSET, class R>
 CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
-  if (!(a.dbg_skip & 1)) run([&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
-  if (!(a.dbg_skip & 2)) run([&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
-  if (!(a.dbg_skip & 4)) run([&](int l) { ph_C<EW>(a, c, t, env0, l); });
-  if (!(a.dbg_skip & 8)) run([&](int l) { ph_D<EW>(a, c, t, env0, l); });
+  if (!(a.dbg_skip & 1)) run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
+  if (!(a.dbg_skip & 2)) run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
+  if (!(a.dbg_skip & 4) && c.nl > 0) {
+    for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {
+      run(PH_C0, [&](int l) { ph_C0<EW>(a, c, t, env0, l, ch); });
+      run(PH_C0B, [&](int l) { ph_C0b<EW>(c, t, l, ch); });
+    }
+    for (int par = 0; t.ws[WS_N] != 0u; par ^= 1) {  // uniform: read after the phase barrier
+      run(PH_C1, [&](int l) { ph_C1<EW>(a, c, t, l, par); });
+      run(PH_C2, [&](int l) { ph_C2<EW>(c, t, l, par); });
+      run(PH_C3, [&](int l) { ph_C3<EW>(c, t, l, par); });
+    }
+  }
+  if (!(a.dbg_skip & 8)) run(PH_D, [&](int l) { ph_D<EW>(a, c, t, env0, l); });
 }
 
-// forward: n_steps fused steps (+ optional trajectory save and return)
-template <int EW, int FNSET, class R>
+// forward: n_steps fused steps; ROLL adds the trajectory save and the return
+// (cotix_rollout), compiled out of the plain step kernel
+template <int EW, int FNSET, bool ROLL, class R>
 CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
-  run([&](int l) {
+  run(PH_LOAD, [&](int l) {
     ph_load<EW>(a, c, t, env0, l);
-    for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
+    if (ROLL)
+      for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
   });
   for (int step = 0; step < a.n_steps; ++step) {
-    if (a.save_dyn != nullptr) run([&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
-    run([&](int l) { ph_A<EW>(a, c, t, env0, l, step); });
+    if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
+    run(PH_A, [&](int l) { ph_A<EW>(a, c, t, env0, l, step); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET>(a, c, t, env0, run);
-    run([&](int l) { ph_E<EW>(a, c, t, env0, l); });
-    if (a.ret != nullptr) run([&](int l) { ph_ret<EW>(a, c, t, env0, l); });
+    if (!(a.dbg_skip & 32)) run(PH_E, [&](int l) { ph_E<EW>(a, c, t, env0, l); });
+    if (ROLL) run(PH_RET, [&](int l) { ph_ret<EW>(a, c, t, env0, l); });
   }
-  run([&](int l) { ph_store<EW>(a, c, t, env0, l); });
+  run(PH_STORE, [&](int l) { ph_store<EW, ROLL>(a, c, t, env0, l); });
 }
 
 // backward: steps n_steps-1 .. 0, each re-played from the saved state (so
 // every discrete choice is the forward's) and then reversed by phase G
 template <int EW, int FNSET, class R>
 CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
-  run([&](int l) { ph_adj_init<EW>(a, c, t, env0, l); });
+  run(PH_ADJ, [&](int l) { ph_adj_init<EW>(a, c, t, env0, l); });
   for (int step = a.n_steps - 1; step >= 0; --step) {
-    run([&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });
-    run([&](int l) { ph_A<EW>(a, c, t, env0, l, step); });
+    run(PH_RESTORE, [&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });
+    run(PH_A, [&](int l) { ph_A<EW>(a, c, t, env0, l, step); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET>(a, c, t, env0, run);
-    run([&](int l) { ph_E<EW, true>(a, c, t, env0, l); });
-    run([&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
+    run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l); });
+    run(PH_G, [&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
   }
-  run([&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });
+  run(PH_ADJ, [&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });
 }
 
 }  // namespace cxk

@@ -177,7 +177,19 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   put(s.o_cpa, cpa);
   put(s.o_cpb, cpb);
   put(s.o_cfn, cfn);
-  std::vector<int> ci, cj, cbeg, ccnt, dbeg, dcnt, dist;
+  // per contact: world offsets, fn and kinds of both parts in one 2-word descriptor
+  if (hot.size() % 2) hot.push_back(0u);  // 8-byte aligned (one ds_read_b64)
+  s.o_cdesc = (int)hot.size();
+  for (int c = 0; c < s.nc; ++c) {
+    const int pa = cpa[c], pb = cpb[c];
+    if (part_woffv[pa] > 1023 || part_woffv[pb] > 1023) return scene_fail(err, "world table too large");
+    hot.push_back((uint32_t)part_woffv[pa] | ((uint32_t)part_woffv[pb] << 10) | ((uint32_t)cfn[c] << 20) |
+                  ((uint32_t)part_kindv[pa] << 23) | ((uint32_t)part_kindv[pb] << 25));
+    hot.push_back((uint32_t)part_nv[pa] | ((uint32_t)part_nv[pb] << 8));
+  }
+  s.nmw = (s.nc + 31) / 32;
+  std::vector<int> ci, cj, cbeg, ccnt;
+  std::vector<uint32_t> cmask;
   std::vector<int> candv;
   for (auto& ck : cell_order) {
     auto& v = cells[ck];
@@ -187,28 +199,23 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
     ccnt.push_back((int)v.size());
     // types ascend, then (ind2, ind1) ascend in v: reverse = last write first
     for (int q = (int)v.size() - 1; q >= 0; --q) candv.push_back((int)v[q]);
-    std::vector<int> d;
+    std::vector<uint32_t> m(s.nmw, 0u);  // the cell's distinct contacts
     for (uint32_t cd : v) {
       int c = (int)((cd >> 18) & 511u);
-      bool seen = false;
-      for (int x : d) seen = seen || x == c;
-      if (!seen) d.push_back(c);
+      m[c >> 5] |= 1u << (c & 31);
     }
-    dbeg.push_back((int)dist.size());
-    dcnt.push_back((int)d.size());
-    for (int x : d) dist.push_back(x);
+    cmask.insert(cmask.end(), m.begin(), m.end());
   }
   if ((int)candv.size() > MAXCAND) return scene_fail(err, "too many candidates");
   put(s.o_ci, ci);
   put(s.o_cj, cj);
   put(s.o_cbeg, cbeg);
   put(s.o_ccnt, ccnt);
-  put(s.o_dbeg, dbeg);
-  put(s.o_dcnt, dcnt);
   put(s.o_tn1, tn1);
   put(s.o_tn2, tn2);
   put(s.o_cand, candv);
-  put(s.o_dist, dist);
+  s.o_cmask = (int)hot.size();
+  for (uint32_t x : cmask) hot.push_back(x);
   if ((int)hot.size() > MAXHOT) return scene_fail(err, "scene tables too large");
   s.nhot = (int)hot.size();
   for (size_t q = 0; q < hot.size(); ++q) s.hot[q] = hot[q];

@@ -43,16 +43,31 @@ namespace {
 // the fused step kernel: WPB independent waves per workgroup, EW envs per wave
 // ---------------------------------------------------------------------------
 constexpr int WPB = 4;
+#ifdef COTIX_PHASE_PROF
+__device__ unsigned long long g_phase_cycles[cxk::PH_COUNT];
+#endif
 // one phase on this lane, then wave-local ordering before the next phase
 struct WaveRun {
   int lane;
+#ifdef COTIX_PHASE_PROF
+  unsigned long long* acc;  // per-phase cycle accumulators (registers after inlining)
   template <class F>
-  __device__ __forceinline__ void operator()(F f) const {
+  __device__ __forceinline__ void operator()(int ph, F f) const {
+    const unsigned long long t0 = clock64();
+    f(lane);
+    cxk::wave_sync();
+    acc[ph] += clock64() - t0;
+  }
+#else
+  template <class F>
+  __device__ __forceinline__ void operator()(int, F f) const {
     f(lane);
     cxk::wave_sync();
   }
+#endif
 };
-template <int EW, int FNSET, bool BWD>
+// MODE 0: step, 1: rollout forward (saves + return), 2: rollout backward
+template <int EW, int FNSET, int MODE>
 __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   extern __shared__ uint32_t lds[];
   const SceneDev* sc = a.sc;
@@ -63,11 +78,23 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int env0 = (blockIdx.x * WPB + wave) * EW;
   if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
-  const cxk::Tile<EW> t{lds + nhot + wave * c.L.S * EW, lds};
-  if (BWD)
-    cxk::run_wave_backward<EW, FNSET>(a, c, t, env0, WaveRun{lane});
+  uint32_t* wbase = lds + nhot + wave * (c.L.S * EW + cxk::ws_words(c.nl, EW));
+  const cxk::Tile<EW> t{wbase, lds, wbase + c.L.S * EW};
+#ifdef COTIX_PHASE_PROF
+  unsigned long long acc[cxk::PH_COUNT];
+  for (int q = 0; q < cxk::PH_COUNT; ++q) acc[q] = 0ull;
+  const WaveRun run{lane, acc};
+#else
+  const WaveRun run{lane};
+#endif
+  if (MODE == 2)
+    cxk::run_wave_backward<EW, FNSET>(a, c, t, env0, run);
   else
-    cxk::run_wave<EW, FNSET>(a, c, t, env0, WaveRun{lane});
+    cxk::run_wave<EW, FNSET, MODE == 1>(a, c, t, env0, run);
+#ifdef COTIX_PHASE_PROF
+  if (lane == 0)
+    for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -175,6 +202,19 @@ extern "C" {
 const char* cotix_last_error(void) { return g_err.c_str(); }
 const char* cotix_version(void) { return "cotix_amd 0.1 (gfx950)"; }
 
+#ifdef COTIX_PHASE_PROF
+// profiling build only: per-phase cycles summed over waves since the last call (then reset)
+int cotix_phase_cycles(unsigned long long* out, int n) {
+  unsigned long long h[cxk::PH_COUNT] = {};
+  if (hip_check(hipDeviceSynchronize(), "sync")) return -1;
+  if (hip_check(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase_cycles), sizeof(h)), "read phase cycles")) return -1;
+  unsigned long long z[cxk::PH_COUNT] = {};
+  if (hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)), "reset phase cycles")) return -1;
+  for (int q = 0; q < n && q < cxk::PH_COUNT; ++q) out[q] = h[q];
+  return cxk::PH_COUNT;
+}
+#endif
+
 int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,
                        const int* part_type, const int* part_nverts, cotix_scene** out) {
   if (!out) return fail("null argument");
@@ -231,8 +271,8 @@ static int check_step_args(const cotix_scene* scene, const float* dyn, const uin
   return 0;
 }
 
-// launch the fused step kernel (forward, or backward re-play when bwd)
-static int launch(cotix_scene* scene, const cxk::KArgs& ka0, bool bwd, cotix_stream_t stream) {
+// launch the fused step kernel (mode 0 step, 1 rollout forward, 2 backward re-play)
+static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_stream_t stream) {
   if (scene_upload(scene)) return -1;
   const int EW = envs_per_wave();
   const size_t lds = cxk::lds_bytes(scene->host, WPB, EW);
@@ -250,14 +290,20 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, bool bwd, cotix_str
   else if (EW == 8) COTIX_LAUNCH(8, FS, BW);  \
   else if (EW == 2) COTIX_LAUNCH(2, FS, BW);  \
   else COTIX_LAUNCH(4, FS, BW);
-  if (bwd) {
-    COTIX_LAUNCH_E(FNS_ANALYTIC, true)  // the host admits analytic scenes only
+  if (mode == 2) {
+    COTIX_LAUNCH_E(FNS_ANALYTIC, 2)  // the host admits analytic scenes only
+  } else if (mode == 1) {
+    if ((fs & ~FNS_ANALYTIC) == 0) {
+      COTIX_LAUNCH_E(FNS_ANALYTIC, 1)
+    } else {
+      COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, 1)
+    }
   } else if ((fs & ~FNS_ANALYTIC) == 0) {
-    COTIX_LAUNCH_E(FNS_ANALYTIC, false)
+    COTIX_LAUNCH_E(FNS_ANALYTIC, 0)
   } else if ((fs & FNS_CIRCLE_POLY) == 0) {
-    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX, false)
+    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX, 0)
   } else {
-    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, false)
+    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, 0)
   }
 #undef COTIX_LAUNCH_E
 #undef COTIX_LAUNCH
@@ -284,7 +330,7 @@ static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* e
   ka.action_body = action_body;
   ka.dyn_reset = dyn_reset;
   ka.resets = resets;
-  return launch(scene, ka, false, stream);
+  return launch(scene, ka, 0, stream);
 }
 
 int cotix_step(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
@@ -324,7 +370,7 @@ int cotix_rollout(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err,
   ka.save_keys = saved_keys;
   ka.ret = ret;
   for (int k = 0; k < scene->host.nb * 6; ++k) ka.ret_w[k] = ret_weights[k];
-  return launch(scene, ka, false, stream);
+  return launch(scene, ka, 1, stream);
 }
 
 int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uint32_t* saved_keys, const float* geom,
@@ -356,7 +402,7 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
   ka.grad_action = grad_action;
   ka.grad_dyn = grad_dyn0;
   for (int k = 0; k < scene->host.nb * 6; ++k) ka.ret_w[k] = ret_weights[k];
-  return launch(scene, ka, true, stream);
+  return launch(scene, ka, 2, stream);
 }
 
 int cotix_physics_euler(float* dyn, int n_bodies, int B, float dt, cotix_stream_t stream) {

@@ -24,7 +24,7 @@ struct EmuScene {
 // wave_sync() guarantees on the GPU)
 struct HostRun {
   template <class F>
-  void operator()(F f) const {
+  void operator()(int, F f) const {
     for (int l = 0; l < cxk::WAVE; ++l) f(l);
   }
 };
@@ -32,26 +32,28 @@ struct HostRun {
 // one wave at a time (waves are independent), through the kernel's own
 // wave programs (cxk::run_wave / run_wave_backward)
 template <int EW>
-void run_blocks(const cxk::KArgs& a, bool bwd) {
+void run_blocks(const cxk::KArgs& a, int mode) {
   const cxk::SceneDev& sc = *a.sc;
   const cxk::Ctx c{sc.nb, sc.np, sc.nc, sc.nl, sc.nt, &sc, cxk::layout(sc.nb, sc.W, sc.nc, sc.nt)};
   const int nwaves = (a.B + EW - 1) / EW;
-  std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)c.L.S * EW);
+  std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)c.L.S * EW + (size_t)cxk::ws_words(sc.nl, EW));
   for (int q = 0; q < sc.nhot; ++q) lds[q] = sc.hot[q];
   for (int wv = 0; wv < nwaves; ++wv) {
     std::fill(lds.begin() + sc.nhot, lds.end(), 0x7FBADBADu);  // poison (a NaN pattern)
-    const cxk::Tile<EW> t{lds.data() + sc.nhot, lds.data()};
-    if (bwd)
+    const cxk::Tile<EW> t{lds.data() + sc.nhot, lds.data(), lds.data() + sc.nhot + (size_t)c.L.S * EW};
+    if (mode == 2)
       cxk::run_wave_backward<EW, 7>(a, c, t, wv * EW, HostRun{});
+    else if (mode == 1)
+      cxk::run_wave<EW, 7, true>(a, c, t, wv * EW, HostRun{});
     else
-      cxk::run_wave<EW, 7>(a, c, t, wv * EW, HostRun{});
+      cxk::run_wave<EW, 7, false>(a, c, t, wv * EW, HostRun{});
   }
 }
-void run_any(const cxk::KArgs& a, int E, bool bwd) {
-  if (E == 1) run_blocks<1>(a, bwd);
-  else if (E == 4) run_blocks<4>(a, bwd);
-  else if (E == 8) run_blocks<8>(a, bwd);
-  else run_blocks<2>(a, bwd);
+void run_any(const cxk::KArgs& a, int E, int mode) {
+  if (E == 1) run_blocks<1>(a, mode);
+  else if (E == 4) run_blocks<4>(a, mode);
+  else if (E == 8) run_blocks<8>(a, mode);
+  else run_blocks<2>(a, mode);
 }
 }  // namespace
 
@@ -80,7 +82,7 @@ int emu_step(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float
              uint32_t* resets, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
   cxk::KArgs a{&s->s, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, action, action_body, dyn_reset, resets, 0};
-  run_any(a, E, false);
+  run_any(a, E, 0);
   return 0;
 }
 
@@ -105,7 +107,7 @@ int emu_rollout(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const fl
   a.save_keys = saved_keys;
   a.ret = ret;
   for (int k = 0; k < s->s.nb * 6; ++k) a.ret_w[k] = ret_w[k];
-  run_any(a, E, false);
+  run_any(a, E, 1);
   return 0;
 }
 
@@ -132,7 +134,7 @@ int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* sa
   a.grad_action = grad_action;
   a.grad_dyn = grad_dyn0;
   for (int k = 0; k < s->s.nb * 6; ++k) a.ret_w[k] = ret_w[k];
-  run_any(a, E, true);
+  run_any(a, E, 2);
   return 0;
 }
 

@@ -1,0 +1,69 @@
+"""Per-phase cycle profile of the fused step kernel (perf tooling, not the
+product).  Needs the profiling build of the library:
+    hipcc ... -DCOTIX_PHASE_PROF -> parallax_amd/_lib/libcotix_amd_prof.so   (tools/phase_prof.py --build)
+and runs the bench workload with it:  python tools/phase_prof.py [--scenario robocup|lunar] [--launches N]"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "parallax_amd", "_lib", "libcotix_amd_prof.so")
+NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
+         "adj"]
+
+
+def build():
+    src = os.path.join(ROOT, "parallax_amd", "csrc", "cotix_step.hip")
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", "-std=c++17",
+           "-fPIC", "-shared", "-DCOTIX_PHASE_PROF", src, "-o", LIB]
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--scenario", default="robocup")
+    ap.add_argument("--launches", type=int, default=10)
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--substeps", type=int, default=64)
+    a = ap.parse_args()
+    if a.build:
+        return build()
+    os.environ["COTIX_AMD_LIB"] = LIB
+    sys.path.insert(0, ROOT)
+    import torch
+    import parallax_amd as pa
+    f = pa._ffi.lib.cotix_phase_cycles
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device("cuda")
+    B = a.envs
+    if a.scenario == "robocup":
+        keys = pa.random.split(pa.random.PRNGKey(3, dev), B).contiguous()
+        scen = pa.RoboCupEnv(batch=B, device=dev, keys=keys, perturb=True)
+    else:
+        tk = pa.random.split(pa.random.PRNGKey(0, dev), B).contiguous()
+        ck = pa.random.split(pa.random.PRNGKey(1, dev), B).contiguous()
+        scen = pa.LunarLander(key=tk, batch=B, device=dev, collider_keys=ck)
+    env = pa.BatchedEnv(scen, autoreset=True)
+    env.reset()
+    env.step(a.substeps)
+    buf = (ctypes.c_ulonglong * 32)()
+    f(buf, 32)  # reset after warm-up
+    for _ in range(a.launches):
+        env.step(a.substeps)
+    torch.cuda.synchronize()
+    n = f(buf, 32)
+    waves = (B + 3) // 4
+    steps = a.launches * a.substeps
+    tot = sum(buf[q] for q in range(n))
+    out = {NAMES[q]: {"cycles_per_wave_step": buf[q] / waves / steps, "share": buf[q] / tot} for q in range(n)
+           if buf[q]}
+    print(json.dumps({"scenario": a.scenario, "envs": B, "cycles_per_wave_step_total": tot / waves / steps,
+                      "phases": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

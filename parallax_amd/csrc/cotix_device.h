@@ -203,11 +203,40 @@ CX_DEV void cumsum_assoc(const float* in, int n, float* out) {
 // ---------------------------------------------------------------------------
 enum : int { KIND_CIRCLE = 0, KIND_AABB = 1, KIND_POLY = 2 };
 constexpr int MAXV = 8;
+// A shape's geometry words (circle: r,cx,cy; aabb: lo.x,lo.y,up.x,up.y; poly:
+// xy*n) live in registers.  Every polygon loop below is unrolled to MAXV with
+// a k < n guard and every per-lane vertex pick is a select chain, so the
+// array is only ever indexed with compile-time constants (no scratch), and a
+// contact fetches its two shapes once (GJK/EPA iterations are pure ALU).
 struct Shape {
   int kind, n;
-  float d[2 * MAXV];  // circle: r,cx,cy; aabb: lo.x,lo.y,up.x,up.y; poly: xy*n
+  float w[2 * MAXV];
+  CX_MF float d(int k) const { return w[k]; }
 };
-CX_DEV v2 vert(const Shape& s, int k) { return v2{s.d[2 * k], s.d[2 * k + 1]}; }
+// vertex k, k varying per lane: select chain (constant-folds for constant k)
+CX_DEV v2 vert(const Shape& s, int k) {
+  v2 r = v2{s.w[0], s.w[1]};
+#pragma unroll
+  for (int q = 1; q < MAXV; ++q)
+    if (q == k) r = v2{s.w[2 * q], s.w[2 * q + 1]};
+  return r;
+}
+// argmin over v[0..n), n <= N at run time: first NaN, else first minimum
+template <int N>
+CX_DEV int argmin_first_n(const float* v, int n) {
+  int nan = -1, b = 0;
+  float bv = v[0];
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    if (k < n) {
+      if (nan < 0 && isn(v[k])) nan = k;
+      if (k > 0 && v[k] < bv) {
+        bv = v[k];
+        b = k;
+      }
+    }
+  return nan >= 0 ? nan : b;
+}
 
 CX_DEV int argmax_first(const float* v, int n) {
   for (int k = 0; k < n; ++k)
@@ -231,86 +260,94 @@ CX_DEV v2 support(const Shape& s, v2 d) {
   if (s.kind == KIND_CIRCLE) {
     float n = nrm(d);
     v2 nd = v2{d.x / n, d.y / n};
-    return v2{nd.x * s.d[0] + s.d[1], nd.y * s.d[0] + s.d[2]};
+    return v2{nd.x * s.d(0) + s.d(1), nd.y * s.d(0) + s.d(2)};
   }
   if (s.kind == KIND_AABB) {
-    return v2{d.x >= 0.0f ? s.d[2] : s.d[0], d.y >= 0.0f ? s.d[3] : s.d[1]};
+    return v2{d.x >= 0.0f ? s.d(2) : s.d(0), d.y >= 0.0f ? s.d(3) : s.d(1)};
   }
   if (vnan(d)) return v2{qnan(), qnan()};
-  // argmax(v . d), first NaN else first max
-  int best = -1;
-  float bv = 0.0f;
-  for (int k = 0; k < s.n; ++k) {
-    float t = s.d[2 * k] * d.x + s.d[2 * k + 1] * d.y;
-    if (best < 0 || (!isn(bv) && (isn(t) || t > bv))) {
-      best = k;
-      bv = t;
-    }
+  // argmax(v . d): first NaN, else first maximum.  Branch-free select chain
+  // (a guarded/branchy form of this loop was miscompiled by hipcc 7.2 at -O2+).
+  float bv = s.w[0] * d.x + s.w[1] * d.y;
+  float bx = s.w[0], by = s.w[1];
+#pragma unroll
+  for (int k = 1; k < MAXV; ++k) {
+    const float x = s.w[2 * k], y = s.w[2 * k + 1];
+    const float t = x * d.x + y * d.y;
+    const bool take = (k < s.n) && !isn(bv) && (isn(t) || t > bv);
+    bv = take ? t : bv;
+    bx = take ? x : bx;
+    by = take ? y : by;
   }
-  return vert(s, best);
+  return v2{bx, by};
 }
 CX_DEV v2 minkowski(const Shape& a, const Shape& b, v2 d) { return sub(support(a, d), support(b, neg(d))); }
 
 CX_DEV bool circle_contains(const Shape& c, v2 p) {  // :28-29
-  float r = c.d[0] + 1e-6f;
-  return sumsq(sub(p, v2{c.d[1], c.d[2]})) <= r * r;
+  float r = c.d(0) + 1e-6f;
+  return sumsq(sub(p, v2{c.d(1), c.d(2)})) <= r * r;
 }
 CX_DEV bool aabb_contains(const Shape& a, v2 p) {  // :105-106
-  return (p.x >= a.d[0] - 1e-6f) && (p.y >= a.d[1] - 1e-6f) && (p.x <= a.d[2] + 1e-6f) && (p.y <= a.d[3] + 1e-6f);
+  return (p.x >= a.d(0) - 1e-6f) && (p.y >= a.d(1) - 1e-6f) && (p.x <= a.d(2) + 1e-6f) && (p.y <= a.d(3) + 1e-6f);
 }
 CX_DEV float fsign(float x) { return isn(x) ? x : (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x)); }
 CX_DEV bool poly_contains(const Shape& s, v2 p) {  // :168-175, edge k = (v_k, v_{k-1})
   float s0 = 0.0f;
   bool ok = true;
-  for (int k = 0; k < s.n; ++k) {
-    v2 e0 = vert(s, k), e1 = vert(s, k == 0 ? s.n - 1 : k - 1);
-    float sg = fsign(dot(sub(p, e0), fnormal(sub(e0, e1))));
-    if (k == 0) s0 = sg;
-    else ok = ok && (sg == s0);
-  }
+  const v2 last = vert(s, s.n - 1);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (k < s.n) {
+      const v2 e0 = v2{s.w[2 * k], s.w[2 * k + 1]};
+      const v2 e1 = k == 0 ? last : v2{s.w[2 * k - 2], s.w[2 * k - 1]};
+      float sg = fsign(dot(sub(p, e0), fnormal(sub(e0, e1))));
+      if (k == 0) s0 = sg;
+      else ok = ok && (sg == s0);
+    }
   return ok && !isn(s0);
 }
-// AABB vertices/edges as a 4-gon: [up, (up.x,lo.y), lo, (lo.x,up.y)] :82-103
-CX_DEV void aabb_verts(const Shape& a, v2* vs) {
-  vs[0] = v2{a.d[2], a.d[3]};
-  vs[1] = v2{a.d[2], a.d[1]};
-  vs[2] = v2{a.d[0], a.d[1]};
-  vs[3] = v2{a.d[0], a.d[3]};
-}
-
 // order_clockwise (cotix/_geometry_utils.py:60-67): sequential mean, atan2,
-// stable sort (insertion sort is stable).
+// stable sort by angle.  The stable order is computed as ranks -- vertex k
+// goes to #{j : ang_j < ang_k} + #{j < k : ang_j ~ ang_k} under sort_lt (a
+// strict weak order: NaN last, -0 ~ +0), the same permutation insertion sort
+// produces -- with every loop unrolled to MAXV (register-only, no scratch).
 CX_DEV void order_clockwise(float* xy, int n) {
   float sx = 0.0f, sy = 0.0f;
-  for (int k = 0; k < n; ++k) {
-    sx = sx + xy[2 * k];
-    sy = sy + xy[2 * k + 1];
-  }
-  float fn = (float)n;
-  float mx = sx / fn, my = sy / fn;
-  float ang[MAXV], px[MAXV], py[MAXV];
-  for (int k = 0; k < n; ++k) {
-    px[k] = xy[2 * k];
-    py[k] = xy[2 * k + 1];
-    ang[k] = atan2_32(py[k] - my, px[k] - mx);
-  }
-  for (int k = 1; k < n; ++k) {
-    float a = ang[k], x = px[k], y = py[k];
-    int j = k - 1;
-    while (j >= 0 && sort_lt(a, ang[j])) {
-      ang[j + 1] = ang[j];
-      px[j + 1] = px[j];
-      py[j + 1] = py[j];
-      --j;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (k < n) {
+      sx = sx + xy[2 * k];
+      sy = sy + xy[2 * k + 1];
     }
-    ang[j + 1] = a;
-    px[j + 1] = x;
-    py[j + 1] = y;
+  const float fn = (float)n;
+  const float mx = sx / fn, my = sy / fn;
+  float ang[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) ang[k] = k < n ? atan2_32(xy[2 * k + 1] - my, xy[2 * k] - mx) : 0.0f;
+  int rank[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j)
+      if (j != k && j < n) r += (sort_lt(ang[j], ang[k]) || (j < k && !sort_lt(ang[k], ang[j]))) ? 1 : 0;
+    rank[k] = r;
   }
-  for (int k = 0; k < n; ++k) {
-    xy[2 * k] = px[k];
-    xy[2 * k + 1] = py[k];
+  float out[2 * MAXV];
+#pragma unroll
+  for (int p = 0; p < MAXV; ++p) {
+    float x = xy[2 * p], y = xy[2 * p + 1];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k)
+      if (k < n && rank[k] == p) {
+        x = xy[2 * k];
+        y = xy[2 * k + 1];
+      }
+    out[2 * p] = x;
+    out[2 * p + 1] = y;
   }
+#pragma unroll
+  for (int k = 0; k < 2 * MAXV; ++k) xy[k] = out[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -322,8 +359,8 @@ struct Contact {
 CX_DEV Contact nan_contact() { return Contact{v2{0.0f, 0.0f}, v2{qnan(), qnan()}}; }
 
 CX_DEV Contact aabb_vs_aabb(const Shape& a, const Shape& b) {  // :61-96
-  const float alx = a.d[0], aly = a.d[1], aux = a.d[2], auy = a.d[3];
-  const float blx = b.d[0], bly = b.d[1], bux = b.d[2], buy = b.d[3];
+  const float alx = a.d(0), aly = a.d(1), aux = a.d(2), auy = a.d(3);
+  const float blx = b.d(0), bly = b.d(1), bux = b.d(2), buy = b.d(3);
   bool below = auy <= bly, above = aly >= buy, left = aux <= blx, right = alx >= bux;
   if (below || left || above || right) return nan_contact();
   const float me = -1e-8f;
@@ -339,8 +376,8 @@ CX_DEV Contact aabb_vs_aabb(const Shape& a, const Shape& b) {  // :61-96
 }
 
 CX_DEV Contact circle_vs_circle(const Shape& a, const Shape& b) {  // :30-58
-  v2 ap = v2{a.d[1], a.d[2]}, bp = v2{b.d[1], b.d[2]};
-  float ar = a.d[0], br = b.d[0];
+  v2 ap = v2{a.d(1), a.d(2)}, bp = v2{b.d(1), b.d(2)};
+  float ar = a.d(0), br = b.d(0);
   v2 delta = sub(ap, bp);
   float dist = nrm(delta);
   v2 dir = (dist == 0.0f) ? v2{1.0f, 0.0f} : divs(delta, dist);
@@ -354,9 +391,9 @@ CX_DEV Contact circle_vs_circle(const Shape& a, const Shape& b) {  // :30-58
 // circle_vs_aabb :99-154.  *err |= 1 when eqx.error_if trips (ccp not in the
 // AABB); the guarded ccp then becomes NaN (EQX_ON_ERROR=nan semantics).
 CX_DEV Contact circle_vs_aabb(const Shape& a, const Shape& b, uint32_t* err) {
-  v2 ap = v2{a.d[1], a.d[2]};
-  float r = a.d[0];
-  v2 lo = v2{b.d[0], b.d[1]}, up = v2{b.d[2], b.d[3]};
+  v2 ap = v2{a.d(1), a.d(2)};
+  float r = a.d(0);
+  v2 lo = v2{b.d(0), b.d(1)}, up = v2{b.d(2), b.d(3)};
   v2 bc = v2{(lo.x + up.x) / 2.0f, (lo.y + up.y) / 2.0f};
   v2 disp = sub(ap, bc);
   v2 l = sub(lo, bc), h = sub(up, bc);
@@ -587,27 +624,27 @@ CX_DEV v2 edge_vs_edge(v2 pa0, v2 pa1, v2 qb0, v2 qb1) {  // :206-225
   if (c != 0.0f && t >= 0.0f && t <= 1.0f && u >= 0.0f && u <= 1.0f) return add(p, scl(r, t));
   return v2{qnan(), qnan()};
 }
-// A and B given as convex n-gons with edges (v_k, v_{k-1}) -- the AABB's
-// own edge list [(v0,v1),(v1,v2),(v2,v3),(v3,v0)] is passed explicitly.
-struct EdgeSet {
-  int n;
-  v2 v[MAXV];      // vertices (get_vertices)
-  v2 ea[MAXV], eb[MAXV];  // edges (get_edges)
-};
-CX_DEV void edges_of_poly(const Shape& s, EdgeSet* e) {
-  e->n = s.n;
-  for (int k = 0; k < s.n; ++k) {
-    e->v[k] = vert(s, k);
-    e->ea[k] = vert(s, k);
-    e->eb[k] = vert(s, k == 0 ? s.n - 1 : k - 1);
+// A and B as convex n-gons: polygon vertices v_k with edges (v_k, v_{k-1});
+// an AABB is the 4-gon [up, (up.x,lo.y), lo, (lo.x,up.y)] with its own edge
+// list [(v0,v1),(v1,v2),(v2,v3),(v3,v0)] (cotix/_convex_shapes.py:82-103).
+// Computed on the fly from the shape view (no private edge arrays).
+CX_DEV int cvx_count(const Shape& s) { return s.kind == KIND_AABB ? 4 : s.n; }
+// vertex k (compile-time k after unrolling); `last` = vertex count-1 of a polygon
+CX_DEV v2 cvx_vert(const Shape& s, int k) {
+  if (s.kind == KIND_AABB) {
+    const float x = (k == 0 || k == 1) ? s.w[2] : s.w[0];
+    const float y = (k == 0 || k == 3) ? s.w[3] : s.w[1];
+    return v2{x, y};
   }
+  return v2{s.w[2 * k], s.w[2 * k + 1]};
 }
-CX_DEV void edges_of_aabb(const Shape& s, EdgeSet* e) {
-  e->n = 4;
-  aabb_verts(s, e->v);
-  for (int k = 0; k < 4; ++k) {
-    e->ea[k] = e->v[k];
-    e->eb[k] = e->v[(k + 1) & 3];
+CX_DEV void cvx_edge(const Shape& s, int k, v2 last, v2* e0, v2* e1) {
+  if (s.kind == KIND_AABB) {
+    *e0 = cvx_vert(s, k);
+    *e1 = cvx_vert(s, (k + 1) & 3);
+  } else {
+    *e0 = cvx_vert(s, k);
+    *e1 = k == 0 ? last : cvx_vert(s, k - 1);
   }
 }
 CX_DEV bool shape_contains(const Shape& s, v2 p) {
@@ -615,37 +652,64 @@ CX_DEV bool shape_contains(const Shape& s, v2 p) {
   if (s.kind == KIND_CIRCLE) return circle_contains(s, p);
   return poly_contains(s, p);
 }
-CX_DEV v2 contact_from_edges(const Shape& A, const EdgeSet& ea, const Shape& B, const EdgeSet& eb) {
+// accumulation order (Appendix A): vertices of A in B, vertices of B in A,
+// then edge intersections B-edge-major, A-edge-minor
+CX_DEV v2 contact_from_edges(const Shape& A, const Shape& B) {
   float n = 0.0f;
   v2 acc = v2{0.0f, 0.0f};
-  for (int k = 0; k < ea.n; ++k)
-    if (shape_contains(B, ea.v[k])) { acc = add(acc, ea.v[k]); n = n + 1.0f; }
-  for (int k = 0; k < eb.n; ++k)
-    if (shape_contains(A, eb.v[k])) { acc = add(acc, eb.v[k]); n = n + 1.0f; }
-  for (int jb = 0; jb < eb.n; ++jb)
-    for (int ia = 0; ia < ea.n; ++ia) {
-      v2 x = edge_vs_edge(ea.ea[ia], ea.eb[ia], eb.ea[jb], eb.eb[jb]);
-      if (!vnan(x)) { acc = add(acc, x); n = n + 1.0f; }
+  const int na = cvx_count(A), nb = cvx_count(B);
+  const v2 lastA = A.kind == KIND_AABB ? v2{0.0f, 0.0f} : vert(A, A.n - 1);
+  const v2 lastB = B.kind == KIND_AABB ? v2{0.0f, 0.0f} : vert(B, B.n - 1);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (k < na) {
+      const v2 v = cvx_vert(A, k);
+      if (shape_contains(B, v)) { acc = add(acc, v); n = n + 1.0f; }
+    }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (k < nb) {
+      const v2 v = cvx_vert(B, k);
+      if (shape_contains(A, v)) { acc = add(acc, v); n = n + 1.0f; }
+    }
+#pragma unroll
+  for (int jb = 0; jb < MAXV; ++jb)
+    if (jb < nb) {
+      v2 b0, b1;
+      cvx_edge(B, jb, lastB, &b0, &b1);
+#pragma unroll
+      for (int ia = 0; ia < MAXV; ++ia)
+        if (ia < na) {
+          v2 a0, a1;
+          cvx_edge(A, ia, lastA, &a0, &a1);
+          v2 x = edge_vs_edge(a0, a1, b0, b1);
+          if (!vnan(x)) { acc = add(acc, x); n = n + 1.0f; }
+        }
     }
   if (n > 0.0f) return divs(acc, n);
   return v2{qnan(), qnan()};
 }
 
-// polygon_vs_polygon :294-315 / aabb_vs_polygon :270-291 (A may be an AABB)
-CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, v2 d0) {
+// polygon_vs_polygon :294-315 / aabb_vs_polygon :270-291 (A may be an AABB).
+// EPA runs iters = |A| + |B| + 1 <= 2*MAXV + 1 steps: at most 20 edges, so
+// the edge buffer is a compile-time register array (epa<14> / epa<20>).
+// need_pen = false (the step kernel, for a part paired with itself: such a
+// cell is only ever chosen as j == i, which resolution skips, so only the
+// NaN-ness of the contact point is observable) skips EPA; pen is then 0.
+CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, v2 d0, bool need_pen = true) {
+  static_assert(2 * MAXV + 1 + 3 <= 20, "EPA buffer bound");
   v2 simplex[3];
   if (!gjk(A, B, d0, simplex)) return nan_contact();
-  int iters = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
-  if (iters > 48) iters = 48;
+  const int iters = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
   Contact c;
-  if (iters + 3 <= 14) c.pen = epa<14>(A, B, simplex, iters);
-  else if (iters + 3 <= 20) c.pen = epa<20>(A, B, simplex, iters);
-  else c.pen = epa_big(A, B, simplex, iters);
-  EdgeSet ea, eb;
-  if (A.kind == KIND_AABB) edges_of_aabb(A, &ea);
-  else edges_of_poly(A, &ea);
-  edges_of_poly(B, &eb);
-  c.cp = contact_from_edges(A, ea, B, eb);
+  c.pen = v2{0.0f, 0.0f};
+  if (!need_pen) {
+  } else if (iters + 3 <= 14) {
+    c.pen = epa<14>(A, B, simplex, iters);
+  } else {
+    c.pen = epa<20>(A, B, simplex, iters);
+  }
+  c.cp = contact_from_edges(A, B);
   return c;
 }
 
@@ -655,24 +719,35 @@ CX_DEV Contact circle_vs_polygon(const Shape& C, const Shape& P, v2 d0) {
   if (!gjk(C, P, d0, simplex)) return nan_contact();
   Contact c;
   c.pen = epa_big(C, P, simplex, 128);
-  v2 pos = v2{C.d[1], C.d[2]};
+  v2 pos = v2{C.d(1), C.d(2)};
   float dists[MAXV];
   v2 disps[MAXV];
-  for (int k = 0; k < P.n; ++k) {
-    v2 a = vert(P, k), b = vert(P, k == 0 ? P.n - 1 : k - 1);
-    if (a.x == 0.0f && a.y == 0.0f && b.x == 0.0f && b.y == 0.0f) {
-      disps[k] = v2{finf(), finf()};
-    } else {
-      float len = sumsq(sub(a, b));
-      float t = dot(sub(pos, b), sub(a, b)) / len;
-      t = clip_(t, 0.0f, 1.0f);
-      disps[k] = sub(pos, add(b, scl(sub(a, b), t)));
+  const v2 last = vert(P, P.n - 1);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    dists[k] = 0.0f;
+    disps[k] = v2{0.0f, 0.0f};
+    if (k < P.n) {
+      v2 a = v2{P.w[2 * k], P.w[2 * k + 1]}, b = k == 0 ? last : v2{P.w[2 * k - 2], P.w[2 * k - 1]};
+      if (a.x == 0.0f && a.y == 0.0f && b.x == 0.0f && b.y == 0.0f) {
+        disps[k] = v2{finf(), finf()};
+      } else {
+        float len = sumsq(sub(a, b));
+        float t = dot(sub(pos, b), sub(a, b)) / len;
+        t = clip_(t, 0.0f, 1.0f);
+        disps[k] = sub(pos, add(b, scl(sub(a, b), t)));
+      }
+      dists[k] = sumsq(disps[k]);
     }
-    dists[k] = sumsq(disps[k]);
   }
-  int k = argmin_first(dists, P.n);
-  c.cp = add(pos, disps[k]);
-  if (dists[k] > C.d[0] * C.d[0]) c.cp = pos;
+  const int k = argmin_first_n<MAXV>(dists, P.n);
+  v2 dk = disps[0];
+  float sk = dists[0];
+#pragma unroll
+  for (int q = 1; q < MAXV; ++q)
+    if (q == k) { dk = disps[q]; sk = dists[q]; }
+  c.cp = add(pos, dk);
+  if (sk > C.d(0) * C.d(0)) c.cp = pos;
   return c;
 }
 

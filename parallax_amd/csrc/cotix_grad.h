@@ -46,8 +46,8 @@ CX_DEV v2 vjp_unit(v2 v, v2 g) {
 
 // aabb_vs_aabb (cotix/_contacts.py:61-96), contact branch
 CX_DEV void aabb_vs_aabb_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, float* ga, float* gb) {
-  const float alx = a.d[0], aly = a.d[1], aux = a.d[2], auy = a.d[3];
-  const float blx = b.d[0], bly = b.d[1], bux = b.d[2], buy = b.d[3];
+  const float alx = a.d(0), aly = a.d(1), aux = a.d(2), auy = a.d(3);
+  const float blx = b.d(0), bly = b.d(1), bux = b.d(2), buy = b.d(3);
   const float me = -1e-8f;
   const float X[4] = {auy - bly, buy - aly, aux - blx, bux - alx};
   float dep[4];
@@ -73,8 +73,8 @@ CX_DEV void aabb_vs_aabb_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, fl
 
 // circle_vs_circle (cotix/_contacts.py:30-58), contact branch
 CX_DEV void circle_vs_circle_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, float* ga, float* gb) {
-  const v2 ap = v2{a.d[1], a.d[2]}, bp = v2{b.d[1], b.d[2]};
-  const float ar = a.d[0], br = b.d[0];
+  const v2 ap = v2{a.d(1), a.d(2)}, bp = v2{b.d(1), b.d(2)};
+  const float ar = a.d(0), br = b.d(0);
   const v2 delta = sub(ap, bp);
   const float dist = nrm(delta);
   const bool zero = dist == 0.0f;
@@ -113,9 +113,9 @@ CX_DEV void circle_vs_circle_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp
 
 // circle_vs_aabb (cotix/_contacts.py:99-154), contact branch
 CX_DEV void circle_vs_aabb_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, float* ga, float* gb) {
-  const v2 ap = v2{a.d[1], a.d[2]};
-  const float r = a.d[0];
-  const v2 lo = v2{b.d[0], b.d[1]}, up = v2{b.d[2], b.d[3]};
+  const v2 ap = v2{a.d(1), a.d(2)};
+  const float r = a.d(0);
+  const v2 lo = v2{b.d(0), b.d(1)}, up = v2{b.d(2), b.d(3)};
   const v2 bc = v2{(lo.x + up.x) / 2.0f, (lo.y + up.y) / 2.0f};
   const v2 disp = sub(ap, bc);
   const v2 l = sub(lo, bc), h = sub(up, bc);

@@ -82,7 +82,7 @@ CX_HD Lay layout(int nb, int W, int nc, int nt) {
   Lay L;
   L.dyn = 0;
   L.world = L.dyn + nb * 6;
-  L.con = L.world + W;
+  L.con = L.world + W + 2 * cx::MAXV;  // slack: shape fetches read 2*MAXV words
   L.m = L.con + nc * 4;
   L.ch = L.m + nb * nb;
   L.key = L.ch + nb;
@@ -144,7 +144,8 @@ CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, con
 // contact-function sets compiled into a step kernel (scene feature mask)
 enum : int { FNS_ANALYTIC = 1, FNS_CONVEX = 2, FNS_CIRCLE_POLY = 4 };
 template <int FNSET>
-CX_DEV cx::Contact run_contact_set(int fn, const cx::Shape& a, const cx::Shape& b, cx::v2 d0, uint32_t* err) {
+CX_DEV cx::Contact run_contact_set(int fn, const cx::Shape& a, const cx::Shape& b, cx::v2 d0, uint32_t* err,
+                                   bool self_pair) {
   using namespace cx;
   if ((FNSET & FNS_ANALYTIC) != 0) {
     if (fn == FN_AABB_AABB) return aabb_vs_aabb(a, b);
@@ -152,7 +153,7 @@ CX_DEV cx::Contact run_contact_set(int fn, const cx::Shape& a, const cx::Shape& 
     if (fn == FN_CIRCLE_CIRCLE) return circle_vs_circle(a, b);
   }
   if ((FNSET & FNS_CONVEX) != 0) {
-    if (fn == FN_POLY_POLY || fn == FN_AABB_POLY) return convex_vs_polygon(a, b, d0);
+    if (fn == FN_POLY_POLY || fn == FN_AABB_POLY) return convex_vs_polygon(a, b, d0, !self_pair);
   }
   if ((FNSET & FNS_CIRCLE_POLY) != 0) {
     if (fn == FN_CIRCLE_POLY) return circle_vs_polygon(a, b, d0);
@@ -334,16 +335,23 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       float s, cs;
       sincos32(t.f(o + 4, e), &s, &cs);
       float xy[2 * MAXV];
-      for (int k = 0; k < n; ++k) {
-        float x = lg[2 * k], y = lg[2 * k + 1];
-        float t0 = (cs * x + (-s) * y) + px * 1.0f;
-        float t1 = (s * x + cs * y) + py * 1.0f;
-        float t2 = (0.0f * x + 0.0f * y) + 1.0f * 1.0f;
-        xy[2 * k] = t0 / t2;
-        xy[2 * k + 1] = t1 / t2;
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) {
+        xy[2 * k] = 0.0f;
+        xy[2 * k + 1] = 0.0f;
+        if (k < n) {
+          float x = lg[2 * k], y = lg[2 * k + 1];
+          float t0 = (cs * x + (-s) * y) + px * 1.0f;
+          float t1 = (s * x + cs * y) + py * 1.0f;
+          float t2 = (0.0f * x + 0.0f * y) + 1.0f * 1.0f;
+          xy[2 * k] = t0 / t2;
+          xy[2 * k + 1] = t1 / t2;
+        }
       }
       order_clockwise(xy, n);
-      for (int k = 0; k < 2 * n; ++k) t.f(wo + k, e) = xy[k];
+#pragma unroll
+      for (int k = 0; k < 2 * MAXV; ++k)
+        if (k < 2 * n) t.f(wo + k, e) = xy[k];
     }
   }
 }
@@ -359,29 +367,22 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     if (g >= a.B) continue;
     const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
     const int fn = (int)((d0w >> 20) & 7u);
+    const int wa = c.L.world + (int)(d0w & 1023u), wb = c.L.world + (int)((d0w >> 10) & 1023u);
     Shape A, Bs;
     A.kind = (int)((d0w >> 23) & 3u);
     Bs.kind = (int)((d0w >> 25) & 3u);
     A.n = (int)(d1w & 255u);
     Bs.n = (int)((d1w >> 8) & 255u);
-    const int wa = c.L.world + (int)(d0w & 1023u), wb = c.L.world + (int)((d0w >> 10) & 1023u);
-    if (FNSET == FNS_ANALYTIC) {
+    // one unconditional fetch of both shapes (the world region is followed
+    // by 2*MAXV words of slack, so every read stays inside the tile)
+    const int nw = FNSET == FNS_ANALYTIC ? 4 : 2 * MAXV;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        A.d[k] = t.f(wa + k, e);
-        Bs.d[k] = t.f(wb + k, e);
-      }
-    } else {
-      const int na = A.kind == KIND_POLY ? 2 * A.n : 4;
-      const int nbf = Bs.kind == KIND_POLY ? 2 * Bs.n : 4;
-#pragma unroll
-      for (int k = 0; k < 2 * MAXV; ++k) {
-        A.d[k] = (k < na) ? t.f(wa + k, e) : 0.0f;
-        Bs.d[k] = (k < nbf) ? t.f(wb + k, e) : 0.0f;
-      }
+    for (int k = 0; k < 2 * MAXV; ++k) {
+      A.w[k] = k < nw ? t.f(wa + k, e) : 0.0f;
+      Bs.w[k] = k < nw ? t.f(wb + k, e) : 0.0f;
     }
     uint32_t er = 0u;
-    Contact ct = run_contact_set<FNSET>(fn, A, Bs, d0, &er);
+    Contact ct = run_contact_set<FNSET>(fn, A, Bs, d0, &er, ((d0w >> 27) & 1u) != 0u);
     const int co = c.L.con + 4 * ci;
     t.f(co + 0, e) = ct.pen.x;
     t.f(co + 1, e) = ct.pen.y;
@@ -732,14 +733,15 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         // the contact: fn(world(part pa), world(part pb)); world = local + body position
         const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
         const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
+        const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
         Shape SA, SB;
         SA.kind = ka;
         SB.kind = kb;
         SA.n = SB.n = 0;
-        const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
+        for (int k = 0; k < 2 * MAXV; ++k) SA.w[k] = SB.w[k] = 0.0f;
         for (int k = 0; k < 4; ++k) {
-          SA.d[k] = t.f(wa + k, e);
-          SB.d[k] = t.f(wb + k, e);
+          SA.w[k] = t.f(wa + k, e);
+          SB.w[k] = t.f(wb + k, e);
         }
         float ga[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         contact_vjp(fn, SA, SB, gpen, gcp, ga, gb);

@@ -184,7 +184,8 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
     const int pa = cpa[c], pb = cpb[c];
     if (part_woffv[pa] > 1023 || part_woffv[pb] > 1023) return scene_fail(err, "world table too large");
     hot.push_back((uint32_t)part_woffv[pa] | ((uint32_t)part_woffv[pb] << 10) | ((uint32_t)cfn[c] << 20) |
-                  ((uint32_t)part_kindv[pa] << 23) | ((uint32_t)part_kindv[pb] << 25));
+                  ((uint32_t)part_kindv[pa] << 23) | ((uint32_t)part_kindv[pb] << 25) |
+                  ((uint32_t)(pa == pb) << 27));  // a part paired with itself: penetration never used
     hot.push_back((uint32_t)part_nv[pa] | ((uint32_t)part_nv[pb] << 8));
   }
   s.nmw = (s.nc + 31) / 32;

@@ -104,14 +104,15 @@ __device__ __forceinline__ cx::Shape load_shape(const float* p) {
   cx::Shape s;
   s.kind = (int)p[0];
   s.n = (int)p[1];
-  for (int k = 0; k < 2 * cx::MAXV; ++k) s.d[k] = p[2 + k];
+#pragma unroll
+  for (int k = 0; k < 2 * cx::MAXV; ++k) s.w[k] = p[2 + k];
   return s;
 }
 __global__ void contacts_kernel(int fn, int n, const float* a, const float* b, float* out, uint32_t* err, float d0x,
                                 float d0y) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  cx::Shape A = load_shape(a + 18 * (size_t)i), Bs = load_shape(b + 18 * (size_t)i);
+  const cx::Shape A = load_shape(a + 18 * (size_t)i), Bs = load_shape(b + 18 * (size_t)i);
   uint32_t er = 0u;
   cx::Contact c = cx::run_contact(fn, A, Bs, cx::v2{d0x, d0y}, &er);
   out[4 * (size_t)i + 0] = c.pen.x;

@@ -152,8 +152,8 @@ int emu_contacts(int fn, int n, const float* a, const float* b, float* out, uint
     Bs.kind = (int)b[18 * i];
     Bs.n = (int)b[18 * i + 1];
     for (int k = 0; k < 16; ++k) {
-      A.d[k] = a[18 * i + 2 + k];
-      Bs.d[k] = b[18 * i + 2 + k];
+      A.w[k] = a[18 * i + 2 + k];
+      Bs.w[k] = b[18 * i + 2 + k];
     }
     uint32_t er = 0;
     cx::Contact c = cx::run_contact(fn, A, Bs, dd, &er);
@@ -165,4 +165,14 @@ int emu_contacts(int fn, int n, const float* a, const float* b, float* out, uint
   }
   return 0;
 }
+}
+
+extern "C" int emu_order_clockwise(float* xy, int n, int nv) {
+  for (int i = 0; i < n; ++i) {
+    float v[2 * cx::MAXV] = {};
+    for (int k = 0; k < 2 * nv; ++k) v[k] = xy[(size_t)i * 2 * nv + k];
+    cx::order_clockwise(v, nv);
+    for (int k = 0; k < 2 * nv; ++k) xy[(size_t)i * 2 * nv + k] = v[k];
+  }
+  return 0;
 }

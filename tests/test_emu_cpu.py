@@ -75,3 +75,28 @@ def test_emu_box_world_trace(emu_lib):
     for e in range(tr["dyn"].shape[1]):
         sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err")}
         run_trace(emu, lib, mg.box_world_bodies(e), None, sub, 1 | 4 | 16, 2, False)
+
+
+def test_emu_order_clockwise_ties_nan_zero(emu_lib):
+    """Stable order by angle (the kernel's rank sort) == the oracle's
+    insertion sort, on duplicate vertices (ties), NaN coordinates and
+    vertices whose angle is +-0 / +-pi."""
+    emu, lib = emu_lib
+    from cotix_oracle import geometry as G
+    rng = np.random.default_rng(4)
+    cases = []
+    for nv in (3, 4, 6, 8):
+        for _ in range(200):
+            xy = rng.integers(-2, 3, size=(nv, 2)).astype(np.float32)  # many duplicates / collinear
+            if rng.random() < 0.2:
+                xy[rng.integers(nv), rng.integers(2)] = np.nan
+            if rng.random() < 0.2:
+                xy[rng.integers(nv)] = (-0.0, 0.0)
+            cases.append(xy)
+    for xy in cases:
+        nv = xy.shape[0]
+        got = np.ascontiguousarray(xy.reshape(-1).copy())
+        lib.emu_order_clockwise(got.ctypes.data_as(emu.P_), 1, nv)
+        want = np.array(G.order_clockwise([tuple(v) for v in xy]), np.float32).reshape(-1)
+        same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+        assert same.all(), (xy, got.reshape(-1, 2), want.reshape(-1, 2))

@@ -208,15 +208,18 @@ def main():
         },
     }
     # HBM traffic per launch from the committed rocprofv3 PMC pass of the same
-    # workload (profiles/latest_pmc.json, tools/gpu_profile.sh); FETCH_SIZE
-    # doubled per MI355X_MICROARCH.md "HBM" (gfx950 reports half the bytes).
+    # workload (profiles/latest_pmc_<scenario>.json, tools/gpu_round.sh);
+    # FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM" (gfx950 reports half
+    # the bytes).  The same pass gives the VALU issue fraction -- the bound
+    # that actually limits this path.
     try:
-        pmc = json.load(open(os.path.join(ROOT, "profiles", "latest_pmc.json")))
+        pmc = json.load(open(os.path.join(ROOT, "profiles", "latest_pmc_%s.json" % a.scenario)))
         c = pmc["config"]
         if (c.get("envs_per_gpu") == B and c.get("substeps_per_launch") == a.substeps
                 and c.get("workload", "").split()[0] == out["config"]["workload"].split()[0]):
             out["roofline"]["traffic"] = pmc["hbm_bytes_per_launch_corrected"]
-            out["roofline"]["traffic_source"] = "profiles/%s_summary.json" % pmc["tag"]
+            out["roofline"]["traffic_source"] = "profiles/%s_%s_summary.json" % (pmc["tag"], a.scenario)
+            out["roofline"]["valu_issue_frac"] = pmc["valu_active_frac_of_wave_cycles"]
     except (OSError, KeyError, ValueError):
         pass
     if rank == 0 and a.cpu_baseline == "auto":

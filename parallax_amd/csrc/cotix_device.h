@@ -213,13 +213,23 @@ struct Shape {
   float w[2 * MAXV];
   CX_MF float d(int k) const { return w[k]; }
 };
-// vertex k, k varying per lane: select chain (constant-folds for constant k)
+CX_DEV uint32_t f2u(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+// vertex k, k varying per lane (0 <= k < MAXV): masked OR of the bit
+// patterns (a plain select chain gets rewritten by LLVM into an indexed
+// load from a scratch copy of the array); constant-folds for constant k
 CX_DEV v2 vert(const Shape& s, int k) {
-  v2 r = v2{s.w[0], s.w[1]};
+  uint32_t x = 0u, y = 0u;
 #pragma unroll
-  for (int q = 1; q < MAXV; ++q)
-    if (q == k) r = v2{s.w[2 * q], s.w[2 * q + 1]};
-  return r;
+  for (int q = 0; q < MAXV; ++q) {
+    const uint32_t m = 0u - (uint32_t)(q == k);
+    x |= f2u(s.w[2 * q]) & m;
+    y |= f2u(s.w[2 * q + 1]) & m;
+  }
+  return v2{__uint_as_float(x), __uint_as_float(y)};
 }
 // argmin over v[0..n), n <= N at run time: first NaN, else first minimum
 template <int N>
@@ -311,19 +321,22 @@ CX_DEV bool poly_contains(const Shape& s, v2 p) {  // :168-175, edge k = (v_k, v
 // goes to #{j : ang_j < ang_k} + #{j < k : ang_j ~ ang_k} under sort_lt (a
 // strict weak order: NaN last, -0 ~ +0), the same permutation insertion sort
 // produces -- with every loop unrolled to MAXV (register-only, no scratch).
-CX_DEV void order_clockwise(float* xy, int n) {
+struct Poly {
+  float x[MAXV], y[MAXV];
+};
+CX_DEV Poly order_clockwise(const Poly& q, int n) {
   float sx = 0.0f, sy = 0.0f;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k)
     if (k < n) {
-      sx = sx + xy[2 * k];
-      sy = sy + xy[2 * k + 1];
+      sx = sx + q.x[k];
+      sy = sy + q.y[k];
     }
   const float fn = (float)n;
   const float mx = sx / fn, my = sy / fn;
   float ang[MAXV];
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) ang[k] = k < n ? atan2_32(xy[2 * k + 1] - my, xy[2 * k] - mx) : 0.0f;
+  for (int k = 0; k < MAXV; ++k) ang[k] = k < n ? atan2_32(q.y[k] - my, q.x[k] - mx) : 0.0f;
   int rank[MAXV];
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
@@ -333,21 +346,33 @@ CX_DEV void order_clockwise(float* xy, int n) {
       if (j != k && j < n) r += (sort_lt(ang[j], ang[k]) || (j < k && !sort_lt(ang[k], ang[j]))) ? 1 : 0;
     rank[k] = r;
   }
-  float out[2 * MAXV];
+  Poly out;
 #pragma unroll
   for (int p = 0; p < MAXV; ++p) {
-    float x = xy[2 * p], y = xy[2 * p + 1];
+    float x = q.x[p], y = q.y[p];
 #pragma unroll
     for (int k = 0; k < MAXV; ++k)
       if (k < n && rank[k] == p) {
-        x = xy[2 * k];
-        y = xy[2 * k + 1];
+        x = q.x[k];
+        y = q.y[k];
       }
-    out[2 * p] = x;
-    out[2 * p + 1] = y;
+    out.x[p] = x;
+    out.y[p] = y;
   }
+  return out;
+}
+CX_DEV void order_clockwise(float* xy, int n) {  // interleaved form (operator kernel, tests)
+  Poly q;
 #pragma unroll
-  for (int k = 0; k < 2 * MAXV; ++k) xy[k] = out[k];
+  for (int k = 0; k < MAXV; ++k) {
+    q.x[k] = k < n ? xy[2 * k] : 0.0f;
+    q.y[k] = k < n ? xy[2 * k + 1] : 0.0f;
+  }
+  const Poly r = order_clockwise(q, n);
+  for (int k = 0; k < n; ++k) {
+    xy[2 * k] = r.x[k];
+    xy[2 * k + 1] = r.y[k];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -503,21 +528,68 @@ CX_DEV float edge_dist(v2 a, v2 b) {  // distance_to_origin :137-154,168-169
   return sumsq(disp);
 }
 
+// EPA edge storage: registers (operator kernels, host; dynamic indices as
+// select chains) or a per-lane LDS column of the step kernel's wave scratch
+// (dynamic indices native, keeps ~4*NE floats out of the VGPR budget).
 template <int NE>
-CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters) {
+struct EdgeRegs {
   v2 e0[NE], e1[NE];
+  CX_MF v2 g0(int k) const {
+    v2 r = e0[0];
+#pragma unroll
+    for (int q = 1; q < NE; ++q)
+      if (q == k) r = e0[q];
+    return r;
+  }
+  CX_MF v2 g1(int k) const {
+    v2 r = e1[0];
+#pragma unroll
+    for (int q = 1; q < NE; ++q)
+      if (q == k) r = e1[q];
+    return r;
+  }
+  CX_MF void s0(int k, v2 v) {
+#pragma unroll
+    for (int q = 0; q < NE; ++q)
+      if (q == k) e0[q] = v;
+  }
+  CX_MF void s1(int k, v2 v) {
+#pragma unroll
+    for (int q = 0; q < NE; ++q)
+      if (q == k) e1[q] = v;
+  }
+};
+struct EdgeCol {  // edge k, component c at p[(4k + c) * st]
+  float* p;
+  int st;
+  CX_MF v2 g0(int k) const { return v2{p[(4 * k) * st], p[(4 * k + 1) * st]}; }
+  CX_MF v2 g1(int k) const { return v2{p[(4 * k + 2) * st], p[(4 * k + 3) * st]}; }
+  CX_MF void s0(int k, v2 v) {
+    p[(4 * k) * st] = v.x;
+    p[(4 * k + 1) * st] = v.y;
+  }
+  CX_MF void s1(int k, v2 v) {
+    p[(4 * k + 2) * st] = v.x;
+    p[(4 * k + 3) * st] = v.y;
+  }
+};
+
+template <int NE, class ES>
+CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters, ES& es) {
   float dist[NE];
+  const v2 z = v2{0.0f, 0.0f};
 #pragma unroll
   for (int k = 0; k < NE; ++k) {
-    e0[k] = v2{0.0f, 0.0f};
-    e1[k] = v2{0.0f, 0.0f};
+    es.s0(k, z);
+    es.s1(k, z);
   }
-  e0[0] = simplex[0]; e1[0] = simplex[1];
-  e0[1] = simplex[1]; e1[1] = simplex[2];
-  e0[2] = simplex[2]; e1[2] = simplex[0];
+  es.s0(0, simplex[0]); es.s1(0, simplex[1]);
+  es.s0(1, simplex[1]); es.s1(1, simplex[2]);
+  es.s0(2, simplex[2]); es.s1(2, simplex[0]);
   const int ne = iters + 3;
+  const v2 sim[3] = {simplex[0], simplex[1], simplex[2]};
 #pragma unroll
-  for (int k = 0; k < NE; ++k) dist[k] = (k < ne) ? edge_dist(e0[k], e1[k]) : finf();
+  for (int k = 0; k < NE; ++k) dist[k] = (k < 3) ? edge_dist(sim[k], sim[(k + 1) % 3]) : ((k < ne) ? edge_dist(z, z) : finf());
   auto argmin_d = [&]() {
     int nanidx = -1, b = 0;
     float bv = dist[0];
@@ -534,12 +606,9 @@ CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters) {
     return nanidx >= 0 ? nanidx : b;
   };
   int bei = argmin_d();
-  v2 best0 = e0[0], best1 = e1[0];
-#pragma unroll
-  for (int k = 0; k < NE; ++k)
-    if (k == bei) { best0 = e0[k]; best1 = e1[k]; }
+  v2 best0 = es.g0(bei), best1 = es.g1(bei);
   v2 newp = simplex[2];
-  v2 prev0 = e0[0], prev1 = e1[0];
+  v2 prev0 = simplex[0], prev1 = simplex[1];
   for (int i = 0; i < iters; ++i) {
     bool c1 = sumsq(sub(best0, best1)) > 1e-9f;
     bool c2 = crs(best0, best1) >= 0.0f;
@@ -554,22 +623,26 @@ CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters) {
     newp = minkowski(a, b, n);
     const int slot = i + 3;
     const float dA = edge_dist(best0, newp), dB = edge_dist(newp, best1);
+    es.s1(bei, newp);
+    es.s0(slot, newp);
+    es.s1(slot, best1);
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
-      if (k == bei) { e1[k] = newp; dist[k] = dA; }
-    }
-#pragma unroll
-    for (int k = 0; k < NE; ++k) {
-      if (k == slot) { e0[k] = newp; e1[k] = best1; dist[k] = dB; }
+      if (k == bei) dist[k] = dA;
+      if (k == slot) dist[k] = dB;
     }
     prev0 = best0;
     prev1 = best1;
     bei = argmin_d();
-#pragma unroll
-    for (int k = 0; k < NE; ++k)
-      if (k == bei) { best0 = e0[k]; best1 = e1[k]; }
+    best0 = es.g0(bei);
+    best1 = es.g1(bei);
   }
   return closest_on_edge_to_origin(best0, best1);
+}
+template <int NE>
+CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters) {
+  EdgeRegs<NE> es;
+  return epa<NE>(a, b, simplex, iters, es);
 }
 
 // generic-iteration EPA (circle_vs_polygon uses 128 iterations): buffer in
@@ -693,24 +766,96 @@ CX_DEV v2 contact_from_edges(const Shape& A, const Shape& B) {
 // polygon_vs_polygon :294-315 / aabb_vs_polygon :270-291 (A may be an AABB).
 // EPA runs iters = |A| + |B| + 1 <= 2*MAXV + 1 steps: at most 20 edges, so
 // the edge buffer is a compile-time register array (epa<14> / epa<20>).
-// need_pen = false (the step kernel, for a part paired with itself: such a
-// cell is only ever chosen as j == i, which resolution skips, so only the
-// NaN-ness of the contact point is observable) skips EPA; pen is then 0.
-CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, v2 d0, bool need_pen = true) {
+// GJK, then EPA when the penetration is needed (need_pen = false: the step
+// kernel, for a part paired with itself -- such a cell is only ever chosen as
+// j == i, which resolution skips, so only the NaN-ness of the contact point
+// is observable; pen is then 0).  Returns whether the shapes collide.
+template <class MakeStore>
+CX_DEV bool gjk_epa(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen, MakeStore make) {
   static_assert(2 * MAXV + 1 + 3 <= 20, "EPA buffer bound");
   v2 simplex[3];
-  if (!gjk(A, B, d0, simplex)) return nan_contact();
+  *pen = v2{0.0f, 0.0f};
+  if (!gjk(A, B, d0, simplex)) return false;
   const int iters = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
-  Contact c;
-  c.pen = v2{0.0f, 0.0f};
-  if (!need_pen) {
-  } else if (iters + 3 <= 14) {
-    c.pen = epa<14>(A, B, simplex, iters);
+  if (!need_pen) return true;
+  if (iters + 3 <= 14) {
+    auto es = make.template get<14>();
+    *pen = epa<14>(A, B, simplex, iters, es);
   } else {
-    c.pen = epa<20>(A, B, simplex, iters);
+    auto es = make.template get<20>();
+    *pen = epa<20>(A, B, simplex, iters, es);
   }
+  return true;
+}
+struct MakeRegs {
+  template <int NE>
+  CX_MF EdgeRegs<NE> get() const { return EdgeRegs<NE>{}; }
+};
+struct MakeCol {
+  float* p;
+  int st;
+  template <int NE>
+  CX_MF EdgeCol get() const { return EdgeCol{p, st}; }
+};
+// GJK, then EPA when the penetration is needed; EPA edges in registers
+CX_DEV bool convex_vs_polygon_pen(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen) {
+  return gjk_epa(A, B, d0, need_pen, pen, MakeRegs{});
+}
+// the same with EPA edges in a per-lane memory column (the step kernel's LDS)
+CX_DEV bool convex_vs_polygon_pen_col(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen, float* col,
+                                      int stride) {
+  return gjk_epa(A, B, d0, need_pen, pen, MakeCol{col, stride});
+}
+CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, v2 d0, bool need_pen = true) {
+  Contact c;
+  if (!convex_vs_polygon_pen(A, B, d0, need_pen, &c.pen)) return nan_contact();
   c.cp = contact_from_edges(A, B);
   return c;
+}
+
+// contact_from_edges split into independent terms, for the wave-cooperative
+// evaluation in the step kernel: term s (0 <= s < cfe_terms) is a vertex of
+// A inside B (s < |A|), a vertex of B inside A, or the intersection of B-edge
+// jb and A-edge ia (B-edge-major); NaN = no contribution.  Summing the terms
+// in s order reproduces contact_from_edges exactly.
+CX_DEV int cfe_terms(const Shape& A, const Shape& B) {
+  const int na = cvx_count(A), nb = cvx_count(B);
+  return na + nb + na * nb;
+}
+// vertex k (varying per lane) of an AABB from its 4 words, or of a polygon
+// through the caller's fetch (the step kernel reads it from LDS)
+template <class VF>
+CX_DEV v2 cvx_vert_d(const Shape& s, int k, VF vf) {
+  if (s.kind == KIND_AABB) {
+    const float x = (k == 0 || k == 1) ? s.w[2] : s.w[0];
+    const float y = (k == 0 || k == 3) ? s.w[3] : s.w[1];
+    return v2{x, y};
+  }
+  return vf(k);
+}
+template <class VF>
+CX_DEV void cvx_edge_d(const Shape& s, int k, VF vf, v2* e0, v2* e1) {
+  *e0 = cvx_vert_d(s, k, vf);
+  if (s.kind == KIND_AABB) *e1 = cvx_vert_d(s, (k + 1) & 3, vf);
+  else *e1 = vf(k == 0 ? s.n - 1 : k - 1);
+}
+template <class VFA, class VFB>
+CX_DEV v2 cfe_term(const Shape& A, const Shape& B, int s, VFA va, VFB vb) {
+  const int na = cvx_count(A), nb = cvx_count(B);
+  const v2 nanv = v2{qnan(), qnan()};
+  if (s < na) {
+    const v2 v = cvx_vert_d(A, s, va);
+    return shape_contains(B, v) ? v : nanv;
+  }
+  if (s < na + nb) {
+    const v2 v = cvx_vert_d(B, s - na, vb);
+    return shape_contains(A, v) ? v : nanv;
+  }
+  const int q = s - na - nb, jb = q / na, ia = q - jb * na;
+  v2 a0, a1, b0, b1;
+  cvx_edge_d(A, ia, va, &a0, &a1);
+  cvx_edge_d(B, jb, vb, &b0, &b1);
+  return edge_vs_edge(a0, a1, b0, b1);
 }
 
 // circle_vs_polygon :157-202

@@ -45,6 +45,7 @@ struct SceneDev {
   int o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts
   int o_cmask;  // per cell nmw words: bitmask of the cell's distinct contacts
   int nmw;      // contact-mask words = ceil(nc / 32)
+  int poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
   int nhot;
   uint32_t hot[MAXHOT];
 };
@@ -75,10 +76,10 @@ struct KArgs {
 
 // per-wave tile layout (words, each x EW envs)
 struct Lay {
-  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, S;
+  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, geo, S;
 };
 constexpr int REC_W = 7;  // per resolution: applied flag, v/w of body i, v/w of body j (pre-resolution)
-CX_HD Lay layout(int nb, int W, int nc, int nt) {
+CX_HD Lay layout(int nb, int W, int nc, int nt, int G) {
   Lay L;
   L.dyn = 0;
   L.world = L.dyn + nb * 6;
@@ -95,17 +96,38 @@ CX_HD Lay layout(int nb, int W, int nc, int nt) {
   L.rec = L.adj + nb * 6;
   L.vm = L.rec + nb * REC_W;        // bit c: contact c has a contact point this step
   L.rst = L.vm + (nc + 31) / 32;    // restart state (autoreset), staged once per launch
-  L.S = L.rst + nb * 6;
+  L.geo = L.rst + nb * 6;           // local part geometry (per env), staged once per launch
+  L.S = L.geo + G;
   return L;
 }
-static inline int tile_words(const SceneDev& s) { return layout(s.nb, s.W, s.nc, s.nt).S; }
+static inline int tile_words(const SceneDev& s) { return layout(s.nb, s.W, s.nc, s.nt, s.G).S; }
 // per-wave scratch of phase C (words, not per env): pass flags, keep flags,
 // active count, two item lists (double buffer), per-item scan positions
 enum : int { WS_FLAG = 0, WS_KEEP = 64, WS_N = 128, WS_LIST = 129 };
-CX_HD int ws_words(int nl, int ew) { return WS_LIST + 3 * nl * ew; }
+// + (polygon scenes) the deferred contact-point area of phase F: per-item
+// flags and list (padded to 64), count, per-batch term counts, term results
+constexpr int CFB = 8;                           // items per batch
+constexpr int CFS = 2 * cx::MAXV + cx::MAXV * cx::MAXV;  // max terms per item
+constexpr int EPA_NE = 20;                        // EPA edge column length (epa<20> bound)
+struct WsLay {
+  int cf_flag, cf_list, cf_n, cf_s, cf_res, epa, words;
+};
+CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly) {
+  WsLay w;
+  const int pad = ((nc * ew + 63) / 64) * 64;
+  w.cf_flag = WS_LIST + 3 * nl * ew;
+  w.cf_list = w.cf_flag + pad;
+  w.cf_n = w.cf_list + pad;
+  w.cf_s = w.cf_n + 1;
+  w.cf_res = w.cf_s + CFB;
+  w.epa = w.cf_res + CFB * CFS * 2;  // per-lane EPA edge columns, [4*EPA_NE][64]
+  w.words = poly ? w.epa + 4 * EPA_NE * 64 : w.cf_flag;
+  return w;
+}
+CX_HD int ws_words(const SceneDev& s, int ew) { return ws_layout(s.nl, s.nc, ew, s.poly).words; }
 // LDS bytes of a workgroup of wpb waves x ew envs
 static inline size_t lds_bytes(const SceneDev& s, int wpb, int ew) {
-  return 4 * ((size_t)s.nhot + ((size_t)tile_words(s) * ew + (size_t)ws_words(s.nl, ew)) * wpb);
+  return 4 * ((size_t)s.nhot + ((size_t)tile_words(s) * ew + (size_t)ws_words(s, ew)) * wpb);
 }
 
 CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, const cx::Params& pl,
@@ -237,14 +259,29 @@ struct Ctx {
   int nb, np, nc, nl, nt;
   const SceneDev* sc;
   Lay L;
+  WsLay W;
 };
+
+// local part geometry of the wave's envs: read from HBM once per launch, not
+// once per step (per-env LunarLander terrain)
+template <int EW>
+CX_DEV void ph_geo(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  if (a.geom == nullptr) return;
+  for (int w = lane; w < c.sc->G * EW; w += WAVE) {
+    int e = w % EW, k = w / EW, g = env0 + e;
+    t.f(c.L.geo + k, e) = (g < a.B) ? a.geom[(a.gstride ? (size_t)g * a.gstride : (size_t)0) + k] : 0.0f;
+  }
+}
 
 template <int EW>
 CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  if (c.sc->poly)  // phase F's flag array incl. its padding to a multiple of 64
+    for (int w = lane; w < c.W.cf_list - c.W.cf_flag; w += WAVE) t.ws[c.W.cf_flag + w] = 0u;
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
     t.f(c.L.dyn + off, e) = (g < a.B) ? a.dyn[(size_t)off * a.B + g] : 0.0f;
   }
+  ph_geo<EW>(a, c, t, env0, lane);
   if (a.dyn_reset != nullptr)
     for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
       int e = w % EW, off = w / EW, g = env0 + e;
@@ -315,7 +352,7 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     int e = w % EW, p = w / EW, g = env0 + e;
     if (g >= a.B) continue;
     const int b = t.ti(sc.o_pbody + p), kind = t.ti(sc.o_pkind + p);
-    const float* lg = a.geom + (a.gstride ? (size_t)g * a.gstride : (size_t)0) + t.ti(sc.o_pgoff + p);
+    const int lgo = c.L.geo + t.ti(sc.o_pgoff + p);  // this part's local geometry in the tile
     const int o = c.L.dyn + b * 6, wo = c.L.world + t.ti(sc.o_pwoff + p);
     const float px = t.f(o + 0, e), py = t.f(o + 1, e);
     if (FNSET == FNS_ANALYTIC || kind != KIND_POLY) {
@@ -325,7 +362,7 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       // (a divergent circle/AABB tail was miscompiled by hipcc 7.2: the
       // circle lanes read an address register only the AABB lanes defined).
       const bool circ = kind == KIND_CIRCLE;
-      const float g0 = lg[0], g1 = lg[1], g2 = lg[2], g3 = lg[3];
+      const float g0 = t.f(lgo, e), g1 = t.f(lgo + 1, e), g2 = t.f(lgo + 2, e), g3 = t.f(lgo + 3, e);
       t.f(wo + 0, e) = circ ? g0 : g0 + px;
       t.f(wo + 1, e) = circ ? g1 + px : g1 + py;
       t.f(wo + 2, e) = circ ? g2 + py : g2 + px;
@@ -334,24 +371,29 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       const int n = t.ti(sc.o_pn + p);
       float s, cs;
       sincos32(t.f(o + 4, e), &s, &cs);
-      float xy[2 * MAXV];
+      Poly q;
 #pragma unroll
       for (int k = 0; k < MAXV; ++k) {
-        xy[2 * k] = 0.0f;
-        xy[2 * k + 1] = 0.0f;
+        q.x[k] = 0.0f;
+        q.y[k] = 0.0f;
         if (k < n) {
-          float x = lg[2 * k], y = lg[2 * k + 1];
+          float x = t.f(lgo + 2 * k, e), y = t.f(lgo + 2 * k + 1, e);
           float t0 = (cs * x + (-s) * y) + px * 1.0f;
           float t1 = (s * x + cs * y) + py * 1.0f;
+          // w = (0*x + 0*y) + 1*1 is exactly 1 (or NaN when x or y is
+          // infinite), so t/w == (w == 1 ? t : NaN) bit for bit
           float t2 = (0.0f * x + 0.0f * y) + 1.0f * 1.0f;
-          xy[2 * k] = t0 / t2;
-          xy[2 * k + 1] = t1 / t2;
+          q.x[k] = t2 == 1.0f ? t0 : cx::qnan();
+          q.y[k] = t2 == 1.0f ? t1 : cx::qnan();
         }
       }
-      order_clockwise(xy, n);
+      const Poly o = order_clockwise(q, n);
 #pragma unroll
-      for (int k = 0; k < 2 * MAXV; ++k)
-        if (k < 2 * n) t.f(wo + k, e) = xy[k];
+      for (int k = 0; k < MAXV; ++k)
+        if (k < n) {
+          t.f(wo + 2 * k, e) = o.x[k];
+          t.f(wo + 2 * k + 1, e) = o.y[k];
+        }
     }
   }
 }
@@ -364,6 +406,7 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   const v2 d0 = v2{sc.d0x, sc.d0y};
   for (int w = lane; w < c.nc * EW; w += WAVE) {
     int e = w % EW, ci = w / EW, g = env0 + e;
+    if ((FNSET & FNS_CONVEX) != 0 && sc.poly) t.ws[c.W.cf_flag + w] = 0u;
     if (g >= a.B) continue;
     const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
     const int fn = (int)((d0w >> 20) & 7u);
@@ -382,7 +425,16 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       Bs.w[k] = k < nw ? t.f(wb + k, e) : 0.0f;
     }
     uint32_t er = 0u;
-    Contact ct = run_contact_set<FNSET>(fn, A, Bs, d0, &er, ((d0w >> 27) & 1u) != 0u);
+    Contact ct;
+    if ((FNSET & FNS_CONVEX) != 0 && (fn == FN_POLY_POLY || fn == FN_AABB_POLY)) {
+      // GJK (+EPA); the contact point is deferred to phase F (wave-cooperative)
+      const bool hit = convex_vs_polygon_pen_col(A, Bs, d0, ((d0w >> 27) & 1u) == 0u, &ct.pen,
+                                                 reinterpret_cast<float*>(t.ws + c.W.epa + lane), WAVE);
+      ct.cp = v2{qnan(), qnan()};
+      if (hit) t.ws[c.W.cf_flag + w] = 1u;
+    } else {
+      ct = run_contact_set<FNSET>(fn, A, Bs, d0, &er, ((d0w >> 27) & 1u) != 0u);
+    }
     const int co = c.L.con + 4 * ci;
     t.f(co + 0, e) = ct.pen.x;
     t.f(co + 1, e) = ct.pen.y;
@@ -402,6 +454,118 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       t.w(c.L.err, e) |= er;
 #endif
     }
+  }
+}
+
+// phase F: deferred polygon contact points (contact_from_edges,
+// cotix/_contacts.py:205-267).  Each colliding polygon item (contact, env)
+// has |A| + |B| + |A||B| independent terms; batches of CFB items spread their
+// terms over the 64 lanes (F2), then one lane per item sums its terms in the
+// reference's order (F3), which is bit-identical to the serial loop.
+// F0: compact the flagged items of chunk `chunk` into the item list
+template <int EW>
+CX_DEV void ph_F0(const Ctx& c, Tile<EW> t, int lane, int chunk) {
+  const uint64_t mask = wave_ballot(t.ws + c.W.cf_flag + chunk * WAVE, lane);
+  const uint32_t base = chunk == 0 ? 0u : t.ws[c.W.cf_n];
+  if (t.ws[c.W.cf_flag + chunk * WAVE + lane] != 0u)
+    t.ws[c.W.cf_list + base + popc64(mask & lanes_below(lane))] = (uint32_t)(chunk * WAVE + lane);
+  if (lane == WAVE - 1) t.ws[c.W.cf_n] = base + (uint32_t)popc64(mask);
+}
+template <int EW>
+CX_DEV void cf_shapes(const Ctx& c, Tile<EW> t, int id, cx::Shape* A, cx::Shape* B, int* wa, int* wb) {
+  const SceneDev& sc = *c.sc;
+  const int e = id % EW, ci = id / EW;
+  const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
+  A->kind = (int)((d0w >> 23) & 3u);
+  B->kind = (int)((d0w >> 25) & 3u);
+  A->n = (int)(d1w & 255u);
+  B->n = (int)((d1w >> 8) & 255u);
+  *wa = c.L.world + (int)(d0w & 1023u);
+  *wb = c.L.world + (int)((d0w >> 10) & 1023u);
+#pragma unroll
+  for (int k = 0; k < 2 * cx::MAXV; ++k) {
+    A->w[k] = t.f(*wa + k, e);
+    B->w[k] = t.f(*wb + k, e);
+  }
+}
+// F1: term counts of the batch starting at item b
+template <int EW>
+CX_DEV void ph_F1(const Ctx& c, Tile<EW> t, int lane, int b) {
+  if (lane >= CFB) return;
+  const int n = (int)t.ws[c.W.cf_n];
+  uint32_t cnt = 0u;
+  if (b + lane < n) {
+    const int id = (int)t.ws[c.W.cf_list + b + lane];
+    const SceneDev& sc = *c.sc;
+    const int ci = id / EW;
+    const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
+    const int na = ((d0w >> 23) & 3u) == (uint32_t)cx::KIND_AABB ? 4 : (int)(d1w & 255u);
+    const int nb = ((d0w >> 25) & 3u) == (uint32_t)cx::KIND_AABB ? 4 : (int)((d1w >> 8) & 255u);
+    cnt = (uint32_t)(na + nb + na * nb);
+  }
+  t.ws[c.W.cf_s + lane] = cnt;
+}
+// F2: round r of the batch: lane -> one term
+template <int EW>
+CX_DEV void ph_F2(const Ctx& c, Tile<EW> t, int lane, int b, int r) {
+  using namespace cx;
+  const int g = r * WAVE + lane;
+  int pre = 0, item = -1;
+#pragma unroll
+  for (int i = 0; i < CFB; ++i) {
+    const int si = (int)t.ws[c.W.cf_s + i];
+    if (item < 0 && g < pre + si) item = i;
+    if (item < 0) pre += si;
+  }
+  if (item < 0) return;
+  const int id = (int)t.ws[c.W.cf_list + b + item], e = id % EW;
+  Shape A, B;
+  int wa, wb;
+  cf_shapes<EW>(c, t, id, &A, &B, &wa, &wb);
+  // per-lane vertex picks straight from the LDS world tile
+  auto va = [&](int k) { return v2{t.f(wa + 2 * k, e), t.f(wa + 2 * k + 1, e)}; };
+  auto vb = [&](int k) { return v2{t.f(wb + 2 * k, e), t.f(wb + 2 * k + 1, e)}; };
+  const v2 x = cfe_term(A, B, g - pre, va, vb);
+  float* res = reinterpret_cast<float*>(t.ws + c.W.cf_res) + 2 * (item * CFS + (g - pre));
+  res[0] = x.x;
+  res[1] = x.y;
+}
+// F3: one lane per item sums its terms in order -> contact point, valid bit
+template <int EW>
+CX_DEV void ph_F3(const Ctx& c, Tile<EW> t, int lane, int b) {
+  using namespace cx;
+  if (lane >= CFB) return;
+  const int n = (int)t.ws[c.W.cf_n];
+  if (b + lane >= n) return;
+  const int id = (int)t.ws[c.W.cf_list + b + lane], e = id % EW, ci = id / EW;
+  const int S = (int)t.ws[c.W.cf_s + lane];
+  const float* res = reinterpret_cast<const float*>(t.ws + c.W.cf_res) + 2 * lane * CFS;
+  float cnt = 0.0f;
+  v2 acc = v2{0.0f, 0.0f};
+  for (int s0 = 0; s0 < S; s0 += 8) {  // fetch 8 terms, then add them in order
+    float xs[8], ys[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      xs[q] = res[2 * (s0 + q)];
+      ys[q] = res[2 * (s0 + q) + 1];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (s0 + q < S && !(isn(xs[q]) || isn(ys[q]))) {
+        acc = add(acc, v2{xs[q], ys[q]});
+        cnt = cnt + 1.0f;
+      }
+  }
+  const v2 cp = cnt > 0.0f ? divs(acc, cnt) : v2{qnan(), qnan()};
+  const int co = c.L.con + 4 * ci;
+  t.f(co + 2, e) = cp.x;
+  t.f(co + 3, e) = cp.y;
+  if (!(isn(cp.x) || isn(cp.y))) {
+#if defined(__HIP__) || defined(__HIPCC__)
+    atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
+#else
+    t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
+#endif
   }
 }
 
@@ -807,12 +971,23 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // emulation of the tests R loops over the 64 lanes.  The phase id is used
 // only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
-             PH_RESTORE, PH_G, PH_ADJ, PH_COUNT };
+             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_COUNT };
 // ---------------------------------------------------------------------------
 template <int EW, int FNSET, class R>
 CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
   if (!(a.dbg_skip & 1)) run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
   if (!(a.dbg_skip & 2)) run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
+  if ((FNSET & FNS_CONVEX) != 0 && c.sc->poly && !(a.dbg_skip & 2)) {
+    for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_F, [&](int l) { ph_F0<EW>(c, t, l, ch); });
+    const int n = (int)t.ws[c.W.cf_n];
+    for (int b = 0; b < n; b += CFB) {
+      run(PH_F, [&](int l) { ph_F1<EW>(c, t, l, b); });
+      int T = 0;
+      for (int i = 0; i < CFB; ++i) T += (int)t.ws[c.W.cf_s + i];
+      for (int r = 0; r * WAVE < T; ++r) run(PH_F, [&](int l) { ph_F2<EW>(c, t, l, b, r); });
+      run(PH_F, [&](int l) { ph_F3<EW>(c, t, l, b); });
+    }
+  }
   if (!(a.dbg_skip & 4) && c.nl > 0) {
     for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {
       run(PH_C0, [&](int l) { ph_C0<EW>(a, c, t, env0, l, ch); });
@@ -850,7 +1025,10 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
 // every discrete choice is the forward's) and then reversed by phase G
 template <int EW, int FNSET, class R>
 CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
-  run(PH_ADJ, [&](int l) { ph_adj_init<EW>(a, c, t, env0, l); });
+  run(PH_ADJ, [&](int l) {
+    ph_geo<EW>(a, c, t, env0, l);
+    ph_adj_init<EW>(a, c, t, env0, l);
+  });
   for (int step = a.n_steps - 1; step >= 0; --step) {
     run(PH_RESTORE, [&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });
     run(PH_A, [&](int l) { ph_A<EW>(a, c, t, env0, l, step); });

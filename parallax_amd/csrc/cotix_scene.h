@@ -224,6 +224,8 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   int nc_tot = s.ncand;
   n_cand = nc_tot;
   fnset = 0;
+  s.poly = 0;
+  for (int c = 0; c < s.nc; ++c) s.poly |= (cfn[c] == cx::FN_POLY_POLY || cfn[c] == cx::FN_AABB_POLY) ? 1 : 0;
   for (int c = 0; c < s.nc; ++c) {
     int fn = cfn[c];
     fnset |= (fn == cx::FN_AABB_AABB || fn == cx::FN_CIRCLE_AABB || fn == cx::FN_CIRCLE_CIRCLE) ? FNS_ANALYTIC

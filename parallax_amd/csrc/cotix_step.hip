@@ -74,11 +74,12 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   const int nhot = sc->nhot;
   for (int i = threadIdx.x; i < nhot; i += WPB * 64) lds[i] = sc->hot[i];
   __syncthreads();
-  const cxk::Ctx c{sc->nb, sc->np, sc->nc, sc->nl, sc->nt, sc, cxk::layout(sc->nb, sc->W, sc->nc, sc->nt)};
+  const cxk::Ctx c{sc->nb, sc->np, sc->nc, sc->nl, sc->nt, sc, cxk::layout(sc->nb, sc->W, sc->nc, sc->nt, sc->G),
+                   cxk::ws_layout(sc->nl, sc->nc, EW, sc->poly)};
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int env0 = (blockIdx.x * WPB + wave) * EW;
   if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
-  uint32_t* wbase = lds + nhot + wave * (c.L.S * EW + cxk::ws_words(c.nl, EW));
+  uint32_t* wbase = lds + nhot + wave * (c.L.S * EW + c.W.words);
   const cxk::Tile<EW> t{wbase, lds, wbase + c.L.S * EW};
 #ifdef COTIX_PHASE_PROF
   unsigned long long acc[cxk::PH_COUNT];

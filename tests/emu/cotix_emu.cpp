@@ -34,9 +34,10 @@ struct HostRun {
 template <int EW>
 void run_blocks(const cxk::KArgs& a, int mode) {
   const cxk::SceneDev& sc = *a.sc;
-  const cxk::Ctx c{sc.nb, sc.np, sc.nc, sc.nl, sc.nt, &sc, cxk::layout(sc.nb, sc.W, sc.nc, sc.nt)};
+  const cxk::Ctx c{sc.nb, sc.np, sc.nc, sc.nl, sc.nt, &sc, cxk::layout(sc.nb, sc.W, sc.nc, sc.nt, sc.G),
+                   cxk::ws_layout(sc.nl, sc.nc, EW, sc.poly)};
   const int nwaves = (a.B + EW - 1) / EW;
-  std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)c.L.S * EW + (size_t)cxk::ws_words(sc.nl, EW));
+  std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)c.L.S * EW + (size_t)cxk::ws_words(sc, EW));
   for (int q = 0; q < sc.nhot; ++q) lds[q] = sc.hot[q];
   for (int wv = 0; wv < nwaves; ++wv) {
     std::fill(lds.begin() + sc.nhot, lds.end(), 0x7FBADBADu);  // poison (a NaN pattern)

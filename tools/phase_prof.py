@@ -12,7 +12,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "parallax_amd", "_lib", "libcotix_amd_prof.so")
 NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
-         "adj"]
+         "adj", "F"]
 
 
 def build():
@@ -29,10 +29,11 @@ def main():
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--substeps", type=int, default=64)
+    ap.add_argument("--lib", default=LIB)
     a = ap.parse_args()
     if a.build:
         return build()
-    os.environ["COTIX_AMD_LIB"] = LIB
+    os.environ["COTIX_AMD_LIB"] = os.path.abspath(a.lib)
     sys.path.insert(0, ROOT)
     import torch
     import parallax_amd as pa

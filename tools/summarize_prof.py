@@ -12,7 +12,8 @@ import sys
 from collections import defaultdict
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/prof"
+scen = sys.argv[2] if len(sys.argv) > 2 else "robocup"
+src = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/prof_%s" % scen
 out = "profiles"
 K = "step_kernel"
 
@@ -36,6 +37,7 @@ raw = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
 corr = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
 summary = {
     "tag": tag,
+    "scenario": scen,
     "kernel": row["Name"],
     "calls": int(row["Calls"]),
     "avg_launch_ns": avg_ns,
@@ -50,14 +52,11 @@ summary = {
     "wait_frac_of_wave_cycles": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
 }
 os.makedirs(out, exist_ok=True)
-json.dump(summary, open(os.path.join(out, "%s_summary.json" % tag), "w"), indent=1)
-json.dump(summary, open(os.path.join(out, "latest_pmc.json"), "w"), indent=1)
-shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, "%s_kernel_stats.csv" % tag))
+json.dump(summary, open(os.path.join(out, "%s_%s_summary.json" % (tag, scen)), "w"), indent=1)
+json.dump(summary, open(os.path.join(out, "latest_pmc_%s.json" % scen), "w"), indent=1)
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, "%s_%s_kernel_stats.csv" % (tag, scen)))
 for d in ("pmc_fetch", "pmc_write", "pmc_sq"):
-    shutil.copy(os.path.join(src, d, "run_counter_collection.csv"), os.path.join(out, "%s_%s.csv" % (tag, d)))
-for f in os.listdir(src):
-    if f.startswith("sweep_"):
-        shutil.copy(os.path.join(src, f), os.path.join(out, "%s_%s" % (tag, f)))
+    shutil.copy(os.path.join(src, d, "run_counter_collection.csv"), os.path.join(out, "%s_%s_%s.csv" % (tag, scen, d)))
 print(json.dumps({k: summary[k] for k in ("avg_launch_ns", "bench_event_launch_ms", "hbm_bytes_per_launch_raw",
                                           "hbm_bytes_per_launch_corrected", "valu_active_frac_of_wave_cycles",
                                           "wait_frac_of_wave_cycles")}, indent=1))

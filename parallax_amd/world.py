@@ -117,6 +117,22 @@ class World:
             "cotix_step")
         return self
 
+    def step_state(self, dyn, keys, err, n_steps=1, dt=1e-2, stages=_ffi.STAGES_ROBOCUP, action=None,
+                   action_body=0):
+        """The fused step on caller-owned state tensors (same layouts as
+        self.dyn / self.keys / self.err) with this world's scene and geometry."""
+        for t, shape in ((dyn, tuple(self.dyn.shape)), (keys, (self.B, 2)), (err, (self.B,))):
+            if tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.device:
+                raise ValueError("state tensor shape/device/layout mismatch")
+        if action is not None:
+            action = action.to(self.device, torch.float32).contiguous()
+            if action.shape != (n_steps, self.B, 2):
+                raise ValueError("action must be [n_steps, B, 2]")
+        _ffi.check(_ffi.lib.cotix_step(
+            self.scene.handle, _ffi.ptr(dyn), _ffi.ptr(keys), _ffi.ptr(err), _ffi.ptr(self.geom), self.geom_stride,
+            self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(action), int(action_body),
+            _ffi.stream_ptr(self.device)), "cotix_step")
+
     def euler(self, dt):
         _ffi.check(_ffi.lib.cotix_physics_euler(_ffi.ptr(self.dyn), len(self.bodies), self.B, float(dt),
                                                 _ffi.stream_ptr(self.device)), "cotix_physics_euler")

@@ -476,3 +476,41 @@ def test_rollout_config5_full_size_vs_emulation(torch_cuda):
     got = acts.grad.cpu().numpy()[:, fin]
     want = (ga * g.cpu().numpy()[None, :, None])[:, fin]
     assert np.allclose(got, want, rtol=1e-6, atol=0)
+
+
+# ---------------------------------------------------------------------------
+# AbstractEnvironment.eval (cotix/_envs.py:37-132) over the fused kernel
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("scene", ["box", "robocup"])
+def test_eval_physics_world_vs_oracle(torch_cuda, scene):
+    torch = torch_cuda
+    import parallax_amd as pa
+    from parallax_amd import envs as E
+    import eval_cases as EC
+    import grad_cases as GC
+    from cotix_oracle import envs as OE
+    B = 8
+    case = GC.box_case(B, 1, seed=5) if scene == "box" else GC.robocup_case(B, 1)
+    ab = case["ab"]
+    if scene == "box":
+        case["S0"][1, ab, 0] = 1.5
+        bodies = _pa_bodies(pa, case["make"]())
+    else:
+        bodies = pa.scenarios.robocup_bodies()
+    w = pa.World(bodies, B, "cuda")
+    state = E.WorldState(torch.tensor(case["S0"], device="cuda").permute(1, 2, 0).contiguous(),
+                         torch.tensor(u32_to_i32(case["keys"]), device="cuda"),
+                         torch.zeros(B, dtype=torch.int32, device="cuda"))
+    env = E.AbstractEnvironment(E.PhysicsWorld(w), state, EC.PDControl(ab), EC.XJudge(ab))
+    out, reward = env.eval(0.6, 3, 10)
+    torch.cuda.synchronize()
+    for e in range(B):
+        ob = case["make"]()
+        for b, row in zip(ob, case["S0"][e]):
+            b.set_dyn(row)
+        (fb, fk), orew = OE.eval_env(case["step"], (ob, np.asarray(case["keys"][e], np.uint32)), EC.OraclePD(ab),
+                                     EC.OracleX(ab), 0.6, 3, 10, GC.D0, ab)
+        want = np.array([b.dyn() for b in fb], np.float32)
+        assert same_f32(out.state.dyn[:, :, e].cpu().numpy(), want), e
+        assert np.array_equal(out.state.keys[e].cpu().numpy().view(np.uint32), fk)
+        assert same_f32(reward[e:e + 1].cpu().numpy(), np.array([orew], np.float32)), (e, reward[e], orew)

@@ -22,6 +22,11 @@
  *   cotix_threefry2x32 / cotix_random_split / cotix_random_uniform
  *                         jax.random primitives called at cotix/_colliders.py:142-295
  *   cotix_order_clockwise order_clockwise              cotix/_geometry_utils.py:60-67
+ *   cotix_rollout / cotix_rollout_backward  BASELINE config 5
+ *   cotix_body_penetration UniversalShape.collides_with / penetrates_with
+ *                         cotix/_universal_shape.py:87-132
+ *   cotix_body_aabb       UniversalShape.possibly_collides_with (AABB.of of the
+ *                         body)  cotix/_universal_shape.py:109-110, _convex_shapes.py:68-77
  */
 #ifndef COTIX_AMD_H
 #define COTIX_AMD_H
@@ -68,7 +73,8 @@ enum {
 
 /* per-env error bits (eqx.error_if sites on the path) */
 enum {
-  COTIX_ERR_CIRCLE_AABB_CCP = 1 /* cotix/_contacts.py:105-107 */
+  COTIX_ERR_CIRCLE_AABB_CCP = 1, /* cotix/_contacts.py:105-107 */
+  COTIX_ERR_AABB_INVALID = 2     /* AABB.of, cotix/_convex_shapes.py:74-75 (body-level broadphase) */
 };
 
 /* Compile a scene (the collider's trace-time enumeration, cotix/_colliders.py:86-131).
@@ -138,6 +144,24 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
                            int geom_stride, int B, int n_steps, float dt, int stages, const float* action,
                            int action_body, const float* ret_weights, float* grad_action, float* grad_dyn0,
                            cotix_stream_t stream);
+
+/* Body-level operators (UniversalShape, cotix/_universal_shape.py:87-132), per env:
+ * cotix_body_penetration: collides_with (GJK over every part pair of the two
+ *   bodies, first colliding pair kept, :87-107) and penetrates_with /
+ *   penetration_depth (EPA, 48 iterations, :112-132).  Supports are the
+ *   reference's wrap_local_support (:32-45, which discards the inverse-rotated
+ *   direction).  collides device i32 [B], pen device f32 [B][2] (0 when not
+ *   colliding).
+ * cotix_body_aabb: AABB.of (cotix/_convex_shapes.py:68-77) of the whole body via
+ *   its global support (:47-59) -- a working version of the reference's
+ *   possibly_collides_with broadphase (:109-110), whose AABB.of_universal does
+ *   not exist.  aabb device f32 [B][4] = lo.x, lo.y, up.x, up.y; err (nullable)
+ *   |= COTIX_ERR_AABB_INVALID when x_max <= x_min or y_max <= y_min (the
+ *   eqx.error_if, EQX_ON_ERROR=nan: the bound becomes NaN). */
+int cotix_body_penetration(const cotix_scene* scene, const float* dyn, const float* geom, int geom_stride, int B,
+                           int body_a, int body_b, int* collides, float* pen, cotix_stream_t stream);
+int cotix_body_aabb(const cotix_scene* scene, const float* dyn, const float* geom, int geom_stride, int B, int body,
+                    float* aabb, uint32_t* err, cotix_stream_t stream);
 
 /* Operator-level entry points (batched over n independent items). */
 int cotix_physics_euler(float* dyn, int n_bodies, int B, float dt, cotix_stream_t stream);

@@ -16,6 +16,7 @@ STAGE_EULER, STAGE_GRAVITY, STAGE_COLLIDER, STAGE_LUNAR, STAGE_ADVANCE_KEY = 1, 
 STAGES_ROBOCUP = STAGE_EULER | STAGE_COLLIDER | STAGE_ADVANCE_KEY
 STAGES_LUNAR = STAGE_EULER | STAGE_GRAVITY | STAGE_COLLIDER | STAGE_LUNAR | STAGE_ADVANCE_KEY
 ERR_CIRCLE_AABB_CCP = 1
+ERR_AABB_INVALID = 2
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -30,6 +31,8 @@ SIGNATURES = {
     "cotix_step_autoreset": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
     "cotix_rollout": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P, _P]),
     "cotix_rollout_backward": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P]),
+    "cotix_body_penetration": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "cotix_body_aabb": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "cotix_physics_euler": (_I, [_P, _I, _I, _F, _P]),
     "cotix_collider_resolve": (_I, [_P, _P, _P, _P, _P, _I, _I, _P]),
     "cotix_lunar_constraints": (_I, [_P, _I, _P]),

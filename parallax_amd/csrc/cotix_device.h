@@ -291,7 +291,23 @@ CX_DEV v2 support(const Shape& s, v2 d) {
   }
   return v2{bx, by};
 }
-CX_DEV v2 minkowski(const Shape& a, const Shape& b, v2 d) { return sub(support(a, d), support(b, neg(d))); }
+// a part inside its body's frame, as UniversalShape.wrap_local_support sees it
+// (cotix/_universal_shape.py:32-45): the inverse_direction result is
+// discarded there (:38), so the local support is taken in the GLOBAL direction
+// and then mapped forward (rotation + translation).  Body-level GJK/EPA only.
+struct WrappedShape {
+  Shape s;
+  float c, sn, px, py;  // cos, sin of the body angle; body position
+};
+CX_DEV v2 support(const WrappedShape& w, v2 d) {
+  const v2 l = support(w.s, d);
+  const float t0 = (w.c * l.x + (-w.sn) * l.y) + w.px * 1.0f;
+  const float t1 = (w.sn * l.x + w.c * l.y) + w.py * 1.0f;
+  const float t2 = (0.0f * l.x + 0.0f * l.y) + 1.0f * 1.0f;
+  return v2{t0 / t2, t1 / t2};
+}
+template <class SA, class SB>
+CX_DEV v2 minkowski(const SA& a, const SB& b, v2 d) { return sub(support(a, d), support(b, neg(d))); }
 
 CX_DEV bool circle_contains(const Shape& c, v2 p) {  // :28-29
   float r = c.d(0) + 1e-6f;
@@ -455,7 +471,8 @@ CX_DEV bool point_in_triangle0(v2 v1, v2 v2_, v2 v3) {  // _geometry_utils.py:12
   return !(has_neg && has_pos);
 }
 
-CX_DEV bool gjk(const Shape& a, const Shape& b, v2 d0, v2* simplex) {
+template <class SA, class SB>
+CX_DEV bool gjk(const SA& a, const SB& b, v2 d0, v2* simplex) {
   v2 s0 = minkowski(a, b, d0);
   v2 s1 = minkowski(a, b, neg(s0));
   v2 dir = fnormal(sub(s1, s0));
@@ -574,8 +591,8 @@ struct EdgeCol {  // edge k, component c at p[(4k + c) * st]
   }
 };
 
-template <int NE, class ES>
-CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters, ES& es) {
+template <int NE, class ES, class SA, class SB>
+CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters, ES& es) {
   float dist[NE];
   const v2 z = v2{0.0f, 0.0f};
 #pragma unroll
@@ -639,15 +656,16 @@ CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters, ES& 
   }
   return closest_on_edge_to_origin(best0, best1);
 }
-template <int NE>
-CX_DEV v2 epa(const Shape& a, const Shape& b, const v2* simplex, int iters) {
+template <int NE, class SA, class SB>
+CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters) {
   EdgeRegs<NE> es;
-  return epa<NE>(a, b, simplex, iters, es);
+  return epa<NE, EdgeRegs<NE>>(a, b, simplex, iters, es);
 }
 
 // generic-iteration EPA (circle_vs_polygon uses 128 iterations): buffer in
 // private memory.  Not on either scenario's path.
-CX_DEV v2 epa_big(const Shape& a, const Shape& b, const v2* simplex, int iters) {
+template <class SA, class SB>
+CX_DEV v2 epa_big(const SA& a, const SB& b, const v2* simplex, int iters) {
   constexpr int NE = 131;
   v2 e0[NE], e1[NE];
   float dist[NE];
@@ -780,10 +798,10 @@ CX_DEV bool gjk_epa(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pe
   if (!need_pen) return true;
   if (iters + 3 <= 14) {
     auto es = make.template get<14>();
-    *pen = epa<14>(A, B, simplex, iters, es);
+    *pen = epa<14, decltype(es)>(A, B, simplex, iters, es);
   } else {
     auto es = make.template get<20>();
-    *pen = epa<20>(A, B, simplex, iters, es);
+    *pen = epa<20, decltype(es)>(A, B, simplex, iters, es);
   }
   return true;
 }

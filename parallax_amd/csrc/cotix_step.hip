@@ -10,6 +10,7 @@
 
 #include "../../include/cotix_amd.h"
 #include "cotix_device.h"
+#include "cotix_body.h"
 #include "cotix_kernel.h"
 #include "cotix_scene.h"
 
@@ -121,6 +122,24 @@ __global__ void contacts_kernel(int fn, int n, const float* a, const float* b, f
   out[4 * (size_t)i + 2] = c.cp.x;
   out[4 * (size_t)i + 3] = c.cp.y;
   if (err) err[i] = er;
+}
+using cxk::BodyParts;
+using cxk::MAXBP;
+__global__ void body_pen_kernel(const float* dyn, int B, const float* geom, int gstride, BodyParts pa, BodyParts pb,
+                                float d0x, float d0y, int* collides, float* pen) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= B) return;
+  cx::v2 p;
+  collides[g] = cxk::body_penetration_env(dyn, B, geom, gstride, pa, pb, cx::v2{d0x, d0y}, g, &p) ? 1 : 0;
+  pen[2 * (size_t)g] = p.x;
+  pen[2 * (size_t)g + 1] = p.y;
+}
+__global__ void body_aabb_kernel(const float* dyn, int B, const float* geom, int gstride, BodyParts pa, float* out,
+                                 uint32_t* err) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= B) return;
+  const uint32_t e = cxk::body_aabb_env(dyn, B, geom, gstride, pa, g, out + 4 * (size_t)g);
+  if (err && e) err[g] |= e;
 }
 __global__ void resolve_kernel(int n, float* d1, const float* p1, float* d2, const float* p2, const float* con) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -431,6 +450,45 @@ int cotix_lunar_constraints(float* dyn, int B, cotix_stream_t stream) {
   hipLaunchKernelGGL(lunar_kernel, dim3((B + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dyn, B,
                      p0, p1, p2);
   return hip_check(hipGetLastError(), "lunar_kernel launch");
+}
+
+static int body_parts(const cotix_scene* scene, int body, BodyParts* bp) {
+  const SceneDev& s = scene->host;
+  if (body < 0 || body >= s.nb) return fail("body index out of range");
+  bp->body = body;
+  bp->n = 0;
+  for (int p = 0; p < s.np; ++p) {
+    if ((int)s.hot[s.o_pbody + p] != body) continue;
+    if (bp->n >= MAXBP) return fail("more than 16 parts in a body");
+    bp->kind[bp->n] = (int)s.hot[s.o_pkind + p];
+    bp->nv[bp->n] = (int)s.hot[s.o_pn + p];
+    bp->goff[bp->n] = (int)s.hot[s.o_pgoff + p];
+    ++bp->n;
+  }
+  if (bp->n == 0) return fail("body has no parts");
+  return 0;
+}
+
+int cotix_body_penetration(const cotix_scene* scene, const float* dyn, const float* geom, int geom_stride, int B,
+                           int body_a, int body_b, int* collides, float* pen, cotix_stream_t stream) {
+  if (!scene || !dyn || !geom || !collides || !pen) return fail("null argument");
+  if (B <= 0) return B == 0 ? 0 : fail("negative size");
+  BodyParts pa, pb;
+  if (body_parts(scene, body_a, &pa) || body_parts(scene, body_b, &pb)) return -1;
+  hipLaunchKernelGGL(body_pen_kernel, dim3((B + 63) / 64), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), dyn,
+                     B, geom, geom_stride, pa, pb, scene->host.d0x, scene->host.d0y, collides, pen);
+  return hip_check(hipGetLastError(), "body_pen_kernel launch");
+}
+
+int cotix_body_aabb(const cotix_scene* scene, const float* dyn, const float* geom, int geom_stride, int B, int body,
+                    float* aabb, uint32_t* err, cotix_stream_t stream) {
+  if (!scene || !dyn || !geom || !aabb) return fail("null argument");
+  if (B <= 0) return B == 0 ? 0 : fail("negative size");
+  BodyParts pa;
+  if (body_parts(scene, body, &pa)) return -1;
+  hipLaunchKernelGGL(body_aabb_kernel, dim3((B + 63) / 64), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), dyn,
+                     B, geom, geom_stride, pa, aabb, err);
+  return hip_check(hipGetLastError(), "body_aabb_kernel launch");
 }
 
 int cotix_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err, cotix_stream_t stream) {

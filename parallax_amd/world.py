@@ -133,6 +133,35 @@ class World:
             self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(action), int(action_body),
             _ffi.stream_ptr(self.device)), "cotix_step")
 
+    # -- body-level operators (UniversalShape, cotix/_universal_shape.py:87-132) --
+    def penetrates_with(self, i, j):
+        """(collides bool [B], penetration f32 [B, 2]) of body i against body j:
+        collides_with over all part pairs, then penetration_depth (EPA, 48 it.)."""
+        col = torch.empty(self.B, dtype=torch.int32, device=self.device)
+        pen = torch.empty(self.B, 2, dtype=torch.float32, device=self.device)
+        _ffi.check(_ffi.lib.cotix_body_penetration(
+            self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.geom), self.geom_stride, self.B, int(i), int(j),
+            _ffi.ptr(col), _ffi.ptr(pen), _ffi.stream_ptr(self.device)), "cotix_body_penetration")
+        return col.bool(), pen
+
+    def collides_with(self, i, j):
+        return self.penetrates_with(i, j)[0]
+
+    def aabb(self, i, err=None):
+        """AABB.of of body i (lo.x, lo.y, up.x, up.y) [B, 4]; err bits OR-ed into `err`."""
+        out = torch.empty(self.B, 4, dtype=torch.float32, device=self.device)
+        _ffi.check(_ffi.lib.cotix_body_aabb(
+            self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.geom), self.geom_stride, self.B, int(i),
+            _ffi.ptr(out), _ffi.ptr(err), _ffi.stream_ptr(self.device)), "cotix_body_aabb")
+        return out
+
+    def possibly_collides_with(self, i, j):
+        """Broadphase: the two bodies' AABBs overlap (the negation of
+        aabb_vs_aabb's separation test, cotix/_contacts.py:62-65)."""
+        a, b = self.aabb(i), self.aabb(j)
+        sep = (a[:, 3] <= b[:, 1]) | (a[:, 2] <= b[:, 0]) | (a[:, 1] >= b[:, 3]) | (a[:, 0] >= b[:, 2])
+        return ~sep
+
     def euler(self, dt):
         _ffi.check(_ffi.lib.cotix_physics_euler(_ffi.ptr(self.dyn), len(self.bodies), self.B, float(dt),
                                                 _ffi.stream_ptr(self.device)), "cotix_physics_euler")

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "../../parallax_amd/csrc/cotix_body.h"
 #include "../../parallax_amd/csrc/cotix_kernel.h"
 #include "../../parallax_amd/csrc/cotix_scene.h"
 
@@ -175,5 +176,42 @@ extern "C" int emu_order_clockwise(float* xy, int n, int nv) {
     cx::order_clockwise(v, nv);
     for (int k = 0; k < 2 * nv; ++k) xy[(size_t)i * 2 * nv + k] = v[k];
   }
+  return 0;
+}
+
+// body-level operators on the host (same device code as the gfx950 kernels)
+static int emu_body_parts(const EmuScene* es, int body, cxk::BodyParts* bp) {
+  const cxk::SceneDev& s = es->s;
+  bp->body = body;
+  bp->n = 0;
+  for (int p = 0; p < s.np; ++p) {
+    if ((int)s.hot[s.o_pbody + p] != body) continue;
+    if (bp->n >= cxk::MAXBP) return -1;
+    bp->kind[bp->n] = (int)s.hot[s.o_pkind + p];
+    bp->nv[bp->n] = (int)s.hot[s.o_pn + p];
+    bp->goff[bp->n] = (int)s.hot[s.o_pgoff + p];
+    ++bp->n;
+  }
+  return bp->n > 0 ? 0 : -1;
+}
+extern "C" int emu_body_penetration(void* scene, const float* dyn, const float* geom, int gstride, int B, int ba,
+                                    int bb, int* collides, float* pen) {
+  const EmuScene* es = static_cast<EmuScene*>(scene);
+  cxk::BodyParts pa, pb;
+  if (emu_body_parts(es, ba, &pa) || emu_body_parts(es, bb, &pb)) return -1;
+  for (int g = 0; g < B; ++g) {
+    cx::v2 p;
+    collides[g] = cxk::body_penetration_env(dyn, B, geom, gstride, pa, pb, cx::v2{es->s.d0x, es->s.d0y}, g, &p);
+    pen[2 * g] = p.x;
+    pen[2 * g + 1] = p.y;
+  }
+  return 0;
+}
+extern "C" int emu_body_aabb(void* scene, const float* dyn, const float* geom, int gstride, int B, int body,
+                             float* out, uint32_t* err) {
+  const EmuScene* es = static_cast<EmuScene*>(scene);
+  cxk::BodyParts pa;
+  if (emu_body_parts(es, body, &pa)) return -1;
+  for (int g = 0; g < B; ++g) err[g] |= cxk::body_aabb_env(dyn, B, geom, gstride, pa, g, out + 4 * g);
   return 0;
 }

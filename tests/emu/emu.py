@@ -17,6 +17,8 @@ def load(asan=False):
                              ctypes.c_int, P_, ctypes.c_int, P_, P_, ctypes.c_int]
     lib.emu_contacts.argtypes = [ctypes.c_int, ctypes.c_int, P_, P_, P_, P_]
     lib.emu_order_clockwise.argtypes = [P_, ctypes.c_int, ctypes.c_int]
+    lib.emu_body_penetration.argtypes = [P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_]
+    lib.emu_body_aabb.argtypes = [P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_]
     lib.emu_rollout.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                 ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, ctypes.c_int]
     lib.emu_rollout_backward.argtypes = [P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,

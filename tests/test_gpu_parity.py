@@ -514,3 +514,44 @@ def test_eval_physics_world_vs_oracle(torch_cuda, scene):
         assert same_f32(out.state.dyn[:, :, e].cpu().numpy(), want), e
         assert np.array_equal(out.state.keys[e].cpu().numpy().view(np.uint32), fk)
         assert same_f32(reward[e:e + 1].cpu().numpy(), np.array([orew], np.float32)), (e, reward[e], orew)
+
+
+# ---------------------------------------------------------------------------
+# body-level operators (UniversalShape, cotix/_universal_shape.py:87-132)
+# ---------------------------------------------------------------------------
+def test_body_operators_vs_oracle(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    import body_cases as BC
+    import grad_cases as GC
+    from cotix_oracle import universal as U
+    B = 256
+    make = lambda: BC.bodies(3)  # noqa: E731
+    obodies = make()
+    bodies = []
+    for b in obodies:
+        parts = []
+        for p in b.parts:
+            if p.kind == "Circle":
+                parts.append(pa.Circle(p.radius, list(p.position)))
+            elif p.kind == "AABB":
+                parts.append(pa.AABB(list(p.lower), list(p.upper)))
+            else:
+                parts.append(pa.Polygon([list(v) for v in p.vertices_]))
+        bodies.append(pa.AnyBody(shape=pa.UniversalShape(*parts), mass=1.0, inertia=1.0))
+    w = pa.World(bodies, B, "cuda")
+    dyn = BC.states(B, seed=11)
+    w.dyn.copy_(torch.tensor(dyn, device="cuda"))
+    for (i, j) in [(0, 1), (1, 2), (2, 0)]:
+        col, pen = w.penetrates_with(i, j)
+        col, pen = col.cpu().numpy(), pen.cpu().numpy()
+        pc = w.possibly_collides_with(i, j).cpu().numpy()
+        for e in range(B):
+            bi, bj = BC.oracle_body(make, dyn, e, i), BC.oracle_body(make, dyn, e, j)
+            ok, p = U.penetrates_with(bi, bj, GC.D0)
+            assert bool(col[e]) == ok and same_f32(pen[e], np.array(p, np.float32)), (i, j, e)
+            (ai, _), (aj, _) = U.body_aabb(bi), U.body_aabb(bj)
+            sep = ai[3] <= aj[1] or ai[2] <= aj[0] or ai[1] >= aj[3] or ai[0] >= aj[2]
+            assert bool(pc[e]) == (not sep), (i, j, e)
+            if ok:  # the narrowphase implies the broadphase
+                assert pc[e]

@@ -122,7 +122,7 @@ class World:
         """The fused step on caller-owned state tensors (same layouts as
         self.dyn / self.keys / self.err) with this world's scene and geometry."""
         for t, shape in ((dyn, tuple(self.dyn.shape)), (keys, (self.B, 2)), (err, (self.B,))):
-            if tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.device:
+            if tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.dyn.device:
                 raise ValueError("state tensor shape/device/layout mismatch")
         if action is not None:
             action = action.to(self.device, torch.float32).contiguous()

@@ -553,5 +553,6 @@ def test_body_operators_vs_oracle(torch_cuda):
             (ai, _), (aj, _) = U.body_aabb(bi), U.body_aabb(bj)
             sep = ai[3] <= aj[1] or ai[2] <= aj[0] or ai[1] >= aj[3] or ai[0] >= aj[2]
             assert bool(pc[e]) == (not sep), (i, j, e)
-            if ok:  # the narrowphase implies the broadphase
-                assert pc[e]
+            # (no "narrowphase implies broadphase" check: through the reference's
+            # wrap_local_support a rotated body's support is not its true extreme
+            # point, so neither operator bounds the other for rotated bodies)

@@ -28,6 +28,11 @@ static inline float __uint_as_float(uint32_t u) {
   memcpy(&f, &u, 4);
   return f;
 }
+static inline uint32_t __float_as_uint(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
 #endif
 
 namespace cx {
@@ -40,8 +45,18 @@ CX_DEV float qnan() { return __builtin_nanf(""); }
 CX_DEV float finf() { return __builtin_inff(); }
 
 // lax.max / lax.min: NaN-propagating, ties keep the first operand.
-CX_DEV float fmax_(float a, float b) { return isn(a) ? a : (isn(b) ? b : (a >= b ? a : b)); }
-CX_DEV float fmin_(float a, float b) { return isn(a) ? a : (isn(b) ? b : (a <= b ? a : b)); }
+// (written as three flat selects: the nested-ternary form compiles to
+// divergent branches on gfx950)
+CX_DEV float fmax_(float a, float b) {
+  const float m = (a >= b) ? a : b;
+  const float n = isn(b) ? b : m;
+  return isn(a) ? a : n;
+}
+CX_DEV float fmin_(float a, float b) {
+  const float m = (a <= b) ? a : b;
+  const float n = isn(b) ? b : m;
+  return isn(a) ? a : n;
+}
 // jnp.clip (jax 0.4.x): minimum(hi, maximum(lo, x))
 CX_DEV float clip_(float x, float lo, float hi) { return fmin_(hi, fmax_(lo, x)); }
 
@@ -399,6 +414,27 @@ struct Contact {
 };
 CX_DEV Contact nan_contact() { return Contact{v2{0.0f, 0.0f}, v2{qnan(), qnan()}}; }
 
+// argmin over 4 values (first NaN, else first minimum) as flat selects
+CX_DEV int argmin4(const float* v) {
+  int k = 0;
+  float bv = v[0];
+#pragma unroll
+  for (int q = 1; q < 4; ++q) {
+    const bool lt = v[q] < bv;
+    bv = lt ? v[q] : bv;
+    k = lt ? q : k;
+  }
+  int nk = isn(v[3]) ? 3 : -1;
+  nk = isn(v[2]) ? 2 : nk;
+  nk = isn(v[1]) ? 1 : nk;
+  nk = isn(v[0]) ? 0 : nk;
+  return nk >= 0 ? nk : k;
+}
+CX_DEV float pick4(int k, float a0, float a1, float a2, float a3) {
+  const float lo = k == 0 ? a0 : a1, hi = k == 2 ? a2 : a3;
+  return k < 2 ? lo : hi;
+}
+
 CX_DEV Contact aabb_vs_aabb(const Shape& a, const Shape& b) {  // :61-96
   const float alx = a.d(0), aly = a.d(1), aux = a.d(2), auy = a.d(3);
   const float blx = b.d(0), bly = b.d(1), bux = b.d(2), buy = b.d(3);
@@ -407,10 +443,12 @@ CX_DEV Contact aabb_vs_aabb(const Shape& a, const Shape& b) {  // :61-96
   const float me = -1e-8f;
   float dep[4] = {fmax_(auy - bly, me), fmax_(buy - aly, me), fmax_(aux - blx, me), fmax_(bux - alx, me)};
   const float dx[4] = {0.0f, 0.0f, -1.0f, 1.0f}, dy[4] = {-1.0f, 1.0f, 0.0f, 0.0f};
-  int k = argmin_first(dep, 4);
-  float md = fmax_(0.0f, dep[k]);
+  (void)dx;
+  (void)dy;
+  const int k = argmin4(dep);
+  float md = fmax_(0.0f, pick4(k, dep[0], dep[1], dep[2], dep[3]));
   Contact c;
-  c.pen = v2{md * dx[k], md * dy[k]};
+  c.pen = v2{md * pick4(k, 0.0f, 0.0f, -1.0f, 1.0f), md * pick4(k, -1.0f, 1.0f, 0.0f, 0.0f)};
   v2 mu = v2{fmin_(aux, bux), fmin_(auy, buy)}, ml = v2{fmax_(alx, blx), fmax_(aly, bly)};
   c.cp = divs(add(mu, ml), 2.0f);
   return c;
@@ -444,8 +482,12 @@ CX_DEV Contact circle_vs_aabb(const Shape& a, const Shape& b, uint32_t* err) {
     ccp = v2{qnan(), qnan()};
   }
   v2 vs[4] = {lo, v2{lo.x, up.y}, up, v2{up.x, lo.y}};
+  // |vs[k] - ccp| < 1e-6 (:118): with correctly rounded sqrt, sqrt(s) < 1e-6f
+  // exactly when s < 0x2b8cbccb (the least s with sqrt(s) >= 1e-6f)
+  const float T = __uint_as_float(0x2b8cbccbu);
   bool perfect = false;
-  for (int k = 0; k < 4; ++k) perfect = perfect || (nrm(sub(vs[k], ccp)) < 1e-6f);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) perfect = perfect | (sumsq(sub(vs[k], ccp)) < T);
   if (!circle_contains(a, ccp)) return nan_contact();
   if (perfect) {
     v2 d = sub(ccp, ap);
@@ -454,9 +496,11 @@ CX_DEV Contact circle_vs_aabb(const Shape& a, const Shape& b, uint32_t* err) {
   }
   float sh[4] = {(ap.y + r) - lo.y, up.y - (ap.y - r), (ap.x + r) - lo.x, up.x - (ap.x - r)};
   const float dx[4] = {0.0f, 0.0f, 1.0f, -1.0f}, dy[4] = {1.0f, -1.0f, 0.0f, 0.0f};
-  int k = argmin_first(sh, 4);
-  float ns = -sh[k];
-  return Contact{v2{ns * dx[k], ns * dy[k]}, ccp};
+  (void)dx;
+  (void)dy;
+  const int k = argmin4(sh);
+  float ns = -pick4(k, sh[0], sh[1], sh[2], sh[3]);
+  return Contact{v2{ns * pick4(k, 0.0f, 0.0f, 1.0f, -1.0f), ns * pick4(k, 1.0f, -1.0f, 0.0f, 0.0f)}, ccp};
 }
 
 // ---------------------------------------------------------------------------
@@ -954,31 +998,82 @@ CX_DEV void apply_impulse(Dyn& b, const Params& m, v2 imp, v2 point) {  // :68-7
   b.vy = b.vy + imp.y / m.mass;
   b.w = b.w + torque / m.inertia;
 }
+// resolve_collision (:52-151) split in two.  Every operand that does not
+// depend on the two bodies' velocities -- the contact, the positions (the
+// resolution changes velocities only) and the parameters -- is folded into
+// ResPre, so the collider's sequential pass over the bodies carries only the
+// velocity-dependent part.  The expressions and their evaluation order are
+// the reference's; pre + seq is bit-identical to the one-piece form.
+// Exact reciprocals of a body's mass and inertia (scene tables): r with
+// x / d == x * r bit for bit for every x -- d = +-inf (r = +-0), +-0 (r =
+// +-inf) or a normal power of two with a normal reciprocal -- or NaN when
+// the division must be performed.
+struct Rcp {
+  float m, i;
+};
+CX_DEV Rcp no_rcp() { return Rcp{qnan(), qnan()}; }
+// x / d; RCP: the scene guarantees d's exact reciprocal r (x * r, bit-identical)
+template <bool RCP>
+CX_DEV float div_r(float x, float d, float r) {
+  if (RCP) return x * r;
+  return x / d;
+}
+struct ResPre {
+  v2 n, r1, r2, pen;  // pen / |pen|; cp - p1; cp - p2 (== velocity_at / apply_impulse arms); pen
+  float den, pterm, ne, mu;  // (1/m1 + 1/m2) + ang; (0.3 |pen|) / 0.01; -(1 + e); (mu1 + mu2) / 2
+};
+template <bool RCP = false>
+CX_DEV ResPre resolve_pre(const Dyn& b1, const Params& m1, Rcp q1, const Dyn& b2, const Params& m2, Rcp q2, v2 pen,
+                          v2 cp) {
+  ResPre p;
+  const float pn = nrm(pen);
+  p.n = v2{pen.x / pn, pen.y / pn};
+  const float e = fmin_(m1.elast, m2.elast);
+  p.r1 = sub(cp, v2{b1.px, b1.py});
+  p.r2 = sub(cp, v2{b2.px, b2.py});
+  const float lev1 = p.r1.x * p.r1.x + p.r1.y * p.r1.y, lev2 = p.r2.x * p.r2.x + p.r2.y * p.r2.y;
+  const float ang = div_r<RCP>(lev1, m1.inertia, q1.i) + div_r<RCP>(lev2, m2.inertia, q2.i);
+  p.den = (div_r<RCP>(1.0f, m1.mass, q1.m) + div_r<RCP>(1.0f, m2.mass, q2.m)) + ang;
+  p.pterm = (0.3f * nrm(pen)) / 0.01f;
+  p.ne = -(1.0f + e);
+  p.mu = (m1.fric + m2.fric) / 2.0f;
+  p.pen = pen;
+  return p;
+}
+// the velocity-dependent part on (vx, vy, w) of both bodies; false when the
+// bodies move apart (:140-146) and nothing is applied
+template <bool RCP = false>
+CX_DEV bool resolve_seq(float& vx1, float& vy1, float& w1, const Params& m1, Rcp q1, float& vx2, float& vy2,
+                        float& w2, const Params& m2, Rcp q2, const ResPre& p) {
+  const v2 v1 = v2{vx1 + (-p.r1.y) * w1, vy1 + p.r1.x * w1};  // velocity_at(b1, cp)
+  const v2 v2_ = v2{vx2 + (-p.r2.y) * w2, vy2 + p.r2.x * w2};
+  const v2 relv = sub(v2_, v1);
+  const float vn = dot(relv, p.n);
+  const float nim = p.ne * vn - p.pterm;
+  const float ni = nim / p.den;
+  v2 imp = scl(p.n, ni);
+  const v2 vd = v2{relv.x + vn * p.n.x, relv.y + vn * p.n.y};
+  const float vdn = nrm(vd);
+  const v2 vdu = v2{vd.x / vdn, vd.y / vdn};
+  float idr = (-vdn) / p.den;
+  idr = clip_(idr, 0.0f, ni * p.mu);
+  imp = add(imp, scl(vdu, idr));
+  if (dot(p.pen, relv) < 0.0f) return false;  // moving apart (:140-146)
+  // apply_impulse(b1, -imp, cp), apply_impulse(b2, imp, cp)  (:68-73)
+  const v2 i1 = neg(imp);
+  const float t1 = crs(p.r1, i1), t2 = crs(p.r2, imp);
+  vx1 = vx1 + div_r<RCP>(i1.x, m1.mass, q1.m);
+  vy1 = vy1 + div_r<RCP>(i1.y, m1.mass, q1.m);
+  w1 = w1 + div_r<RCP>(t1, m1.inertia, q1.i);
+  vx2 = vx2 + div_r<RCP>(imp.x, m2.mass, q2.m);
+  vy2 = vy2 + div_r<RCP>(imp.y, m2.mass, q2.m);
+  w2 = w2 + div_r<RCP>(t2, m2.inertia, q2.i);
+  return true;
+}
 CX_DEV bool resolve_collision(Dyn& b1, const Params& m1, Dyn& b2, const Params& m2, v2 pen, v2 cp) {  // :52-151
   if (vnan(cp)) return false;
-  v2 v1 = velocity_at(b1, cp), v2_ = velocity_at(b2, cp);
-  v2 relv = sub(v2_, v1);
-  float pn = nrm(pen);
-  v2 n = v2{pen.x / pn, pen.y / pn};
-  float vn = dot(relv, n);
-  float e = fmin_(m1.elast, m2.elast);
-  v2 r1 = sub(cp, v2{b1.px, b1.py}), r2 = sub(cp, v2{b2.px, b2.py});
-  float lev1 = r1.x * r1.x + r1.y * r1.y, lev2 = r2.x * r2.x + r2.y * r2.y;
-  float ang = lev1 / m1.inertia + lev2 / m2.inertia;
-  float nim = (-(1.0f + e)) * vn - (0.3f * nrm(pen)) / 0.01f;
-  float ni = nim / ((1.0f / m1.mass + 1.0f / m2.mass) + ang);
-  v2 imp = scl(n, ni);
-  float mu = (m1.fric + m2.fric) / 2.0f;
-  v2 vd = v2{relv.x + vn * n.x, relv.y + vn * n.y};
-  float vdn = nrm(vd);
-  v2 vdu = v2{vd.x / vdn, vd.y / vdn};
-  float idr = (-vdn) / ((1.0f / m1.mass + 1.0f / m2.mass) + ang);
-  idr = clip_(idr, 0.0f, ni * mu);
-  imp = add(imp, scl(vdu, idr));
-  if (dot(pen, relv) < 0.0f) return false;  // moving apart (:140-146)
-  apply_impulse(b1, m1, neg(imp), cp);
-  apply_impulse(b2, m2, imp, cp);
-  return true;
+  const ResPre p = resolve_pre(b1, m1, no_rcp(), b2, m2, no_rcp(), pen, cp);
+  return resolve_seq(b1.vx, b1.vy, b1.w, m1, no_rcp(), b2.vx, b2.vy, b2.w, m2, no_rcp(), p);
 }
 CX_DEV v2 rotate(v2 v, float ang) {  // _geometry_utils.py:81-88
   float s, c;

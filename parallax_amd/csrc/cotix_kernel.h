@@ -35,17 +35,30 @@ constexpr int MAXB = 16, MAXP = 32, MAXC = 256, MAXL = 128, MAXT = 13, MAXCAND =
 constexpr int MAXHOT = 8192;
 constexpr int WAVE = 64;
 
+// workload counters of the host emulation (tools/collider_stats.py); no-ops
+// in every other build
+#ifdef COTIX_STATS
+struct Stats {
+  unsigned long long wave_steps, active_items, rounds, resolutions, f_items, b_items;
+};
+inline Stats g_stats{};
+#define CXK_STAT(f, v) (cxk::g_stats.f += (unsigned long long)(v))
+#else
+#define CXK_STAT(f, v) ((void)0)
+#endif
+
 // Scene tables.  Everything the step reads per item is packed into hot[]
 // (word offsets below) and copied to LDS once per launch.
 struct SceneDev {
   int nb, np, nc, nl, nt, G, W, ncand;  // bodies, parts, contacts, cells, types, geom/world floats, candidates
   float d0x, d0y;                       // GJK start direction (constant)
-  int o_par, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
+  int o_par, o_rcp, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
   int o_ci, o_cj, o_cbeg, o_ccnt, o_tn1, o_tn2, o_cand;
   int o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts
   int o_cmask;  // per cell nmw words: bitmask of the cell's distinct contacts
   int nmw;      // contact-mask words = ceil(nc / 32)
   int poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
+  int rcp_all;  // 1: every mass and inertia has an exact reciprocal (o_rcp): resolutions multiply
   int nhot;
   uint32_t hot[MAXHOT];
 };
@@ -76,9 +89,17 @@ struct KArgs {
 
 // per-wave tile layout (words, each x EW envs)
 struct Lay {
-  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, geo, S;
+  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, geo, rp, kw, kww, rflag, S;
 };
+// key window: the per-step keys of KWIN consecutive steps, precomputed
+// together (phase K) -- the collider keys depend on the key chain only, never
+// on the physics.  Slot s (KW words): sk0[2], skt[2*nt], then choice uniform[nb].
+constexpr int KWIN = 16;
 constexpr int REC_W = 7;  // per resolution: applied flag, v/w of body i, v/w of body j (pre-resolution)
+// per resolution (phase E0 -> E1): partner body (or RP_NONE), cx::ResPre, partner mass/inertia
+enum : int { RP_J, RP_NX, RP_NY, RP_R1X, RP_R1Y, RP_R2X, RP_R2Y, RP_PX, RP_PY, RP_DEN, RP_PT, RP_NE, RP_MU, RP_MJ, RP_IJ,
+             RP_QMJ, RP_QIJ, RP_W };
+constexpr uint32_t RP_NONE = 0xFFFFFFFFu;
 CX_HD Lay layout(int nb, int W, int nc, int nt, int G) {
   Lay L;
   L.dyn = 0;
@@ -97,7 +118,11 @@ CX_HD Lay layout(int nb, int W, int nc, int nt, int G) {
   L.vm = L.rec + nb * REC_W;        // bit c: contact c has a contact point this step
   L.rst = L.vm + (nc + 31) / 32;    // restart state (autoreset), staged once per launch
   L.geo = L.rst + nb * 6;           // local part geometry (per env), staged once per launch
-  L.S = L.geo + G;
+  L.rp = L.geo + G;                 // resolution operands (E0 -> E1)
+  L.kww = 2 + 2 * nt + nb;          // key window slot words
+  L.kw = L.rp + nb * RP_W;
+  L.rflag = L.kw + KWIN * L.kww;    // this step restarts the env (autoreset)
+  L.S = L.rflag + 1;
   return L;
 }
 static inline int tile_words(const SceneDev& s) { return layout(s.nb, s.W, s.nc, s.nt, s.G).S; }
@@ -297,8 +322,58 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
 }
 
 // phase A: Euler (cotix/_physics_solvers.py:16-33) + driver extras + key chain
+// phase K: the key window (steps step0 .. step0+n-1), three passes.
+// K0 (one lane per env): the driver key chain k_{s+1} = split(k_s)[0] and the
+// collider's skey_0 = split(k_s)[0] (cotix/_colliders.py:142,
+// examples/test_viz.py:39,66).
 template <int EW>
-CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+CX_DEV void ph_K0(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int n) {
+  using namespace cx;
+  const Lay& L = c.L;
+  for (int e = lane; e < EW; e += WAVE) {
+    key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
+    for (int s = 0; s < n; ++s) {
+      const key2 s0 = split_at(k, 2u, 0u);
+      t.w(L.kw + s * L.kww, e) = s0.a;
+      t.w(L.kw + s * L.kww + 1, e) = s0.b;
+      if (a.stages & COTIX_STAGE_ADVANCE_KEY) k = s0;
+    }
+  }
+}
+// K1 (item = (step, env)): the per-type keys skey = split(skey)[0] (:175)
+template <int EW>
+CX_DEV void ph_K1(const Ctx& c, Tile<EW> t, int lane, int n) {
+  using namespace cx;
+  const Lay& L = c.L;
+  for (int w = lane; w < n * EW; w += WAVE) {
+    const int e = w % EW, o = L.kw + (w / EW) * L.kww;
+    key2 k = key2{t.w(o, e), t.w(o + 1, e)};
+    for (int q = 0; q < c.nt; ++q) {
+      k = split_at(k, 2u, 0u);
+      t.w(o + 2 + 2 * q, e) = k.a;
+      t.w(o + 3 + 2 * q, e) = k.b;
+    }
+  }
+}
+// K2 (item = (step, body, env)): the uniform of body i's contact choice,
+// jr.choice(split(skey, n)[i], p) (:284-295) -> unit float of random_bits
+template <int EW>
+CX_DEV void ph_K2(const Ctx& c, Tile<EW> t, int lane, int n) {
+  using namespace cx;
+  const Lay& L = c.L;
+  const int nb = c.nb;
+  for (int w = lane; w < n * nb * EW; w += WAVE) {
+    const int e = w % EW, i = (w / EW) % nb, o = L.kw + (w / EW / nb) * L.kww;
+    const int so = c.nt > 0 ? o + 2 + 2 * (c.nt - 1) : o;
+    const key2 ck = split_at(key2{t.w(so, e), t.w(so + 1, e)}, (uint32_t)nb, (uint32_t)i);
+    t.f(o + 2 + 2 * c.nt + i, e) = unit_float(bits1(ck));
+  }
+}
+
+// PRE: the step's keys come from the key window (slot `slot`); otherwise
+// (backward re-play from saved keys) they are split here.
+template <int EW, bool PRE = false>
+CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step, int slot = 0) {
   using namespace cx;
   const int nb = c.nb;
   const Lay& L = c.L;
@@ -324,8 +399,15 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     }
   }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
+    if (PRE) {  // sk0, skt of this step from the window
+      const int nw = 2 + 2 * c.nt, o = L.kw + slot * L.kww;
+      for (int w = lane; w < nw * EW; w += WAVE) {
+        const int e = w % EW, q = w / EW;
+        t.w(L.sk0 + q, e) = t.w(o + q, e);  // sk0 and skt are adjacent in both
+      }
+    }
     for (int e = lane; e < EW; e += WAVE) {
-      if (!(a.dbg_skip & 16)) {
+      if (!PRE && !(a.dbg_skip & 16)) {
         key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
         key2 s = split_at(k, 2u, 0u);  // cotix/_colliders.py:142 == next driver key
         t.w(L.sk0, e) = s.a;
@@ -336,9 +418,15 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
           t.w(L.skt + 2 * q + 1, e) = s.b;
         }
       }
-      for (int q = 0; q < nb * nb; ++q) t.w(L.m + q, e) = 0xFFFFFFFFu;
-      for (int q = 0; q < c.sc->nmw; ++q) t.w(L.vm + q, e) = 0u;
-      for (int q = 0; q < nb; ++q) t.w(L.ch + q, e) = (uint32_t)q;
+    }
+    // per-step collider scratch: all_contacts cells empty (:137-140), no valid
+    // contact, choice = self -- spread over the lanes
+    const int nm = nb * nb, nv = c.sc->nmw;
+    for (int w = lane; w < (nm + nv + nb) * EW; w += WAVE) {
+      const int e = w % EW, q = w / EW;
+      if (q < nm) t.w(L.m + q, e) = 0xFFFFFFFFu;
+      else if (q < nm + nv) t.w(L.vm + q - nm, e) = 0u;
+      else t.w(L.ch + q - nm - nv, e) = (uint32_t)(q - nm - nv);
     }
   }
 }
@@ -409,6 +497,7 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     if ((FNSET & FNS_CONVEX) != 0 && sc.poly) t.ws[c.W.cf_flag + w] = 0u;
     if (g >= a.B) continue;
     const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
+    CXK_STAT(b_items, 1);
     const int fn = (int)((d0w >> 20) & 7u);
     const int wa = c.L.world + (int)(d0w & 1023u), wb = c.L.world + (int)((d0w >> 10) & 1023u);
     Shape A, Bs;
@@ -674,42 +763,62 @@ CX_DEV void ph_C3(const Ctx& c, Tile<EW> t, int lane, int par) {
 }
 
 // phase D: choose_random_contact (cotix/_colliders.py:274-295)
-template <int EW>
-CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+// one (body i, env) item of phase D; NB > 0: the body count at compile time
+// (unrolled loads and selects), NB == 0: any count up to MAXB
+template <int EW, bool PRE, int NB>
+CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
   using namespace cx;
-  const int nb = c.nb, nt = c.nt;
+  constexpr int MB = NB > 0 ? NB : MAXB;
+  const int nb = NB > 0 ? NB : c.nb, nt = c.nt;
   const Lay& L = c.L;
-  for (int w = lane; w < nb * EW; w += WAVE) {
-    int e = w % EW, i = w / EW, g = env0 + e;
-    if (g >= a.B) continue;
-    int cnt = 0;
-    uint32_t good = 0u;
-    for (int j = 0; j < nb; ++j)
-      if ((int)t.w(L.m + i * nb + j, e) >= 0) {
-        good |= 1u << j;
-        ++cnt;
-      }
-    int ch = i;
-    if (cnt > 0) {
-      float p[MAXB], cs[MAXB];
-      const float fc = (float)cnt;
+  int cnt = 0;
+  uint32_t good = 0u;
 #pragma unroll
-      for (int j = 0; j < MAXB; ++j) p[j] = (((good >> j) & 1u) ? 1.0f : 0.0f) / fc;
+  for (int j = 0; j < MB; ++j)
+    if (j < nb && (int)t.w(L.m + i * nb + j, e) >= 0) {
+      good |= 1u << j;
+      ++cnt;
+    }
+  int ch = i;
+  if (cnt > 0) {
+    float p[MB], cs[MB];
+    // p = notnan / count (:280-283): 1/count or 0/count == +0 (count > 0)
+    const float inv = 1.0f / (float)cnt;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) p[j] = ((good >> j) & 1u) ? inv : 0.0f;
+    if (NB > 0)
+      cumsum_fixed<MB>(p, cs);
+    else
       cumsum_n(p, nb, cs);
+    float u;
+    if (PRE) {
+      u = t.f(L.kw + slot * L.kww + 2 + 2 * nt + i, e);
+    } else {
       const int so = nt > 0 ? L.skt + 2 * (nt - 1) : L.sk0;
       key2 ck = split_at(key2{t.w(so, e), t.w(so + 1, e)}, (uint32_t)nb, (uint32_t)i);
-      float u = unit_float(bits1(ck));
-      float last = cs[0];
-#pragma unroll
-      for (int j = 1; j < MAXB; ++j)
-        if (j < nb) last = cs[j];
-      float r = last * (1.0f - u);
-      ch = nb;
-#pragma unroll
-      for (int j = MAXB - 1; j >= 0; --j)
-        if (j < nb && !(cs[j] < r)) ch = j;  // first j with r <= cumsum[j]
+      u = unit_float(bits1(ck));
     }
-    t.w(L.ch + i, e) = (uint32_t)ch;
+    float last = cs[0];
+#pragma unroll
+    for (int j = 1; j < MB; ++j)
+      if (j < nb) last = cs[j];
+    float r = last * (1.0f - u);
+    ch = nb;
+#pragma unroll
+    for (int j = MB - 1; j >= 0; --j)
+      if (j < nb && !(cs[j] < r)) ch = j;  // first j with r <= cumsum[j]
+  }
+  t.w(L.ch + i, e) = (uint32_t)ch;
+}
+template <int EW, bool PRE = false>
+CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int slot = 0) {
+  const int nb = c.nb;
+  for (int w = lane; w < nb * EW; w += WAVE) {
+    const int e = w % EW, i = w / EW;
+    if (env0 + e >= a.B) continue;
+    if (nb == 5) d_item<EW, PRE, 5>(c, t, e, i, slot);
+    else if (nb == 4) d_item<EW, PRE, 4>(c, t, e, i, slot);
+    else d_item<EW, PRE, 0>(c, t, e, i, slot);
   }
 }
 
@@ -717,8 +826,178 @@ CX_DEV cx::Params load_par(const uint32_t* tb, int o) {
   return cx::Params{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1]), __uint_as_float(tb[o + 2]),
                     __uint_as_float(tb[o + 3])};
 }
+CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
+  return cx::Rcp{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1])};
+}
 
 // phase E: sequential resolution (:310-336), joints, key update, restarts.
+// E0 (item = (body i, env), all lanes): everything of resolution i that does
+// not depend on velocities -- partner j = choice[i], the contact, the
+// positions (a resolution changes velocities only) and the parameters --
+// folded into cx::ResPre.  E1 (one lane per env): the sequential pass over
+// the bodies carrying only the velocity-dependent part, velocities held in
+// registers for the common body counts.
+template <int EW, bool RCP>
+CX_DEV void ph_E0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  using namespace cx;
+  if (!(a.stages & COTIX_STAGE_COLLIDER)) return;
+  const SceneDev& sc = *c.sc;
+  const int nb = c.nb;
+  const Lay& L = c.L;
+  for (int w = lane; w < nb * EW; w += WAVE) {
+    const int e = w % EW, i = w / EW, g = env0 + e;
+    if (g >= a.B) continue;
+    const int ro = L.rp + RP_W * i;
+    uint32_t jj = RP_NONE;
+    const int j = (int)t.w(L.ch + i, e);
+    if (!(j == i || j < 0 || j >= nb)) {
+      const int cid = (int)t.w(L.m + i * nb + j, e);
+      if (cid >= 0) {
+        const int co = L.con + 4 * cid;
+        const v2 cp = v2{t.f(co + 2, e), t.f(co + 3, e)};
+        if (!vnan(cp)) {  // resolve_collision returns unchanged bodies on a NaN contact point
+          const int oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
+          const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
+          const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
+          const Params pj = load_par(t.tb, sc.o_par + 4 * j);
+          const Rcp qj = load_rcp(t.tb, sc.o_rcp + 2 * j);
+          const ResPre p = resolve_pre<RCP>(bi, load_par(t.tb, sc.o_par + 4 * i), load_rcp(t.tb, sc.o_rcp + 2 * i), bj, pj,
+                                       qj, v2{t.f(co, e), t.f(co + 1, e)}, cp);
+          t.f(ro + RP_NX, e) = p.n.x;
+          t.f(ro + RP_NY, e) = p.n.y;
+          t.f(ro + RP_R1X, e) = p.r1.x;
+          t.f(ro + RP_R1Y, e) = p.r1.y;
+          t.f(ro + RP_R2X, e) = p.r2.x;
+          t.f(ro + RP_R2Y, e) = p.r2.y;
+          t.f(ro + RP_PX, e) = p.pen.x;
+          t.f(ro + RP_PY, e) = p.pen.y;
+          t.f(ro + RP_DEN, e) = p.den;
+          t.f(ro + RP_PT, e) = p.pterm;
+          t.f(ro + RP_NE, e) = p.ne;
+          t.f(ro + RP_MU, e) = p.mu;
+          t.f(ro + RP_MJ, e) = pj.mass;
+          t.f(ro + RP_IJ, e) = pj.inertia;
+          t.f(ro + RP_QMJ, e) = qj.m;
+          t.f(ro + RP_QIJ, e) = qj.i;
+          jj = (uint32_t)j;
+          CXK_STAT(resolutions, 1);
+        }
+      }
+    }
+    t.w(ro + RP_J, e) = jj;
+  }
+}
+
+template <int EW>
+CX_DEV cx::ResPre load_rp(Tile<EW> t, int ro, int e) {
+  cx::ResPre p;
+  p.n = cx::v2{t.f(ro + RP_NX, e), t.f(ro + RP_NY, e)};
+  p.r1 = cx::v2{t.f(ro + RP_R1X, e), t.f(ro + RP_R1Y, e)};
+  p.r2 = cx::v2{t.f(ro + RP_R2X, e), t.f(ro + RP_R2Y, e)};
+  p.pen = cx::v2{t.f(ro + RP_PX, e), t.f(ro + RP_PY, e)};
+  p.den = t.f(ro + RP_DEN, e);
+  p.pterm = t.f(ro + RP_PT, e);
+  p.ne = t.f(ro + RP_NE, e);
+  p.mu = t.f(ro + RP_MU, e);
+  return p;
+}
+
+// E1 sequential pass, NB (== nb) bodies' velocities in registers; body j is
+// picked and written back by unrolled selects (no scratch)
+template <int EW, bool REC, int NB, bool RCP>
+CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
+  using namespace cx;
+  const SceneDev& sc = *c.sc;
+  const Lay& L = c.L;
+  float vx[NB], vy[NB], vw[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    vx[b] = t.f(L.dyn + 6 * b + 2, e);
+    vy[b] = t.f(L.dyn + 6 * b + 3, e);
+    vw[b] = t.f(L.dyn + 6 * b + 5, e);
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int ro = L.rp + RP_W * i;
+    const uint32_t j = t.w(ro + RP_J, e);
+    if (REC) t.w(L.rec + REC_W * i, e) = 0u;
+    if (j == RP_NONE) continue;
+    float jx = 0.0f, jy = 0.0f, jw = 0.0f;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if ((uint32_t)b == j) {
+        jx = vx[b];
+        jy = vy[b];
+        jw = vw[b];
+      }
+    if (REC) {
+      const int rc = L.rec + REC_W * i;
+      t.f(rc + 1, e) = vx[i];
+      t.f(rc + 2, e) = vy[i];
+      t.f(rc + 3, e) = vw[i];
+      t.f(rc + 4, e) = jx;
+      t.f(rc + 5, e) = jy;
+      t.f(rc + 6, e) = jw;
+    }
+    const Params pi = load_par(t.tb, sc.o_par + 4 * i);
+    const Params pj = Params{t.f(ro + RP_MJ, e), t.f(ro + RP_IJ, e), 0.0f, 0.0f};
+    const Rcp qj = Rcp{t.f(ro + RP_QMJ, e), t.f(ro + RP_QIJ, e)};
+    const bool applied = resolve_seq<RCP>(vx[i], vy[i], vw[i], pi, load_rcp(t.tb, sc.o_rcp + 2 * i), jx, jy, jw, pj, qj,
+                                     load_rp<EW>(t, ro, e));
+    if (REC) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if ((uint32_t)b == j) {
+        vx[b] = jx;
+        vy[b] = jy;
+        vw[b] = jw;
+      }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    t.f(L.dyn + 6 * b + 2, e) = vx[b];
+    t.f(L.dyn + 6 * b + 3, e) = vy[b];
+    t.f(L.dyn + 6 * b + 5, e) = vw[b];
+  }
+}
+// E1 for any body count: the same pass on the LDS tile
+template <int EW, bool REC, bool RCP>
+CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e) {
+  using namespace cx;
+  const SceneDev& sc = *c.sc;
+  const Lay& L = c.L;
+  for (int i = 0; i < c.nb; ++i) {
+    const int ro = L.rp + RP_W * i;
+    const uint32_t j = t.w(ro + RP_J, e);
+    if (REC) t.w(L.rec + REC_W * i, e) = 0u;
+    if (j == RP_NONE) continue;
+    const int oi = L.dyn + 6 * i, oj = L.dyn + 6 * (int)j;
+    float ix = t.f(oi + 2, e), iy = t.f(oi + 3, e), iw = t.f(oi + 5, e);
+    float jx = t.f(oj + 2, e), jy = t.f(oj + 3, e), jw = t.f(oj + 5, e);
+    if (REC) {
+      const int rc = L.rec + REC_W * i;
+      t.f(rc + 1, e) = ix;
+      t.f(rc + 2, e) = iy;
+      t.f(rc + 3, e) = iw;
+      t.f(rc + 4, e) = jx;
+      t.f(rc + 5, e) = jy;
+      t.f(rc + 6, e) = jw;
+    }
+    const Params pi = load_par(t.tb, sc.o_par + 4 * i);
+    const Params pj = Params{t.f(ro + RP_MJ, e), t.f(ro + RP_IJ, e), 0.0f, 0.0f};
+    const Rcp qj = Rcp{t.f(ro + RP_QMJ, e), t.f(ro + RP_QIJ, e)};
+    const bool applied = resolve_seq<RCP>(ix, iy, iw, pi, load_rcp(t.tb, sc.o_rcp + 2 * i), jx, jy, jw, pj, qj,
+                                     load_rp<EW>(t, ro, e));
+    if (REC) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
+    t.f(oi + 2, e) = ix;
+    t.f(oi + 3, e) = iy;
+    t.f(oi + 5, e) = iw;
+    t.f(oj + 2, e) = jx;
+    t.f(oj + 3, e) = jy;
+    t.f(oj + 5, e) = jw;
+  }
+}
+
 // REC (backward re-play only): record, per resolution, whether the impulses
 // were applied and the pre-resolution velocities of the two bodies.
 template <int EW, bool REC = false>
@@ -731,34 +1010,18 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     int g = env0 + e;
     if (g >= a.B) continue;
     if (a.stages & COTIX_STAGE_COLLIDER) {
-      for (int i = 0; i < nb; ++i) {
-        if (REC) t.w(L.rec + REC_W * i, e) = 0u;
-        const int j = (int)t.w(L.ch + i, e);
-        if (j == i || j < 0 || j >= nb) continue;
-        const int cid = (int)t.w(L.m + i * nb + j, e);
-        if (cid < 0) continue;
-        const int co = L.con + 4 * cid, oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
-        Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), t.f(oi + 2, e), t.f(oi + 3, e), t.f(oi + 4, e), t.f(oi + 5, e)};
-        Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), t.f(oj + 2, e), t.f(oj + 3, e), t.f(oj + 4, e), t.f(oj + 5, e)};
-        if (REC) {
-          const int ro = L.rec + REC_W * i;
-          t.f(ro + 1, e) = bi.vx;
-          t.f(ro + 2, e) = bi.vy;
-          t.f(ro + 3, e) = bi.w;
-          t.f(ro + 4, e) = bj.vx;
-          t.f(ro + 5, e) = bj.vy;
-          t.f(ro + 6, e) = bj.w;
+      if (sc.rcp_all) {
+        switch (nb) {
+          case 4: e1_regs<EW, REC, 4, true>(c, t, e); break;
+          case 5: e1_regs<EW, REC, 5, true>(c, t, e); break;
+          default: e1_tile<EW, REC, true>(c, t, e); break;
         }
-        const bool applied =
-            resolve_collision(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
-                              v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)});
-        if (REC) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
-        t.f(oi + 2, e) = bi.vx;
-        t.f(oi + 3, e) = bi.vy;
-        t.f(oi + 5, e) = bi.w;
-        t.f(oj + 2, e) = bj.vx;
-        t.f(oj + 3, e) = bj.vy;
-        t.f(oj + 5, e) = bj.w;
+      } else {
+        switch (nb) {
+          case 4: e1_regs<EW, REC, 4, false>(c, t, e); break;
+          case 5: e1_regs<EW, REC, 5, false>(c, t, e); break;
+          default: e1_tile<EW, REC, false>(c, t, e); break;
+        }
       }
     }
     if ((a.stages & COTIX_STAGE_LUNAR) && nb >= 3) {
@@ -782,13 +1045,26 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       t.w(L.key, e) = t.w(L.sk0, e);
       t.w(L.key + 1, e) = t.w(L.sk0 + 1, e);
     }
-    if (a.dyn_reset != nullptr && t.w(L.err, e) != 0u) {
-      // episode end on an error_if trip (the reference raises here): restart
-      // the env from its reset state; the key chain continues.
-      for (int off = 0; off < nb * 6; ++off) t.f(L.dyn + off, e) = t.f(L.rst + off, e);
+    if (a.dyn_reset != nullptr) {
+      // episode end on an error_if trip (the reference raises here): the env
+      // restarts from its reset state (phase R, spread over the lanes); the
+      // key chain continues.
+      const uint32_t r = t.w(L.err, e) != 0u ? 1u : 0u;
+      t.w(L.rflag, e) = r;
       t.w(L.err, e) = 0u;
-      t.w(L.nres, e) = t.w(L.nres, e) + 1u;
+      t.w(L.nres, e) = t.w(L.nres, e) + r;
     }
+  }
+}
+
+// phase R (autoreset launches): restore the restarting envs' state,
+// item = (state word, env)
+template <int EW>
+CX_DEV void ph_R(const Ctx& c, Tile<EW> t, int lane) {
+  const Lay& L = c.L;
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    const int e = w % EW, off = w / EW;
+    if (t.w(L.rflag, e) != 0u) t.f(L.dyn + off, e) = t.f(L.rst + off, e);
   }
 }
 
@@ -971,15 +1247,16 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // emulation of the tests R loops over the 64 lanes.  The phase id is used
 // only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
-             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_COUNT };
+             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_COUNT };
 // ---------------------------------------------------------------------------
-template <int EW, int FNSET, class R>
-CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
+template <int EW, int FNSET, bool PRE, class R>
+CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot) {
   if (!(a.dbg_skip & 1)) run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
   if (!(a.dbg_skip & 2)) run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
   if ((FNSET & FNS_CONVEX) != 0 && c.sc->poly && !(a.dbg_skip & 2)) {
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_F, [&](int l) { ph_F0<EW>(c, t, l, ch); });
     const int n = (int)t.ws[c.W.cf_n];
+    CXK_STAT(f_items, n);
     for (int b = 0; b < n; b += CFB) {
       run(PH_F, [&](int l) { ph_F1<EW>(c, t, l, b); });
       int T = 0;
@@ -993,13 +1270,16 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_C0, [&](int l) { ph_C0<EW>(a, c, t, env0, l, ch); });
       run(PH_C0B, [&](int l) { ph_C0b<EW>(c, t, l, ch); });
     }
+    CXK_STAT(wave_steps, 1);
+    CXK_STAT(active_items, t.ws[WS_N]);
     for (int par = 0; t.ws[WS_N] != 0u; par ^= 1) {  // uniform: read after the phase barrier
+      CXK_STAT(rounds, 1);
       run(PH_C1, [&](int l) { ph_C1<EW>(a, c, t, l, par); });
       run(PH_C2, [&](int l) { ph_C2<EW>(c, t, l, par); });
       run(PH_C3, [&](int l) { ph_C3<EW>(c, t, l, par); });
     }
   }
-  if (!(a.dbg_skip & 8)) run(PH_D, [&](int l) { ph_D<EW>(a, c, t, env0, l); });
+  if (!(a.dbg_skip & 8)) run(PH_D, [&](int l) { ph_D<EW, PRE>(a, c, t, env0, l, slot); });
 }
 
 // forward: n_steps fused steps; ROLL adds the trajectory save and the return
@@ -1011,11 +1291,23 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     if (ROLL)
       for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
   });
+  const bool keys = (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !(a.dbg_skip & 16);
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
-    run(PH_A, [&](int l) { ph_A<EW>(a, c, t, env0, l, step); });
-    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET>(a, c, t, env0, run);
-    if (!(a.dbg_skip & 32)) run(PH_E, [&](int l) { ph_E<EW>(a, c, t, env0, l); });
+    const int slot = step % KWIN;
+    if (keys && slot == 0) {
+      const int n = a.n_steps - step < KWIN ? a.n_steps - step : KWIN;
+      run(PH_K, [&](int l) { ph_K0<EW>(a, c, t, l, n); });
+      run(PH_K, [&](int l) { ph_K1<EW>(c, t, l, n); });
+      if (a.stages & COTIX_STAGE_COLLIDER) run(PH_K, [&](int l) { ph_K2<EW>(c, t, l, n); });
+    }
+    run(PH_A, [&](int l) { ph_A<EW, true>(a, c, t, env0, l, step, slot); });
+    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot);
+    if (!(a.dbg_skip & 32)) {
+      run(PH_E, [&](int l) { c.sc->rcp_all ? ph_E0<EW, true>(a, c, t, env0, l) : ph_E0<EW, false>(a, c, t, env0, l); });
+      run(PH_E, [&](int l) { ph_E<EW>(a, c, t, env0, l); });
+      if (a.dyn_reset != nullptr) run(PH_E, [&](int l) { ph_R<EW>(c, t, l); });
+    }
     if (ROLL) run(PH_RET, [&](int l) { ph_ret<EW>(a, c, t, env0, l); });
   }
   run(PH_STORE, [&](int l) { ph_store<EW, ROLL>(a, c, t, env0, l); });
@@ -1031,8 +1323,9 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
   });
   for (int step = a.n_steps - 1; step >= 0; --step) {
     run(PH_RESTORE, [&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });
-    run(PH_A, [&](int l) { ph_A<EW>(a, c, t, env0, l, step); });
-    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET>(a, c, t, env0, run);
+    run(PH_A, [&](int l) { ph_A<EW, false>(a, c, t, env0, l, step); });
+    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0);
+    run(PH_E, [&](int l) { c.sc->rcp_all ? ph_E0<EW, true>(a, c, t, env0, l) : ph_E0<EW, false>(a, c, t, env0, l); });
     run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l); });
     run(PH_G, [&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
   }

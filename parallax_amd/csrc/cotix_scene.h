@@ -2,6 +2,7 @@
 // (cotix/_colliders.py:86-131) done once per scene.  Host C++ only; shared by
 // the library (cotix_step.hip) and the CPU emulation harness (tests/emu).
 #pragma once
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <string>
@@ -12,6 +13,19 @@
 #include "cotix_kernel.h"
 
 namespace cxk {
+
+// the exact reciprocal of a mass / inertia (cx::Rcp): r with x / d == x * r
+// for every x, or NaN when no such r exists
+inline float exact_rcp(float d) {
+  if (std::isinf(d)) return std::signbit(d) ? -0.0f : 0.0f;
+  if (d == 0.0f) return std::signbit(d) ? -INFINITY : INFINITY;
+  if (std::isnan(d) || !std::isnormal(d)) return NAN;
+  int ex;
+  const float m = std::frexp(d, &ex);
+  if (std::fabs(m) != 0.5f) return NAN;  // not a power of two
+  const float r = 1.0f / d;
+  return std::isnormal(r) ? r : NAN;
+}
 
 inline int scene_fail(std::string& err, const std::string& m) {
   err = m;
@@ -162,6 +176,18 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
       std::memcpy(&u, &body_params[q], 4);
       hot.push_back(u);
     }
+  }
+  {
+    s.o_rcp = (int)hot.size();  // exact reciprocals of mass and inertia (cx::Rcp)
+    s.rcp_all = 1;
+    for (int b = 0; b < n_bodies; ++b)
+      for (int q = 0; q < 2; ++q) {
+        const float r = exact_rcp(body_params[4 * b + q]);
+        if (std::isnan(r)) s.rcp_all = 0;
+        uint32_t u;
+        std::memcpy(&u, &r, 4);
+        hot.push_back(u);
+      }
   }
   put(s.o_pbody, part_bodyv);
   put(s.o_pkind, part_kindv);

@@ -306,11 +306,15 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int fs = scene->fnset;
 #define COTIX_LAUNCH(EE, FS, BW) hipLaunchKernelGGL((step_kernel<EE, FS, BW>), grid, block, lds, st, ka)
+#ifdef COTIX_EW4_ONLY  // tooling builds (phase profile): the default tiling only, compiles faster
+#define COTIX_LAUNCH_E(FS, BW) COTIX_LAUNCH(4, FS, BW);
+#else
 #define COTIX_LAUNCH_E(FS, BW)                \
   if (EW == 1) COTIX_LAUNCH(1, FS, BW);       \
   else if (EW == 8) COTIX_LAUNCH(8, FS, BW);  \
   else if (EW == 2) COTIX_LAUNCH(2, FS, BW);  \
   else COTIX_LAUNCH(4, FS, BW);
+#endif
   if (mode == 2) {
     COTIX_LAUNCH_E(FNS_ANALYTIC, 2)  // the host admits analytic scenes only
   } else if (mode == 1) {

@@ -215,3 +215,17 @@ extern "C" int emu_body_aabb(void* scene, const float* dyn, const float* geom, i
   for (int g = 0; g < B; ++g) err[g] |= cxk::body_aabb_env(dyn, B, geom, gstride, pa, g, out + 4 * g);
   return 0;
 }
+
+#ifdef COTIX_STATS
+// workload counters (tools/collider_stats.py): read and reset
+extern "C" int emu_stats(unsigned long long* out) {
+  out[0] = cxk::g_stats.wave_steps;
+  out[1] = cxk::g_stats.active_items;
+  out[2] = cxk::g_stats.rounds;
+  out[3] = cxk::g_stats.resolutions;
+  out[4] = cxk::g_stats.f_items;
+  out[5] = cxk::g_stats.b_items;
+  cxk::g_stats = cxk::Stats{};
+  return 6;
+}
+#endif

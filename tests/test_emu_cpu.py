@@ -100,3 +100,91 @@ def test_emu_order_clockwise_ties_nan_zero(emu_lib):
         want = np.array(G.order_clockwise([tuple(v) for v in xy]), np.float32).reshape(-1)
         same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
         assert same.all(), (xy, got.reshape(-1, 2), want.reshape(-1, 2))
+
+
+@pytest.mark.parametrize("EW", [1, 4])
+@pytest.mark.parametrize("scenario", ["robocup", "lunar"])
+def test_emu_fused_equals_single_steps(emu_lib, EW, scenario):
+    """One launch of 37 fused steps (three key windows, the last one partial)
+    == 37 one-step launches, bit for bit, with episode restarts on (RoboCup)."""
+    emu, lib = emu_lib
+    from cotix_oracle import physics as P
+    name = "robocup_trace.npz" if scenario == "robocup" else "lunar_trace.npz"
+    tr = np.load(os.path.join(GOLD, name))
+    if scenario == "robocup":
+        h, geom = emu.oracle_scene(lib, P.robocup_bodies())
+        gstride, stages = 0, 1 | 4 | 16
+    else:
+        rows = [emu.oracle_scene(lib, P.lunar_lander_bodies(k))[1] for k in tr["terrain_keys"]]
+        h, _ = emu.oracle_scene(lib, P.lunar_lander_bodies(tr["terrain_keys"][0]))
+        geom = np.ascontiguousarray(np.stack(rows).astype(np.float32))
+        gstride, stages = geom.shape[1], 1 | 2 | 4 | 8 | 16
+    dyn0 = np.ascontiguousarray(tr["dyn"][0].transpose(1, 2, 0))
+    keys0 = np.ascontiguousarray(tr["keys"][0]).astype(np.uint32)
+    reset = dyn0.copy() if scenario == "robocup" else None
+    B, T = dyn0.shape[2], 37
+    fused = [dyn0.copy(), keys0.copy(), np.zeros(B, np.uint32)]
+    emu.step(lib, h, *fused, geom, gstride, T, stages, E=EW, dyn_reset=reset)
+    single = [dyn0.copy(), keys0.copy(), np.zeros(B, np.uint32)]
+    for _ in range(T):
+        emu.step(lib, h, *single, geom, gstride, 1, stages, E=EW, dyn_reset=reset)
+    assert same_f32(fused[0], single[0])
+    assert np.array_equal(fused[1], single[1]) and np.array_equal(fused[2], single[2])
+
+
+def test_emu_robocup_autoreset_vs_cport(emu_lib):
+    """Episode restarts (the bench workload) on CPU: the kernel logic vs the
+    C port of the oracle, 64 perturbed envs x 2 launches of 20 fused steps."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    from cotix_oracle import physics as P
+    if not os.path.exists(cport.LIB):
+        pytest.skip("oracle C port not built (make -C oracle)")
+    clib = cport.load()
+    dyn, keys = cport.robocup_batch(64)
+    dyn, keys = np.ascontiguousarray(dyn, np.float32), np.ascontiguousarray(keys, np.uint32)
+    reset = dyn.copy()
+    h, geom = emu.oracle_scene(lib, P.robocup_bodies())
+    sc = cport.Scene(clib, P.robocup_bodies())
+    got = [dyn.copy(), keys.copy(), np.zeros(64, np.uint32), np.zeros(64, np.uint32)]
+    want = [dyn.copy(), keys.copy(), np.zeros(64, np.uint32), np.zeros(64, np.uint32)]
+    for _ in range(2):
+        emu.step(lib, h, got[0], got[1], got[2], geom, 0, 20, 1 | 4 | 16, E=4, dyn_reset=reset, resets=got[3])
+        sc.step(want[0], want[1], want[2], 20, cport.STAGES_ROBOCUP, None, reset, want[3])
+    assert want[3].sum() > 0
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)
+
+
+def test_perfect_vertex_threshold():
+    """circle_vs_aabb's `norm(v - ccp) < 1e-6` (cotix/_contacts.py:118) is
+    evaluated in the kernels as `sumsq < 0x2b8cbccb` (no sqrt): with a
+    correctly rounded sqrt the two agree for every float32 sum of squares."""
+    T = np.uint32(0x2B8CBCCB).view(np.float32)
+    c = np.float32(1e-6)
+    bits = np.arange(0x2B8CBCCB - (1 << 20), 0x2B8CBCCB + (1 << 20), dtype=np.uint32)
+    rng = np.random.default_rng(0)
+    bits = np.concatenate([bits, rng.integers(0, 0x7F800001, 1 << 20, dtype=np.uint32),
+                           np.array([0, 0x7F800000, 0x7FC00000], np.uint32)])
+    s = bits.view(np.float32)
+    assert np.array_equal(np.sqrt(s) < c, s < T)
+
+
+@pytest.mark.parametrize("name", ["aabb_aabb", "circle_circle", "circle_aabb", "poly_poly", "aabb_poly",
+                                  "circle_poly"])
+def test_emu_contact_operators_vs_golden(emu_lib, name):
+    """The kernels' contact functions (cotix_device.h, host build) on the
+    ~6,000 golden operator cases, bit for bit, error bits included."""
+    emu, lib = emu_lib
+    g = np.load(os.path.join(GOLD, "contacts.npz"))
+    a = np.ascontiguousarray(g[name + "_a"], np.float32)
+    b = np.ascontiguousarray(g[name + "_b"], np.float32)
+    n = a.shape[0]
+    out = np.zeros((n, 4), np.float32)
+    err = np.zeros(n, np.uint32)
+    lib.emu_contacts(int(g[name + "_fn"]), n, a.ctypes.data_as(emu.P_), b.ctypes.data_as(emu.P_),
+                     out.ctypes.data_as(emu.P_), err.ctypes.data_as(emu.P_))
+    assert same_f32(out, g[name + "_out"])
+    assert np.array_equal(err, g[name + "_err"])

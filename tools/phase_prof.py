@@ -12,13 +12,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "parallax_amd", "_lib", "libcotix_amd_prof.so")
 NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
-         "adj", "F"]
+         "adj", "F", "K"]
 
 
 def build():
     src = os.path.join(ROOT, "parallax_amd", "csrc", "cotix_step.hip")
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", "-std=c++17",
-           "-fPIC", "-shared", "-DCOTIX_PHASE_PROF", src, "-o", LIB]
+           "-fPIC", "-shared", "-DCOTIX_PHASE_PROF", "-DCOTIX_EW4_ONLY", src, "-o", LIB]
     subprocess.run(cmd, check=True)
 
 
@@ -57,12 +57,13 @@ def main():
         env.step(a.substeps)
     torch.cuda.synchronize()
     n = f(buf, 32)
-    waves = (B + 3) // 4
+    ew = int(os.environ.get("COTIX_ENVS_PER_WAVE", "4"))
+    waves = (B + ew - 1) // ew
     steps = a.launches * a.substeps
     tot = sum(buf[q] for q in range(n))
     out = {NAMES[q]: {"cycles_per_wave_step": buf[q] / waves / steps, "share": buf[q] / tot} for q in range(n)
            if buf[q]}
-    print(json.dumps({"scenario": a.scenario, "envs": B, "cycles_per_wave_step_total": tot / waves / steps,
+    print(json.dumps({"scenario": a.scenario, "envs": B, "envs_per_wave": ew, "cycles_per_wave_step_total": tot / waves / steps,
                       "phases": out}, indent=1))
 
 

@@ -49,7 +49,9 @@ inline Stats g_stats{};
 
 // Scene tables.  Everything the step reads per item is packed into hot[]
 // (word offsets below) and copied to LDS once per launch.
-struct SceneDev {
+// the scalar header (offsets, counts) travels in the kernel arguments, so
+// phases read it from registers, never from global memory
+struct SceneHdr {
   int nb, np, nc, nl, nt, G, W, ncand;  // bodies, parts, contacts, cells, types, geom/world floats, candidates
   float d0x, d0y;                       // GJK start direction (constant)
   int o_par, o_rcp, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
@@ -59,13 +61,17 @@ struct SceneDev {
   int nmw;      // contact-mask words = ceil(nc / 32)
   int poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
   int rcp_all;  // 1: every mass and inertia has an exact reciprocal (o_rcp): resolutions multiply
+  int fnset;    // FNS_* bits of the contact functions the scene uses (kernel instantiation)
   int nhot;
+};
+struct SceneDev : SceneHdr {
   uint32_t hot[MAXHOT];
 };
 
 // kernel arguments (passed by value)
 struct KArgs {
   const SceneDev* sc;
+  SceneHdr sh;         // *sc's header (by value: kernel-argument registers)
   float* dyn;          // [nb][6][B]
   uint32_t* keys;      // [B][2]
   uint32_t* err;       // [B]
@@ -125,7 +131,7 @@ CX_HD Lay layout(int nb, int W, int nc, int nt, int G) {
   L.S = L.rflag + 1;
   return L;
 }
-static inline int tile_words(const SceneDev& s) { return layout(s.nb, s.W, s.nc, s.nt, s.G).S; }
+static inline int tile_words(const SceneHdr& s) { return layout(s.nb, s.W, s.nc, s.nt, s.G).S; }
 // per-wave scratch of phase C (words, not per env): pass flags, keep flags,
 // active count, two item lists (double buffer), per-item scan positions
 enum : int { WS_FLAG = 0, WS_KEEP = 64, WS_N = 128, WS_LIST = 129 };
@@ -149,9 +155,9 @@ CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly) {
   w.words = poly ? w.epa + 4 * EPA_NE * 64 : w.cf_flag;
   return w;
 }
-CX_HD int ws_words(const SceneDev& s, int ew) { return ws_layout(s.nl, s.nc, ew, s.poly).words; }
+CX_HD int ws_words(const SceneHdr& s, int ew) { return ws_layout(s.nl, s.nc, ew, s.poly).words; }
 // LDS bytes of a workgroup of wpb waves x ew envs
-static inline size_t lds_bytes(const SceneDev& s, int wpb, int ew) {
+static inline size_t lds_bytes(const SceneHdr& s, int wpb, int ew) {
   return 4 * ((size_t)s.nhot + ((size_t)tile_words(s) * ew + (size_t)ws_words(s, ew)) * wpb);
 }
 
@@ -282,17 +288,21 @@ struct Tile {
 
 struct Ctx {
   int nb, np, nc, nl, nt;
-  const SceneDev* sc;
+  SceneHdr sh;
   Lay L;
   WsLay W;
 };
+template <int EW>
+CX_HD Ctx make_ctx(const SceneHdr& h) {
+  return Ctx{h.nb, h.np, h.nc, h.nl, h.nt, h, layout(h.nb, h.W, h.nc, h.nt, h.G), ws_layout(h.nl, h.nc, EW, h.poly)};
+}
 
 // local part geometry of the wave's envs: read from HBM once per launch, not
 // once per step (per-env LunarLander terrain)
 template <int EW>
 CX_DEV void ph_geo(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   if (a.geom == nullptr) return;
-  for (int w = lane; w < c.sc->G * EW; w += WAVE) {
+  for (int w = lane; w < c.sh.G * EW; w += WAVE) {
     int e = w % EW, k = w / EW, g = env0 + e;
     t.f(c.L.geo + k, e) = (g < a.B) ? a.geom[(a.gstride ? (size_t)g * a.gstride : (size_t)0) + k] : 0.0f;
   }
@@ -300,7 +310,7 @@ CX_DEV void ph_geo(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
 
 template <int EW>
 CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
-  if (c.sc->poly)  // phase F's flag array incl. its padding to a multiple of 64
+  if (c.sh.poly)  // phase F's flag array incl. its padding to a multiple of 64
     for (int w = lane; w < c.W.cf_list - c.W.cf_flag; w += WAVE) t.ws[c.W.cf_flag + w] = 0u;
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
@@ -419,15 +429,13 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         }
       }
     }
-    // per-step collider scratch: all_contacts cells empty (:137-140), no valid
-    // contact, choice = self -- spread over the lanes
-    const int nm = nb * nb, nv = c.sc->nmw;
-    for (int w = lane; w < (nm + nv + nb) * EW; w += WAVE) {
-      const int e = w % EW, q = w / EW;
-      if (q < nm) t.w(L.m + q, e) = 0xFFFFFFFFu;
-      else if (q < nm + nv) t.w(L.vm + q - nm, e) = 0u;
-      else t.w(L.ch + q - nm - nv, e) = (uint32_t)(q - nm - nv);
-    }
+    // per-step collider scratch: all_contacts cells empty (:137-140), choice =
+    // self (m and ch are adjacent in the tile: one flat, branch-free pass), no
+    // valid contact
+    const int nm = nb * nb;
+    for (int w = lane; w < (nm + nb) * EW; w += WAVE)
+      t.u[L.m * EW + w] = w < nm * EW ? 0xFFFFFFFFu : (uint32_t)(w / EW - nm);
+    for (int w = lane; w < c.sh.nmw * EW; w += WAVE) t.u[L.vm * EW + w] = 0u;
   }
 }
 
@@ -435,7 +443,7 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
 template <int EW, int FNSET>
 CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   for (int w = lane; w < c.np * EW; w += WAVE) {
     int e = w % EW, p = w / EW, g = env0 + e;
     if (g >= a.B) continue;
@@ -490,7 +498,7 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
 template <int EW, int FNSET>
 CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const v2 d0 = v2{sc.d0x, sc.d0y};
   for (int w = lane; w < c.nc * EW; w += WAVE) {
     int e = w % EW, ci = w / EW, g = env0 + e;
@@ -562,7 +570,7 @@ CX_DEV void ph_F0(const Ctx& c, Tile<EW> t, int lane, int chunk) {
 }
 template <int EW>
 CX_DEV void cf_shapes(const Ctx& c, Tile<EW> t, int id, cx::Shape* A, cx::Shape* B, int* wa, int* wb) {
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const int e = id % EW, ci = id / EW;
   const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
   A->kind = (int)((d0w >> 23) & 3u);
@@ -585,7 +593,7 @@ CX_DEV void ph_F1(const Ctx& c, Tile<EW> t, int lane, int b) {
   uint32_t cnt = 0u;
   if (b + lane < n) {
     const int id = (int)t.ws[c.W.cf_list + b + lane];
-    const SceneDev& sc = *c.sc;
+    const SceneHdr& sc = c.sh;
     const int ci = id / EW;
     const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
     const int na = ((d0w >> 23) & 3u) == (uint32_t)cx::KIND_AABB ? 4 : (int)(d1w & 255u);
@@ -670,7 +678,7 @@ CX_DEV void ph_F3(const Ctx& c, Tile<EW> t, int lane, int b) {
 template <int EW>
 CX_DEV void ph_C0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int chunk) {
   using namespace cx;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const int id = chunk * WAVE + lane;
   uint32_t flag = 0u;
   if (id < c.nl * EW) {
@@ -699,7 +707,7 @@ CX_DEV void ph_C0b(const Ctx& c, Tile<EW> t, int lane, int chunk) {
 template <int EW>
 CX_DEV void ph_C1(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int par) {
   using namespace cx;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const int NI = c.nl * EW;
   const uint32_t* list = t.ws + WS_LIST + par * NI;
   const int n = (int)t.ws[WS_N], np = n < WAVE ? n : WAVE, G = WAVE / np;
@@ -727,7 +735,7 @@ CX_DEV void ph_C1(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int par) {
 // R2: per item, the first passing draw writes the cell; else advance
 template <int EW>
 CX_DEV void ph_C2(const Ctx& c, Tile<EW> t, int lane, int par) {
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const uint64_t mask = wave_ballot(t.ws + WS_FLAG, lane);
   const int NI = c.nl * EW;
   const uint32_t* list = t.ws + WS_LIST + par * NI;
@@ -841,7 +849,7 @@ template <int EW, bool RCP>
 CX_DEV void ph_E0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
   if (!(a.stages & COTIX_STAGE_COLLIDER)) return;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const int nb = c.nb;
   const Lay& L = c.L;
   for (int w = lane; w < nb * EW; w += WAVE) {
@@ -907,7 +915,7 @@ CX_DEV cx::ResPre load_rp(Tile<EW> t, int ro, int e) {
 template <int EW, bool REC, int NB, bool RCP>
 CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
   using namespace cx;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
   float vx[NB], vy[NB], vw[NB];
 #pragma unroll
@@ -964,7 +972,7 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
 template <int EW, bool REC, bool RCP>
 CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e) {
   using namespace cx;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
   for (int i = 0; i < c.nb; ++i) {
     const int ro = L.rp + RP_W * i;
@@ -1003,7 +1011,7 @@ CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e) {
 template <int EW, bool REC = false>
 CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const int nb = c.nb;
   const Lay& L = c.L;
   for (int e = lane; e < EW; e += WAVE) {
@@ -1149,7 +1157,7 @@ CX_DEV void ph_adj_init(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
 template <int EW>
 CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   using namespace cx;
-  const SceneDev& sc = *c.sc;
+  const SceneHdr& sc = c.sh;
   const int nb = c.nb;
   const Lay& L = c.L;
   for (int e = lane; e < EW; e += WAVE) {
@@ -1247,13 +1255,13 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // emulation of the tests R loops over the 64 lanes.  The phase id is used
 // only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
-             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_COUNT };
+             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_COUNT };
 // ---------------------------------------------------------------------------
 template <int EW, int FNSET, bool PRE, class R>
 CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot) {
   if (!(a.dbg_skip & 1)) run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
   if (!(a.dbg_skip & 2)) run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
-  if ((FNSET & FNS_CONVEX) != 0 && c.sc->poly && !(a.dbg_skip & 2)) {
+  if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && !(a.dbg_skip & 2)) {
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_F, [&](int l) { ph_F0<EW>(c, t, l, ch); });
     const int n = (int)t.ws[c.W.cf_n];
     CXK_STAT(f_items, n);
@@ -1304,9 +1312,9 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     run(PH_A, [&](int l) { ph_A<EW, true>(a, c, t, env0, l, step, slot); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot);
     if (!(a.dbg_skip & 32)) {
-      run(PH_E, [&](int l) { c.sc->rcp_all ? ph_E0<EW, true>(a, c, t, env0, l) : ph_E0<EW, false>(a, c, t, env0, l); });
-      run(PH_E, [&](int l) { ph_E<EW>(a, c, t, env0, l); });
-      if (a.dyn_reset != nullptr) run(PH_E, [&](int l) { ph_R<EW>(c, t, l); });
+      run(PH_E, [&](int l) { c.sh.rcp_all ? ph_E0<EW, true>(a, c, t, env0, l) : ph_E0<EW, false>(a, c, t, env0, l); });
+      run(PH_E1, [&](int l) { ph_E<EW>(a, c, t, env0, l); });
+      if (a.dyn_reset != nullptr) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     }
     if (ROLL) run(PH_RET, [&](int l) { ph_ret<EW>(a, c, t, env0, l); });
   }
@@ -1325,7 +1333,7 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
     run(PH_RESTORE, [&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });
     run(PH_A, [&](int l) { ph_A<EW, false>(a, c, t, env0, l, step); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0);
-    run(PH_E, [&](int l) { c.sc->rcp_all ? ph_E0<EW, true>(a, c, t, env0, l) : ph_E0<EW, false>(a, c, t, env0, l); });
+    run(PH_E, [&](int l) { c.sh.rcp_all ? ph_E0<EW, true>(a, c, t, env0, l) : ph_E0<EW, false>(a, c, t, env0, l); });
     run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l); });
     run(PH_G, [&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
   }

@@ -257,6 +257,7 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
     fnset |= (fn == cx::FN_AABB_AABB || fn == cx::FN_CIRCLE_AABB || fn == cx::FN_CIRCLE_CIRCLE) ? FNS_ANALYTIC
              : (fn == cx::FN_CIRCLE_POLY ? FNS_CIRCLE_POLY : FNS_CONVEX);
   }
+  s.fnset = fnset;
   return 0;
 }
 

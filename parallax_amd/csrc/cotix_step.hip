@@ -59,6 +59,14 @@ struct WaveRun {
     cxk::wave_sync();
     acc[ph] += clock64() - t0;
   }
+#elif defined(COTIX_ASM_MARKERS)  // tooling: phase markers in the ISA (tools/isa_phases.py)
+  template <class F>
+  __device__ __forceinline__ void operator()(int ph, F f) const {
+    asm volatile(";#PHASE_BEGIN %0" ::"s"(ph));
+    f(lane);
+    cxk::wave_sync();
+    asm volatile(";#PHASE_END %0" ::"s"(ph));
+  }
 #else
   template <class F>
   __device__ __forceinline__ void operator()(int, F f) const {
@@ -72,11 +80,10 @@ template <int EW, int FNSET, int MODE>
 __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   extern __shared__ uint32_t lds[];
   const SceneDev* sc = a.sc;
-  const int nhot = sc->nhot;
+  const int nhot = a.sh.nhot;
   for (int i = threadIdx.x; i < nhot; i += WPB * 64) lds[i] = sc->hot[i];
   __syncthreads();
-  const cxk::Ctx c{sc->nb, sc->np, sc->nc, sc->nl, sc->nt, sc, cxk::layout(sc->nb, sc->W, sc->nc, sc->nt, sc->G),
-                   cxk::ws_layout(sc->nl, sc->nc, EW, sc->poly)};
+  const cxk::Ctx c = cxk::make_ctx<EW>(a.sh);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int env0 = (blockIdx.x * WPB + wave) * EW;
   if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
@@ -300,6 +307,7 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
   if (lds > 160 * 1024) return fail("scene too large for the LDS tile");
   cxk::KArgs ka = ka0;
   ka.sc = scene->dev;
+  ka.sh = scene->host;  // the header by value (kernel arguments)
   const char* dbg = getenv("COTIX_DEBUG_SKIP");
   ka.dbg_skip = dbg ? atoi(dbg) : 0;
   dim3 grid((ka.B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);

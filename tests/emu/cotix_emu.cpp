@@ -35,20 +35,24 @@ struct HostRun {
 template <int EW>
 void run_blocks(const cxk::KArgs& a, int mode) {
   const cxk::SceneDev& sc = *a.sc;
-  const cxk::Ctx c{sc.nb, sc.np, sc.nc, sc.nl, sc.nt, &sc, cxk::layout(sc.nb, sc.W, sc.nc, sc.nt, sc.G),
-                   cxk::ws_layout(sc.nl, sc.nc, EW, sc.poly)};
+  const cxk::Ctx c = cxk::make_ctx<EW>(sc);
   const int nwaves = (a.B + EW - 1) / EW;
   std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)c.L.S * EW + (size_t)cxk::ws_words(sc, EW));
   for (int q = 0; q < sc.nhot; ++q) lds[q] = sc.hot[q];
   for (int wv = 0; wv < nwaves; ++wv) {
     std::fill(lds.begin() + sc.nhot, lds.end(), 0x7FBADBADu);  // poison (a NaN pattern)
     const cxk::Tile<EW> t{lds.data() + sc.nhot, lds.data(), lds.data() + sc.nhot + (size_t)c.L.S * EW};
+    // the kernel instantiation the library launches: analytic-only scenes get
+    // the circle/AABB program (FNSET 1), others the full one
+    const bool an = (sc.fnset & ~cxk::FNS_ANALYTIC) == 0;
     if (mode == 2)
-      cxk::run_wave_backward<EW, 7>(a, c, t, wv * EW, HostRun{});
+      an ? cxk::run_wave_backward<EW, 1>(a, c, t, wv * EW, HostRun{})
+         : cxk::run_wave_backward<EW, 7>(a, c, t, wv * EW, HostRun{});
     else if (mode == 1)
-      cxk::run_wave<EW, 7, true>(a, c, t, wv * EW, HostRun{});
+      an ? cxk::run_wave<EW, 1, true>(a, c, t, wv * EW, HostRun{}) : cxk::run_wave<EW, 7, true>(a, c, t, wv * EW, HostRun{});
     else
-      cxk::run_wave<EW, 7, false>(a, c, t, wv * EW, HostRun{});
+      an ? cxk::run_wave<EW, 1, false>(a, c, t, wv * EW, HostRun{})
+         : cxk::run_wave<EW, 7, false>(a, c, t, wv * EW, HostRun{});
   }
 }
 void run_any(const cxk::KArgs& a, int E, int mode) {
@@ -83,7 +87,21 @@ int emu_step(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float
              int n_steps, float dt, int stages, const float* action, int action_body, const float* dyn_reset,
              uint32_t* resets, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
-  cxk::KArgs a{&s->s, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, action, action_body, dyn_reset, resets, 0};
+  cxk::KArgs a{};
+  a.sc = &s->s;
+  a.dyn = dyn;
+  a.keys = keys;
+  a.err = err;
+  a.geom = geom;
+  a.gstride = gstride;
+  a.B = B;
+  a.n_steps = n_steps;
+  a.dt = dt;
+  a.stages = stages;
+  a.action = action;
+  a.action_body = action_body;
+  a.dyn_reset = dyn_reset;
+  a.resets = resets;
   run_any(a, E, 0);
   return 0;
 }

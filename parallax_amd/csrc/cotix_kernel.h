@@ -134,7 +134,7 @@ CX_HD Lay layout(int nb, int W, int nc, int nt, int G) {
 static inline int tile_words(const SceneHdr& s) { return layout(s.nb, s.W, s.nc, s.nt, s.G).S; }
 // per-wave scratch of phase C (words, not per env): pass flags, keep flags,
 // active count, two item lists (double buffer), per-item scan positions
-enum : int { WS_FLAG = 0, WS_KEEP = 64, WS_N = 128, WS_LIST = 129 };
+enum : int { WS_FLAG = 0, WS_KEEP = 64, WS_KEEP2 = 128, WS_N = 192, WS_LIST = 193 };
 // + (polygon scenes) the deferred contact-point area of phase F: per-item
 // flags and list (padded to 64), count, per-batch term counts, term results
 constexpr int CFB = 8;                           // items per batch
@@ -770,6 +770,97 @@ CX_DEV void ph_C3(const Ctx& c, Tile<EW> t, int lane, int par) {
   if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)(kept + (n > WAVE ? n - WAVE : 0));
 }
 
+// Phase C when every (cell, env) item fits one lane (nl * EW <= 64): item
+// id == lane, the pending items are a 64-bit ballot mask (no compaction
+// passes), and each lane updates only its own item's state, so one round is
+// two phases.  Pending flags alternate between WS_KEEP and WS_KEEP2.
+CX_DEV int select_bit(uint64_t m, int k) {  // position of the k-th (0-based) set bit of m
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t lo = m & ((1ull << w) - 1ull);
+    const int c = popc64(lo);
+    const bool up = k >= c;
+    k = up ? k - c : k;
+    m = up ? (m >> w) : lo;
+    pos = up ? pos + w : pos;
+  }
+  return pos;
+}
+// M0: activity (a cell whose distinct contacts are all NaN never writes)
+template <int EW>
+CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  const SceneHdr& sc = c.sh;
+  uint32_t flag = 0u;
+  if (lane < c.nl * EW) {
+    const int e = lane % EW, l = lane / EW;
+    if (env0 + e < a.B) {
+      bool any = false;
+      for (int q = 0; q < sc.nmw; ++q) any = any || (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
+      if (any) {
+        flag = 1u;
+        t.ws[WS_LIST + 2 * c.nl * EW + lane] = 0u;  // scan position
+      }
+    }
+  }
+  t.ws[WS_KEEP + lane] = flag;
+}
+// M1: the pending count (read after the phase: 0 ends the scan), then every
+// lane draws one candidate: G = 64 / n lanes per pending item, in mask order
+template <int EW>
+CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
+  const int n = popc64(pend);
+  if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)n;
+  uint32_t pass = 0u;
+  if (n > 0) {
+    const int G = WAVE / n, slot = lane / G, q = lane % G;
+    if (slot < n) {
+      const int id = select_bit(pend, slot), e = id % EW, l = id / EW;
+      const int idx = (int)t.ws[WS_LIST + 2 * c.nl * EW + id] + q;
+      if (idx < t.ti(sc.o_ccnt + l)) {
+        const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
+        const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
+        const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
+        if (!(isn(cpx) || isn(cpy))) {  // a NaN candidate never writes
+          const key2 sk = key2{t.w(c.L.skt + 2 * ty, e), t.w(c.L.skt + 2 * ty + 1, e)};
+          const key2 k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
+          const key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);   // :254
+          pass = bernoulli_half(split_at(k, 2u, 0u)) ? 1u : 0u;                      // :222-223
+        }
+      }
+    }
+  }
+  t.ws[WS_FLAG + lane] = pass;
+}
+// M2: lane `lane` settles its own item: the first passing draw of its slot
+// writes the cell, else the scan position advances by G
+template <int EW>
+CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
+  const SceneHdr& sc = c.sh;
+  const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
+  const uint64_t pm = wave_ballot(t.ws + WS_FLAG, lane);
+  uint32_t keep = 0u;
+  if ((pend >> lane) & 1ull) {
+    const int n = popc64(pend), G = WAVE / n, slot = popc64(pend & lanes_below(lane));
+    const int e = lane % EW, l = lane / EW;
+    const uint64_t gm = G == WAVE ? ~0ull : ((1ull << G) - 1ull);
+    const uint64_t bits = (pm >> (slot * G)) & gm;
+    uint32_t& pos = t.ws[WS_LIST + 2 * c.nl * EW + lane];
+    if (bits != 0ull) {
+      const int idx = (int)pos + __builtin_ctzll(bits);
+      const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
+      t.w(c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = (cd >> 18) & 511u;
+    } else {
+      pos = pos + (uint32_t)G;
+      keep = (int)pos < t.ti(sc.o_ccnt + l) ? 1u : 0u;
+    }
+  }
+  t.ws[(par ? WS_KEEP : WS_KEEP2) + lane] = keep;
+}
+
 // phase D: choose_random_contact (cotix/_colliders.py:274-295)
 // one (body i, env) item of phase D; NB > 0: the body count at compile time
 // (unrolled loads and selects), NB == 0: any count up to MAXB
@@ -1273,7 +1364,17 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_F, [&](int l) { ph_F3<EW>(c, t, l, b); });
     }
   }
-  if (!(a.dbg_skip & 4) && c.nl > 0) {
+  if (!(a.dbg_skip & 4) && c.nl > 0 && c.nl * EW <= WAVE) {
+    run(PH_C0, [&](int l) { ph_M0<EW>(a, c, t, env0, l); });
+    CXK_STAT(wave_steps, 1);
+    for (int par = 0;; par ^= 1) {
+      run(PH_C1, [&](int l) { ph_M1<EW>(c, t, l, par); });
+      if (t.ws[WS_N] == 0u) break;  // uniform: read after the phase barrier
+      CXK_STAT(rounds, 1);
+      if (par == 0) CXK_STAT(active_items, t.ws[WS_N]);
+      run(PH_C2, [&](int l) { ph_M2<EW>(c, t, l, par); });
+    }
+  } else if (!(a.dbg_skip & 4) && c.nl > 0) {
     for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {
       run(PH_C0, [&](int l) { ph_C0<EW>(a, c, t, env0, l, ch); });
       run(PH_C0B, [&](int l) { ph_C0b<EW>(c, t, l, ch); });

@@ -48,7 +48,7 @@ def run_trace(emu, lib, bodies, geom_rows, tr, stages, EW, per_env_geom):
         assert np.array_equal(err, np.bitwise_or.reduce(tr["err"][: t + 1], axis=0)), "err step %d" % t
 
 
-@pytest.mark.parametrize("EW", [1, 2, 4])
+@pytest.mark.parametrize("EW", [1, 2, 4, 8])  # EW 8: 12 cells x 8 envs > 64 lanes -> the list-based scan
 def test_emu_robocup_trace(emu_lib, EW):
     emu, lib = emu_lib
     from cotix_oracle import physics as P

@@ -382,40 +382,49 @@ CX_DEV void ph_K2(const Ctx& c, Tile<EW> t, int lane, int n) {
 
 // PRE: the step's keys come from the key window (slot `slot`); otherwise
 // (backward re-play from saved keys) they are split here.
+// Euler (cotix/_physics_solvers.py:16-33) + the driver's velocity terms for
+// body b of env e (examples/test_viz.py:27-31; the config-5 action hook)
+template <int EW>
+CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int b, int step) {
+  const int o = c.L.dyn + b * 6;
+  if (!(a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))) return;
+  if (a.stages & COTIX_STAGE_EULER) {
+    t.f(o + 0, e) = t.f(o + 0, e) + t.f(o + 2, e) * a.dt;
+    t.f(o + 1, e) = t.f(o + 1, e) + t.f(o + 3, e) * a.dt;
+    t.f(o + 4, e) = t.f(o + 4, e) + t.f(o + 5, e) * a.dt;
+  }
+  if ((a.stages & COTIX_STAGE_GRAVITY) && b == 0) {  // examples/test_viz.py:27-31
+    t.f(o + 2, e) = t.f(o + 2, e) + 0.0f;
+    t.f(o + 3, e) = t.f(o + 3, e) + -0.002f;
+  }
+  if (a.action != nullptr && b == a.action_body) {
+    const float* ac = a.action + ((size_t)step * a.B + env0 + e) * 2;
+    t.f(o + 2, e) = t.f(o + 2, e) + ac[0];
+    t.f(o + 3, e) = t.f(o + 3, e) + ac[1];
+  }
+}
+// per-step collider scratch: all_contacts cells empty (:137-140), choice =
+// self (m and ch are adjacent in the tile: one flat, branch-free pass), no
+// valid contact
+template <int EW>
+CX_DEV void reset_scratch(const Ctx& c, Tile<EW> t, int lane) {
+  const int nm = c.nb * c.nb;
+  for (int w = lane; w < (nm + c.nb) * EW; w += WAVE)
+    t.u[c.L.m * EW + w] = w < nm * EW ? 0xFFFFFFFFu : (uint32_t)(w / EW - nm);
+  for (int w = lane; w < c.sh.nmw * EW; w += WAVE) t.u[c.L.vm * EW + w] = 0u;
+}
+
 template <int EW, bool PRE = false>
 CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step, int slot = 0) {
   using namespace cx;
   const int nb = c.nb;
   const Lay& L = c.L;
-  if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY)) {
+  if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
     for (int w = lane; w < nb * EW; w += WAVE) {
-      int e = w % EW, b = w / EW, g = env0 + e;
-      if (g >= a.B) continue;
-      const int o = L.dyn + b * 6;
-      if (a.stages & COTIX_STAGE_EULER) {
-        t.f(o + 0, e) = t.f(o + 0, e) + t.f(o + 2, e) * a.dt;
-        t.f(o + 1, e) = t.f(o + 1, e) + t.f(o + 3, e) * a.dt;
-        t.f(o + 4, e) = t.f(o + 4, e) + t.f(o + 5, e) * a.dt;
-      }
-      if ((a.stages & COTIX_STAGE_GRAVITY) && b == 0) {  // examples/test_viz.py:27-31
-        t.f(o + 2, e) = t.f(o + 2, e) + 0.0f;
-        t.f(o + 3, e) = t.f(o + 3, e) + -0.002f;
-      }
-      if (a.action != nullptr && b == a.action_body) {
-        const float* ac = a.action + ((size_t)step * a.B + g) * 2;
-        t.f(o + 2, e) = t.f(o + 2, e) + ac[0];
-        t.f(o + 3, e) = t.f(o + 3, e) + ac[1];
-      }
+      const int e = w % EW, b = w / EW;
+      if (env0 + e < a.B) euler_item<EW>(a, c, t, env0, e, b, step);
     }
-  }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
-    if (PRE) {  // sk0, skt of this step from the window
-      const int nw = 2 + 2 * c.nt, o = L.kw + slot * L.kww;
-      for (int w = lane; w < nw * EW; w += WAVE) {
-        const int e = w % EW, q = w / EW;
-        t.w(L.sk0 + q, e) = t.w(o + q, e);  // sk0 and skt are adjacent in both
-      }
-    }
     for (int e = lane; e < EW; e += WAVE) {
       if (!PRE && !(a.dbg_skip & 16)) {
         key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
@@ -429,13 +438,7 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         }
       }
     }
-    // per-step collider scratch: all_contacts cells empty (:137-140), choice =
-    // self (m and ch are adjacent in the tile: one flat, branch-free pass), no
-    // valid contact
-    const int nm = nb * nb;
-    for (int w = lane; w < (nm + nb) * EW; w += WAVE)
-      t.u[L.m * EW + w] = w < nm * EW ? 0xFFFFFFFFu : (uint32_t)(w / EW - nm);
-    for (int w = lane; w < c.sh.nmw * EW; w += WAVE) t.u[L.vm * EW + w] = 0u;
+    reset_scratch<EW>(c, t, lane);
   }
 }
 
@@ -705,7 +708,7 @@ CX_DEV void ph_C0b(const Ctx& c, Tile<EW> t, int lane, int chunk) {
 }
 // R1: every lane draws one candidate of its item
 template <int EW>
-CX_DEV void ph_C1(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int par) {
+CX_DEV void ph_C1(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int par, int kso) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int NI = c.nl * EW;
@@ -721,7 +724,7 @@ CX_DEV void ph_C1(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int par) {
       const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
       const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
       if (!(isn(cpx) || isn(cpy))) {  // a NaN candidate never writes
-        const key2 sk = key2{t.w(c.L.skt + 2 * ty, e), t.w(c.L.skt + 2 * ty + 1, e)};
+        const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
         const key2 k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
         const key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);   // :254
         pass = bernoulli_half(split_at(k, 2u, 0u)) ? 1u : 0u;                      // :222-223
@@ -808,7 +811,7 @@ CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
 // M1: the pending count (read after the phase: 0 ends the scan), then every
 // lane draws one candidate: G = 64 / n lanes per pending item, in mask order
 template <int EW>
-CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par) {
+CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par, int kso) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
@@ -825,7 +828,7 @@ CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par) {
         const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
         const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
         if (!(isn(cpx) || isn(cpy))) {  // a NaN candidate never writes
-          const key2 sk = key2{t.w(c.L.skt + 2 * ty, e), t.w(c.L.skt + 2 * ty + 1, e)};
+          const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
           const key2 k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
           const key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);   // :254
           pass = bernoulli_half(split_at(k, 2u, 0u)) ? 1u : 0u;                      // :222-223
@@ -862,9 +865,60 @@ CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
 }
 
 // phase D: choose_random_contact (cotix/_colliders.py:274-295)
+CX_DEV cx::Params load_par(const uint32_t* tb, int o) {
+  return cx::Params{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1]), __uint_as_float(tb[o + 2]),
+                    __uint_as_float(tb[o + 3])};
+}
+CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
+  return cx::Rcp{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1])};
+}
+
+// resolution i's velocity-independent operands (phase E0 of the design:
+// computed by the phase-D item (body i, env e) right after its choice j)
+template <int EW, bool RCP>
+CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const Lay& L = c.L;
+  const int ro = L.rp + RP_W * i;
+  uint32_t jj = RP_NONE;
+  if (!(j == i || j < 0 || j >= c.nb) && cid >= 0) {
+    const int co = L.con + 4 * cid;
+    const v2 cp = v2{t.f(co + 2, e), t.f(co + 3, e)};
+    if (!vnan(cp)) {  // resolve_collision returns unchanged bodies on a NaN contact point
+      const int oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
+      const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
+      const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
+      const Params pj = load_par(t.tb, sc.o_par + 4 * j);
+      const Rcp qj = load_rcp(t.tb, sc.o_rcp + 2 * j);
+      const ResPre p = resolve_pre<RCP>(bi, load_par(t.tb, sc.o_par + 4 * i), load_rcp(t.tb, sc.o_rcp + 2 * i), bj, pj,
+                                        qj, v2{t.f(co, e), t.f(co + 1, e)}, cp);
+      t.f(ro + RP_NX, e) = p.n.x;
+      t.f(ro + RP_NY, e) = p.n.y;
+      t.f(ro + RP_R1X, e) = p.r1.x;
+      t.f(ro + RP_R1Y, e) = p.r1.y;
+      t.f(ro + RP_R2X, e) = p.r2.x;
+      t.f(ro + RP_R2Y, e) = p.r2.y;
+      t.f(ro + RP_PX, e) = p.pen.x;
+      t.f(ro + RP_PY, e) = p.pen.y;
+      t.f(ro + RP_DEN, e) = p.den;
+      t.f(ro + RP_PT, e) = p.pterm;
+      t.f(ro + RP_NE, e) = p.ne;
+      t.f(ro + RP_MU, e) = p.mu;
+      t.f(ro + RP_MJ, e) = pj.mass;
+      t.f(ro + RP_IJ, e) = pj.inertia;
+      t.f(ro + RP_QMJ, e) = qj.m;
+      t.f(ro + RP_QIJ, e) = qj.i;
+      jj = (uint32_t)j;
+      CXK_STAT(resolutions, 1);
+    }
+  }
+  t.w(ro + RP_J, e) = jj;
+}
+
 // one (body i, env) item of phase D; NB > 0: the body count at compile time
 // (unrolled loads and selects), NB == 0: any count up to MAXB
-template <int EW, bool PRE, int NB>
+template <int EW, bool PRE, int NB, bool RCP>
 CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
   using namespace cx;
   constexpr int MB = NB > 0 ? NB : MAXB;
@@ -872,12 +926,15 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
   const Lay& L = c.L;
   int cnt = 0;
   uint32_t good = 0u;
+  int mm[MB];
 #pragma unroll
-  for (int j = 0; j < MB; ++j)
-    if (j < nb && (int)t.w(L.m + i * nb + j, e) >= 0) {
+  for (int j = 0; j < MB; ++j) {
+    mm[j] = j < nb ? (int)t.w(L.m + i * nb + j, e) : -1;
+    if (mm[j] >= 0) {
       good |= 1u << j;
       ++cnt;
     }
+  }
   int ch = i;
   if (cnt > 0) {
     float p[MB], cs[MB];
@@ -908,6 +965,10 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
       if (j < nb && !(cs[j] < r)) ch = j;  // first j with r <= cumsum[j]
   }
   t.w(L.ch + i, e) = (uint32_t)ch;
+  int cid = -1;  // all_contacts[i, ch], picked from the loaded row
+#pragma unroll
+  for (int j = 0; j < MB; ++j) cid = j == ch ? mm[j] : cid;
+  e0_item<EW, RCP>(c, t, e, i, ch, cid);
 }
 template <int EW, bool PRE = false>
 CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int slot = 0) {
@@ -915,19 +976,18 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   for (int w = lane; w < nb * EW; w += WAVE) {
     const int e = w % EW, i = w / EW;
     if (env0 + e >= a.B) continue;
-    if (nb == 5) d_item<EW, PRE, 5>(c, t, e, i, slot);
-    else if (nb == 4) d_item<EW, PRE, 4>(c, t, e, i, slot);
-    else d_item<EW, PRE, 0>(c, t, e, i, slot);
+    if (c.sh.rcp_all) {
+      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, slot);
+      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, slot);
+      else d_item<EW, PRE, 0, true>(c, t, e, i, slot);
+    } else {
+      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, slot);
+      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, slot);
+      else d_item<EW, PRE, 0, false>(c, t, e, i, slot);
+    }
   }
 }
 
-CX_DEV cx::Params load_par(const uint32_t* tb, int o) {
-  return cx::Params{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1]), __uint_as_float(tb[o + 2]),
-                    __uint_as_float(tb[o + 3])};
-}
-CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
-  return cx::Rcp{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1])};
-}
 
 // phase E: sequential resolution (:310-336), joints, key update, restarts.
 // E0 (item = (body i, env), all lanes): everything of resolution i that does
@@ -936,56 +996,6 @@ CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
 // folded into cx::ResPre.  E1 (one lane per env): the sequential pass over
 // the bodies carrying only the velocity-dependent part, velocities held in
 // registers for the common body counts.
-template <int EW, bool RCP>
-CX_DEV void ph_E0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
-  using namespace cx;
-  if (!(a.stages & COTIX_STAGE_COLLIDER)) return;
-  const SceneHdr& sc = c.sh;
-  const int nb = c.nb;
-  const Lay& L = c.L;
-  for (int w = lane; w < nb * EW; w += WAVE) {
-    const int e = w % EW, i = w / EW, g = env0 + e;
-    if (g >= a.B) continue;
-    const int ro = L.rp + RP_W * i;
-    uint32_t jj = RP_NONE;
-    const int j = (int)t.w(L.ch + i, e);
-    if (!(j == i || j < 0 || j >= nb)) {
-      const int cid = (int)t.w(L.m + i * nb + j, e);
-      if (cid >= 0) {
-        const int co = L.con + 4 * cid;
-        const v2 cp = v2{t.f(co + 2, e), t.f(co + 3, e)};
-        if (!vnan(cp)) {  // resolve_collision returns unchanged bodies on a NaN contact point
-          const int oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
-          const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
-          const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
-          const Params pj = load_par(t.tb, sc.o_par + 4 * j);
-          const Rcp qj = load_rcp(t.tb, sc.o_rcp + 2 * j);
-          const ResPre p = resolve_pre<RCP>(bi, load_par(t.tb, sc.o_par + 4 * i), load_rcp(t.tb, sc.o_rcp + 2 * i), bj, pj,
-                                       qj, v2{t.f(co, e), t.f(co + 1, e)}, cp);
-          t.f(ro + RP_NX, e) = p.n.x;
-          t.f(ro + RP_NY, e) = p.n.y;
-          t.f(ro + RP_R1X, e) = p.r1.x;
-          t.f(ro + RP_R1Y, e) = p.r1.y;
-          t.f(ro + RP_R2X, e) = p.r2.x;
-          t.f(ro + RP_R2Y, e) = p.r2.y;
-          t.f(ro + RP_PX, e) = p.pen.x;
-          t.f(ro + RP_PY, e) = p.pen.y;
-          t.f(ro + RP_DEN, e) = p.den;
-          t.f(ro + RP_PT, e) = p.pterm;
-          t.f(ro + RP_NE, e) = p.ne;
-          t.f(ro + RP_MU, e) = p.mu;
-          t.f(ro + RP_MJ, e) = pj.mass;
-          t.f(ro + RP_IJ, e) = pj.inertia;
-          t.f(ro + RP_QMJ, e) = qj.m;
-          t.f(ro + RP_QIJ, e) = qj.i;
-          jj = (uint32_t)j;
-          CXK_STAT(resolutions, 1);
-        }
-      }
-    }
-    t.w(ro + RP_J, e) = jj;
-  }
-}
 
 template <int EW>
 CX_DEV cx::ResPre load_rp(Tile<EW> t, int ro, int e) {
@@ -1015,10 +1025,24 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
     vy[b] = t.f(L.dyn + 6 * b + 3, e);
     vw[b] = t.f(L.dyn + 6 * b + 5, e);
   }
+  // every resolution's operands up front: one LDS latency for the pass
+  uint32_t jv[NB];
+  ResPre pr[NB];
+  Params pj[NB], pi[NB];
+  Rcp qj[NB], qi[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int ro = L.rp + RP_W * i;
-    const uint32_t j = t.w(ro + RP_J, e);
+    jv[i] = t.w(ro + RP_J, e);
+    pr[i] = load_rp<EW>(t, ro, e);
+    pj[i] = Params{t.f(ro + RP_MJ, e), t.f(ro + RP_IJ, e), 0.0f, 0.0f};
+    qj[i] = Rcp{t.f(ro + RP_QMJ, e), t.f(ro + RP_QIJ, e)};
+    pi[i] = load_par(t.tb, sc.o_par + 4 * i);
+    qi[i] = load_rcp(t.tb, sc.o_rcp + 2 * i);
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const uint32_t j = jv[i];
     if (REC) t.w(L.rec + REC_W * i, e) = 0u;
     if (j == RP_NONE) continue;
     float jx = 0.0f, jy = 0.0f, jw = 0.0f;
@@ -1038,11 +1062,7 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
       t.f(rc + 5, e) = jy;
       t.f(rc + 6, e) = jw;
     }
-    const Params pi = load_par(t.tb, sc.o_par + 4 * i);
-    const Params pj = Params{t.f(ro + RP_MJ, e), t.f(ro + RP_IJ, e), 0.0f, 0.0f};
-    const Rcp qj = Rcp{t.f(ro + RP_QMJ, e), t.f(ro + RP_QIJ, e)};
-    const bool applied = resolve_seq<RCP>(vx[i], vy[i], vw[i], pi, load_rcp(t.tb, sc.o_rcp + 2 * i), jx, jy, jw, pj, qj,
-                                     load_rp<EW>(t, ro, e));
+    const bool applied = resolve_seq<RCP>(vx[i], vy[i], vw[i], pi[i], qi[i], jx, jy, jw, pj[i], qj[i], pr[i]);
     if (REC) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
 #pragma unroll
     for (int b = 0; b < NB; ++b)
@@ -1100,7 +1120,7 @@ CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e) {
 // REC (backward re-play only): record, per resolution, whether the impulses
 // were applied and the pre-resolution velocities of the two bodies.
 template <int EW, bool REC = false>
-CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int nb = c.nb;
@@ -1141,8 +1161,8 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       }
     }
     if (a.stages & COTIX_STAGE_ADVANCE_KEY) {  // examples/test_viz.py:39,66
-      t.w(L.key, e) = t.w(L.sk0, e);
-      t.w(L.key + 1, e) = t.w(L.sk0 + 1, e);
+      t.w(L.key, e) = t.w(kso, e);
+      t.w(L.key + 1, e) = t.w(kso + 1, e);
     }
     if (a.dyn_reset != nullptr) {
       // episode end on an error_if trip (the reference raises here): the env
@@ -1348,8 +1368,10 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
              PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_COUNT };
 // ---------------------------------------------------------------------------
+// kso: tile offset of this step's sk0 (skt follows): the key window slot, or
+// L.sk0 where phase A splits the keys (backward re-play)
 template <int EW, int FNSET, bool PRE, class R>
-CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot) {
+CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso) {
   if (!(a.dbg_skip & 1)) run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
   if (!(a.dbg_skip & 2)) run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
   if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && !(a.dbg_skip & 2)) {
@@ -1368,7 +1390,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     run(PH_C0, [&](int l) { ph_M0<EW>(a, c, t, env0, l); });
     CXK_STAT(wave_steps, 1);
     for (int par = 0;; par ^= 1) {
-      run(PH_C1, [&](int l) { ph_M1<EW>(c, t, l, par); });
+      run(PH_C1, [&](int l) { ph_M1<EW>(c, t, l, par, kso); });
       if (t.ws[WS_N] == 0u) break;  // uniform: read after the phase barrier
       CXK_STAT(rounds, 1);
       if (par == 0) CXK_STAT(active_items, t.ws[WS_N]);
@@ -1383,7 +1405,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     CXK_STAT(active_items, t.ws[WS_N]);
     for (int par = 0; t.ws[WS_N] != 0u; par ^= 1) {  // uniform: read after the phase barrier
       CXK_STAT(rounds, 1);
-      run(PH_C1, [&](int l) { ph_C1<EW>(a, c, t, l, par); });
+      run(PH_C1, [&](int l) { ph_C1<EW>(a, c, t, l, par, kso); });
       run(PH_C2, [&](int l) { ph_C2<EW>(c, t, l, par); });
       run(PH_C3, [&](int l) { ph_C3<EW>(c, t, l, par); });
     }
@@ -1401,6 +1423,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
   });
   const bool keys = (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !(a.dbg_skip & 16);
+
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
@@ -1410,11 +1433,11 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       run(PH_K, [&](int l) { ph_K1<EW>(c, t, l, n); });
       if (a.stages & COTIX_STAGE_COLLIDER) run(PH_K, [&](int l) { ph_K2<EW>(c, t, l, n); });
     }
+    const int kso = c.L.kw + slot * c.L.kww;  // this step's sk0, skt in the key window
     run(PH_A, [&](int l) { ph_A<EW, true>(a, c, t, env0, l, step, slot); });
-    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot);
+    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso);
     if (!(a.dbg_skip & 32)) {
-      run(PH_E, [&](int l) { c.sh.rcp_all ? ph_E0<EW, true>(a, c, t, env0, l) : ph_E0<EW, false>(a, c, t, env0, l); });
-      run(PH_E1, [&](int l) { ph_E<EW>(a, c, t, env0, l); });
+      run(PH_E1, [&](int l) { ph_E<EW>(a, c, t, env0, l, kso); });
       if (a.dyn_reset != nullptr) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     }
     if (ROLL) run(PH_RET, [&](int l) { ph_ret<EW>(a, c, t, env0, l); });
@@ -1433,9 +1456,8 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
   for (int step = a.n_steps - 1; step >= 0; --step) {
     run(PH_RESTORE, [&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });
     run(PH_A, [&](int l) { ph_A<EW, false>(a, c, t, env0, l, step); });
-    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0);
-    run(PH_E, [&](int l) { c.sh.rcp_all ? ph_E0<EW, true>(a, c, t, env0, l) : ph_E0<EW, false>(a, c, t, env0, l); });
-    run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l); });
+    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0, c.L.sk0);
+    run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
     run(PH_G, [&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
   }
   run(PH_ADJ, [&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });

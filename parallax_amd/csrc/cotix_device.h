@@ -89,44 +89,45 @@ CX_DEV float cos_poly(float r) {
           0.5f * z) +
          1.0f;
 }
+// (the kernels below are written as flat selects: their branchy forms
+// compile to divergent branches on gfx950; every value is computed by the
+// same expression as the branchy form, so the results are identical)
 CX_DEV void sincos32(float x, float* s_out, float* c_out) {
-  if (isn(x) || __builtin_isinf(x)) {
-    *s_out = qnan();
-    *c_out = qnan();
-    return;
-  }
-  float t = x * 0.636619772367581343f;
+  const bool bad = isn(x) || __builtin_isinf(x);
+  const float xs = bad ? 0.0f : x;
+  float t = xs * 0.636619772367581343f;
   float k = (t + 12582912.0f) - 12582912.0f;
-  float r = ((x - k * 1.5703125f) - k * 4.837512969970703125e-4f) - k * 7.54978995489188216e-8f;
+  float r = ((xs - k * 1.5703125f) - k * 4.837512969970703125e-4f) - k * 7.54978995489188216e-8f;
   float s = sin_poly(r), c = cos_poly(r);
   int q = ((int)k) & 3;
-  if (q == 0) { *s_out = s; *c_out = c; }
-  else if (q == 1) { *s_out = c; *c_out = -s; }
-  else if (q == 2) { *s_out = -s; *c_out = -c; }
-  else { *s_out = -c; *c_out = s; }
+  // q = 0: (s, c), 1: (c, -s), 2: (-s, -c), 3: (-c, s)
+  float so = (q & 1) ? c : s, co = (q & 1) ? -s : c;
+  so = (q & 2) ? -so : so;
+  co = (q & 2) ? -co : co;
+  *s_out = bad ? qnan() : so;
+  *c_out = bad ? qnan() : co;
 }
 CX_DEV float atan01(float t) {
-  float y0 = 0.0f;
-  if (t > 0.4142135623730950f) {
-    y0 = 0.785398163397448309616f;
-    t = (t - 1.0f) / (t + 1.0f);
-  }
+  const bool big = t > 0.4142135623730950f;
+  const float y0 = big ? 0.785398163397448309616f : 0.0f;
+  t = big ? (t - 1.0f) / (t + 1.0f) : t;
   float z = t * t;
   float p = ((((8.05374449538e-2f * z + -1.38776856032e-1f) * z + 1.99777106478e-1f) * z + -3.33329491539e-1f) * z) * t + t;
   return y0 + p;
 }
 CX_DEV float atan2_32(float y, float x) {
   const float PI = 3.14159265358979323846f, PIO2 = 1.57079632679489661923f;
-  if (isn(x) || isn(y)) return qnan();
-  if (y == 0.0f) {
-    if (x > 0.0f || (x == 0.0f && !__builtin_signbit(x))) return y;
-    return __builtin_signbit(y) ? -PI : PI;
-  }
-  if (x == 0.0f) return y < 0.0f ? -PIO2 : PIO2;
-  float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
-  float r = (ay <= ax) ? atan01(ay / ax) : (PIO2 - atan01(ax / ay));
-  if (x < 0.0f) r = PI - r;
-  return y < 0.0f ? -r : r;
+  const float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
+  const bool sw = !(ay <= ax);  // (ay <= ax) ? atan01(ay / ax) : PIO2 - atan01(ax / ay)
+  float r = atan01((sw ? ax : ay) / (sw ? ay : ax));
+  r = sw ? PIO2 - r : r;
+  r = x < 0.0f ? PI - r : r;
+  r = y < 0.0f ? -r : r;
+  // special cases, lowest priority first: x == 0, then y == 0, then NaN
+  r = x == 0.0f ? (y < 0.0f ? -PIO2 : PIO2) : r;
+  const float y0r = (x > 0.0f || (x == 0.0f && !__builtin_signbit(x))) ? y : (__builtin_signbit(y) ? -PI : PI);
+  r = y == 0.0f ? y0r : r;
+  return (isn(x) || isn(y)) ? qnan() : r;
 }
 // lax.sort order key: -0 == +0, NaN after everything (all NaN equal).
 CX_DEV bool sort_lt(float a, float b) {

@@ -61,6 +61,7 @@ struct SceneHdr {
   int nmw;      // contact-mask words = ceil(nc / 32)
   int poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
   int rcp_all;  // 1: every mass and inertia has an exact reciprocal (o_rcp): resolutions multiply
+  int rcp_mask; // bit b: body b's mass and inertia have exact reciprocals (bodies < 32)
   int fnset;    // FNS_* bits of the contact functions the scene uses (kernel instantiation)
   int nhot;
 };
@@ -161,35 +162,51 @@ static inline size_t lds_bytes(const SceneHdr& s, int wpb, int ew) {
   return 4 * ((size_t)s.nhot + ((size_t)tile_words(s) * ew + (size_t)ws_words(s, ew)) * wpb);
 }
 
+// RL / RG: the lander's / both legs' mass and inertia have exact
+// reciprocals (ql, qr, qll; cx::Rcp) -- their divisions become products
+template <bool RL = false, bool RG = false>
 CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, const cx::Params& pl,
-                              const cx::Params& pr, const cx::Params& pll) {
-  // LunarLander.step, cotix/_lunar_lander.py:145-218
+                              const cx::Params& pr, const cx::Params& pll, cx::Rcp ql = cx::no_rcp(),
+                              cx::Rcp qr = cx::no_rcp(), cx::Rcp qll = cx::no_rcp()) {
+  // LunarLander.step, cotix/_lunar_lander.py:145-218.  The anchors are taken
+  // before any impulse (impulses change velocities only), so each body's
+  // sin/cos (rotate, cotix/_geometry_utils.py:81-88) is evaluated once.
   using namespace cx;
   const float f05 = 0.05f;
+  float sl, cl, sr, cr, sll, cll;
+  sincos32(lander.a, &sl, &cl);
+  sincos32(rleg.a, &sr, &cr);
+  sincos32(lleg.a, &sll, &cll);
+  auto rot = [](v2 v, float sn, float cs) { return v2{cs * v.x + (-sn) * v.y, sn * v.x + cs * v.y}; };
   v2 lp = v2{lander.px, lander.py};
-  v2 llj1 = add(rotate(v2{24.0f * f05, -8.0f * f05}, lander.a), lp);
-  v2 llj2 = add(rotate(v2{24.0f * f05, 0.0f * f05}, lander.a), lp);
+  v2 llj1 = add(rot(v2{24.0f * f05, -8.0f * f05}, sl, cl), lp);
+  v2 llj2 = add(rot(v2{24.0f * f05, 0.0f * f05}, sl, cl), lp);
   v2 lj1 = v2{lleg.px, lleg.py};
-  v2 lj2 = add(v2{lleg.px, lleg.py}, rotate(v2{0.0f, 0.4f}, lleg.a));
-  v2 lrj1 = add(rotate(v2{-24.0f * f05, -8.0f * f05}, lander.a), lp);
-  v2 lrj2 = add(rotate(v2{-24.0f * f05, 0.0f * f05}, lander.a), lp);
+  v2 lj2 = add(v2{lleg.px, lleg.py}, rot(v2{0.0f, 0.4f}, sll, cll));
+  v2 lrj1 = add(rot(v2{-24.0f * f05, -8.0f * f05}, sl, cl), lp);
+  v2 lrj2 = add(rot(v2{-24.0f * f05, 0.0f * f05}, sl, cl), lp);
   v2 rj1 = v2{rleg.px, rleg.py};
-  v2 rj2 = add(v2{rleg.px, rleg.py}, rotate(v2{0.0f, 0.4f}, rleg.a));
-  struct J {
-    static CX_MF void fixed(Dyn& b1, const Params& m1, v2 c1, Dyn& b2, const Params& m2, v2 c2) {
-      const float f05 = 0.05f;
-      v2 dp = sub(c1, c2);
-      v2 dv = sub(velocity_at(b1, c1), velocity_at(b2, c2));
-      float k = nrm(dv) + 0.1f;
-      v2 imp = v2{dp.x * 1.0f + (dv.x * k) * f05, dp.y * 1.0f + (dv.y * k) * f05};
-      apply_impulse(b1, m1, neg(imp), c1);
-      apply_impulse(b2, m2, imp, c2);
-    }
+  v2 rj2 = add(v2{rleg.px, rleg.py}, rot(v2{0.0f, 0.4f}, sr, cr));
+  // apply_impulse (cotix/_bodies.py:68-73) with optional exact reciprocals
+  auto apply = [](Dyn& b, const Params& m, Rcp q, bool r, v2 imp, v2 point) {
+    const v2 arm = sub(point, v2{b.px, b.py});
+    const float torque = crs(arm, imp);
+    b.vx = b.vx + (r ? imp.x * q.m : imp.x / m.mass);
+    b.vy = b.vy + (r ? imp.y * q.m : imp.y / m.mass);
+    b.w = b.w + (r ? torque * q.i : torque / m.inertia);
   };
-  J::fixed(lander, pl, llj1, lleg, pll, lj1);
-  J::fixed(lander, pl, llj2, lleg, pll, lj2);
-  J::fixed(lander, pl, lrj1, rleg, pr, rj1);
-  J::fixed(lander, pl, lrj2, rleg, pr, rj2);
+  auto fixed = [&](Dyn& b1, const Params& m1, Rcp q1, v2 c1, Dyn& b2, const Params& m2, Rcp q2, v2 c2) {
+    v2 dp = sub(c1, c2);
+    v2 dv = sub(velocity_at(b1, c1), velocity_at(b2, c2));
+    float k = nrm(dv) + 0.1f;
+    v2 imp = v2{dp.x * 1.0f + (dv.x * k) * f05, dp.y * 1.0f + (dv.y * k) * f05};
+    apply(b1, m1, q1, RL, neg(imp), c1);
+    apply(b2, m2, q2, RG, imp, c2);
+  };
+  fixed(lander, pl, ql, llj1, lleg, pll, qll, lj1);
+  fixed(lander, pl, ql, llj2, lleg, pll, qll, lj2);
+  fixed(lander, pl, ql, lrj1, rleg, pr, qr, rj1);
+  fixed(lander, pl, ql, lrj2, rleg, pr, qr, rj2);
   rleg.w = rleg.w * 0.95f;
   lleg.w = lleg.w * 0.95f;
 }
@@ -1150,8 +1167,15 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         const int o = L.dyn + 6 * b;
         d[b] = Dyn{t.f(o, e), t.f(o + 1, e), t.f(o + 2, e), t.f(o + 3, e), t.f(o + 4, e), t.f(o + 5, e)};
       }
-      lunar_constraints(d[0], d[1], d[2], load_par(t.tb, sc.o_par), load_par(t.tb, sc.o_par + 4),
-                        load_par(t.tb, sc.o_par + 8));
+      const Params p0 = load_par(t.tb, sc.o_par), p1 = load_par(t.tb, sc.o_par + 4), p2 = load_par(t.tb, sc.o_par + 8);
+      const Rcp q0 = load_rcp(t.tb, sc.o_rcp), q1 = load_rcp(t.tb, sc.o_rcp + 2), q2 = load_rcp(t.tb, sc.o_rcp + 4);
+      const int rm = sc.rcp_mask;  // scene constant: uniform branch
+      if ((rm & 7) == 7)
+        lunar_constraints<true, true>(d[0], d[1], d[2], p0, p1, p2, q0, q1, q2);
+      else if ((rm & 6) == 6)
+        lunar_constraints<false, true>(d[0], d[1], d[2], p0, p1, p2, q0, q1, q2);
+      else
+        lunar_constraints<false, false>(d[0], d[1], d[2], p0, p1, p2, q0, q1, q2);
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
         const int o = L.dyn + 6 * b;

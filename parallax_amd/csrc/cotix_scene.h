@@ -180,10 +180,15 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   {
     s.o_rcp = (int)hot.size();  // exact reciprocals of mass and inertia (cx::Rcp)
     s.rcp_all = 1;
+    s.rcp_mask = 0;
+    for (int b = 0; b < n_bodies; ++b) s.rcp_mask |= (b < 32 ? 1 << b : 0);
     for (int b = 0; b < n_bodies; ++b)
       for (int q = 0; q < 2; ++q) {
         const float r = exact_rcp(body_params[4 * b + q]);
-        if (std::isnan(r)) s.rcp_all = 0;
+        if (std::isnan(r)) {
+          s.rcp_all = 0;
+          if (b < 32) s.rcp_mask &= ~(1 << b);
+        }
         uint32_t u;
         std::memcpy(&u, &r, 4);
         hot.push_back(u);

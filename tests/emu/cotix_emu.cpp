@@ -247,3 +247,13 @@ extern "C" int emu_stats(unsigned long long* out) {
   return 6;
 }
 #endif
+
+// the kernels' deterministic f32 transcendentals (tests: vs the oracle)
+extern "C" int emu_sincos(const float* x, int n, float* s, float* c) {
+  for (int i = 0; i < n; ++i) cx::sincos32(x[i], &s[i], &c[i]);
+  return 0;
+}
+extern "C" int emu_atan2(const float* y, const float* x, int n, float* out) {
+  for (int i = 0; i < n; ++i) out[i] = cx::atan2_32(y[i], x[i]);
+  return 0;
+}

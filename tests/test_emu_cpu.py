@@ -188,3 +188,32 @@ def test_emu_contact_operators_vs_golden(emu_lib, name):
                      out.ctypes.data_as(emu.P_), err.ctypes.data_as(emu.P_))
     assert same_f32(out, g[name + "_out"])
     assert np.array_equal(err, g[name + "_err"])
+
+
+def _edge_floats(rng, n):
+    special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 1e-38, np.pi, -np.pi, np.pi / 2,
+                        -np.pi / 2, np.pi / 4, 3 * np.pi / 4, 1e4, -1e4, 0.41421356, 0.41421357, 1.0, -1.0],
+                       np.float32)
+    return np.concatenate([special, rng.normal(0, 3, n).astype(np.float32),
+                           rng.uniform(-1e3, 1e3, n).astype(np.float32)])
+
+
+def test_emu_transcendentals_vs_oracle(emu_lib):
+    """sincos32 / atan2_32 of the kernels (cotix_device.h, branch-free selects)
+    == the oracle's (branchy) restatement, bit for bit, on edge cases
+    (+-0, +-inf, NaN, quadrant and octant boundaries) and random values."""
+    emu, lib = emu_lib
+    from cotix_oracle import geometry as G
+    rng = np.random.default_rng(7)
+    x = np.ascontiguousarray(_edge_floats(rng, 2000))
+    s = np.zeros_like(x)
+    c = np.zeros_like(x)
+    lib.emu_sincos(x.ctypes.data_as(emu.P_), x.size, s.ctypes.data_as(emu.P_), c.ctypes.data_as(emu.P_))
+    want = np.array([G.sincos32(v) for v in x], np.float32)
+    assert same_f32(s, want[:, 0]) and same_f32(c, want[:, 1])
+    yy, xx = np.meshgrid(_edge_floats(rng, 60), _edge_floats(rng, 60))
+    yy, xx = np.ascontiguousarray(yy.ravel()), np.ascontiguousarray(xx.ravel())
+    out = np.zeros_like(yy)
+    lib.emu_atan2(yy.ctypes.data_as(emu.P_), xx.ctypes.data_as(emu.P_), yy.size, out.ctypes.data_as(emu.P_))
+    want = np.array([G.atan2_32(a, b) for a, b in zip(yy, xx)], np.float32)
+    assert same_f32(out, want)

@@ -132,6 +132,7 @@ def main():
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
     obs_all = torch.empty(world_size * B, len(scen.bodies), 6, device=dev) if dist else None
+    obs_local = torch.empty(B, len(scen.bodies), 6, device=dev) if dist else None
 
     # HIP events around every step-kernel launch, on the stream it runs on
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
@@ -143,7 +144,7 @@ def main():
         if i is not None:
             evs[i][1].record()
         if dist is not None:  # north star: RCCL all-gather of the observation tensor
-            dist.all_gather_into_tensor(obs_all, env.observation().contiguous())
+            dist.all_gather_into_tensor(obs_all, env.observation(obs_local))
 
     for _ in range(a.warmup):
         one_step()

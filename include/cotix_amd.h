@@ -27,6 +27,10 @@
  *                         cotix/_universal_shape.py:87-132
  *   cotix_body_aabb       UniversalShape.possibly_collides_with (AABB.of of the
  *                         body)  cotix/_universal_shape.py:109-110, _convex_shapes.py:68-77
+ *   cotix_observe         the observation tensor of env.step()
+ *   cotix_render          env.draw(painter) via Painter callbacks  cotix/_viz.py:55-75,
+ *                         cotix/_robocup.py:140-150, cotix/_lunar_lander.py:220-225
+ *   cotix_check_state     class_invariant  cotix/_design_by_contract.py:80-107
  */
 #ifndef COTIX_AMD_H
 #define COTIX_AMD_H
@@ -74,7 +78,8 @@ enum {
 /* per-env error bits (eqx.error_if sites on the path) */
 enum {
   COTIX_ERR_CIRCLE_AABB_CCP = 1, /* cotix/_contacts.py:105-107 */
-  COTIX_ERR_AABB_INVALID = 2     /* AABB.of, cotix/_convex_shapes.py:74-75 (body-level broadphase) */
+  COTIX_ERR_AABB_INVALID = 2,    /* AABB.of, cotix/_convex_shapes.py:74-75 (body-level broadphase) */
+  COTIX_ERR_STATE_NONFINITE = 4  /* class_invariant, cotix/_design_by_contract.py:80-107: NaN/inf state */
 };
 
 /* Compile a scene (the collider's trace-time enumeration, cotix/_colliders.py:86-131).
@@ -162,6 +167,25 @@ int cotix_body_penetration(const cotix_scene* scene, const float* dyn, const flo
                            int body_a, int body_b, int* collides, float* pen, cotix_stream_t stream);
 int cotix_body_aabb(const cotix_scene* scene, const float* dyn, const float* geom, int geom_stride, int B, int body,
                     float* aabb, uint32_t* err, cotix_stream_t stream);
+
+/* Observation export: obs device f32 [B][n_bodies][6] (per env: px, py, vx,
+ * vy, angle, angular_velocity of every body) from dyn [n_bodies][6][B] -- the
+ * tensor env.step() returns and the multi-GPU path all-gathers. */
+int cotix_observe(const float* dyn, int n_bodies, int B, float* obs, cotix_stream_t stream);
+
+/* Render export (replaces the Painter host callbacks of env.draw(painter),
+ * cotix/_viz.py:55-75, cotix/_robocup.py:140-150, cotix/_lunar_lander.py:220-225):
+ * prims device f32 [B][cotix_render_count(scene)][4]; per part in scene order:
+ * Circle -> (cx, cy, r, NaN), AABB -> its 4 edges, Polygon -> its n edges
+ * (x0, y0, x1, y1), of the part transformed by its body (get_edges order). */
+int cotix_render_count(const cotix_scene* scene);
+int cotix_render(const cotix_scene* scene, const float* dyn, const float* geom, int geom_stride, int B, float* prims,
+                 cotix_stream_t stream);
+
+/* Contract check (class_invariant, cotix/_design_by_contract.py:80-107, on the
+ * world state): err[env] |= COTIX_ERR_STATE_NONFINITE when any dynamic state
+ * word of the env is NaN or infinite.  err device u32 [B]. */
+int cotix_check_state(const float* dyn, int n_bodies, int B, uint32_t* err, cotix_stream_t stream);
 
 /* Operator-level entry points (batched over n independent items). */
 int cotix_physics_euler(float* dyn, int n_bodies, int B, float dt, cotix_stream_t stream);

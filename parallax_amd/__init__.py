@@ -5,6 +5,7 @@ mirroring the reference's body/shape/operator surface.
 """
 from . import _ffi  # noqa: F401  (raises ImportError when the HIP library is missing)
 from . import random  # noqa: F401
+from . import contracts, render  # noqa: F401
 from .bodies import AnyBody, BodyView  # noqa: F401
 from .env import BatchedEnv  # noqa: F401
 from .physics import (ContactInfo, ExplicitEulerPhysics, RandomizedCollider, SimpleConstraintSolver,  # noqa: F401

@@ -17,6 +17,7 @@ STAGES_ROBOCUP = STAGE_EULER | STAGE_COLLIDER | STAGE_ADVANCE_KEY
 STAGES_LUNAR = STAGE_EULER | STAGE_GRAVITY | STAGE_COLLIDER | STAGE_LUNAR | STAGE_ADVANCE_KEY
 ERR_CIRCLE_AABB_CCP = 1
 ERR_AABB_INVALID = 2
+ERR_STATE_NONFINITE = 4
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -42,6 +43,10 @@ SIGNATURES = {
     "cotix_random_split": (_I, [_P, _I, _I, _P, _P]),
     "cotix_random_uniform": (_I, [_P, _I, _I, _F, _F, _P, _P]),
     "cotix_order_clockwise": (_I, [_P, _I, _I, _P]),
+    "cotix_observe": (_I, [_P, _I, _I, _P, _P]),
+    "cotix_render_count": (_I, [_P]),
+    "cotix_render": (_I, [_P, _P, _P, _I, _I, _P, _P]),
+    "cotix_check_state": (_I, [_P, _I, _I, _P, _P]),
     "cotix_last_error": (ctypes.c_char_p, []),
     "cotix_version": (ctypes.c_char_p, []),
 }

@@ -109,4 +109,75 @@ CX_DEV uint32_t body_aabb_env(const float* dyn, int B, const float* geom, int gs
   return e;
 }
 
+// ---------------------------------------------------------------------------
+// render export: the geometry of env.draw(painter) (cotix/_robocup.py:140-150,
+// cotix/_lunar_lander.py:220-225) as a per-env primitive table instead of
+// jax.debug.callback draws (cotix/_viz.py:55-75).  Per part, in scene order:
+//   Circle  -> 1 primitive  (cx, cy, r, NaN)          Circle.draw, :43-44
+//   AABB    -> 4 edge lines (x0, y0, x1, y1)          AABB.drawEdges / get_edges, :82-93,131-133
+//   Polygon -> n edge lines (v_k, v_{k-1})            Polygon.drawEdges / get_edges, :160-163,192-194
+// of the part transformed by its body (Polygon.transform re-sorts, :181-187).
+// Colours and draw order are static (host side, parallax_amd/render.py).
+constexpr int MAXRP = 32;  // parts per scene
+struct SceneParts {
+  int np;
+  int body[MAXRP], kind[MAXRP], nv[MAXRP], goff[MAXRP], poff[MAXRP];
+};
+CX_HD int render_prims(int kind, int nv) { return kind == cx::KIND_CIRCLE ? 1 : (kind == cx::KIND_AABB ? 4 : nv); }
+CX_DEV void render_part_env(const float* dyn, int B, const float* geom, int gstride, const SceneParts& sp, int p, int g,
+                            float* out) {
+  const float* lg = geom + (gstride ? (size_t)g * gstride : (size_t)0) + sp.goff[p];
+  float c, sn, px, py;
+  body_frame(dyn, B, sp.body[p], g, &c, &sn, &px, &py);
+  float* o = out + 4 * sp.poff[p];
+  if (sp.kind[p] == cx::KIND_CIRCLE) {  // Circle.transform: position + shift (:37-41)
+    o[0] = lg[1] + px;
+    o[1] = lg[2] + py;
+    o[2] = lg[0];
+    o[3] = cx::qnan();
+  } else if (sp.kind[p] == cx::KIND_AABB) {  // lower/upper + shift (:113-117); vs = up, (up.x, lo.y), lo, (lo.x, up.y)
+    const float lx = lg[0] + px, ly = lg[1] + py, ux = lg[2] + px, uy = lg[3] + py;
+    const float vx[4] = {ux, ux, lx, lx}, vy[4] = {uy, ly, ly, uy};
+    for (int k = 0; k < 4; ++k) {
+      o[4 * k + 0] = vx[k];
+      o[4 * k + 1] = vy[k];
+      o[4 * k + 2] = vx[(k + 1) & 3];
+      o[4 * k + 3] = vy[(k + 1) & 3];
+    }
+  } else {  // forward_vector of every vertex (the step kernel's phase T arithmetic), then order_clockwise
+    const int n = sp.nv[p];
+    cx::Poly q;
+    for (int k = 0; k < cx::MAXV; ++k) {
+      q.x[k] = 0.0f;
+      q.y[k] = 0.0f;
+      if (k < n) {
+        const float x = lg[2 * k], y = lg[2 * k + 1];
+        const float t0 = (c * x + (-sn) * y) + px * 1.0f, t1 = (sn * x + c * y) + py * 1.0f;
+        const float t2 = (0.0f * x + 0.0f * y) + 1.0f * 1.0f;
+        q.x[k] = t2 == 1.0f ? t0 : cx::qnan();
+        q.y[k] = t2 == 1.0f ? t1 : cx::qnan();
+      }
+    }
+    const cx::Poly v = cx::order_clockwise(q, n);
+    for (int k = 0; k < n; ++k) {
+      const int km = k == 0 ? n - 1 : k - 1;
+      o[4 * k + 0] = v.x[k];
+      o[4 * k + 1] = v.y[k];
+      o[4 * k + 2] = v.x[km];
+      o[4 * k + 3] = v.y[km];
+    }
+  }
+}
+
+// class_invariant (cotix/_design_by_contract.py:80-107) of a body's dynamic
+// state: every word finite ("detect jnp.nans or invalid values early")
+CX_DEV uint32_t state_check_env(const float* dyn, int n_bodies, int B, int g) {
+  bool bad = false;
+  for (int k = 0; k < 6 * n_bodies; ++k) {
+    const float v = dyn[(size_t)k * B + g];
+    bad = bad | cx::isn(v) | __builtin_isinf(v);
+  }
+  return bad ? (uint32_t)COTIX_ERR_STATE_NONFINITE : 0u;
+}
+
 }  // namespace cxk

@@ -148,6 +148,27 @@ __global__ void body_aabb_kernel(const float* dyn, int B, const float* geom, int
   const uint32_t e = cxk::body_aabb_env(dyn, B, geom, gstride, pa, g, out + 4 * (size_t)g);
   if (err && e) err[g] |= e;
 }
+__global__ void render_kernel(const float* dyn, int B, const float* geom, int gstride, cxk::SceneParts sp, int nprim,
+                              float* prims) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (env, part), part fastest
+  if (t >= (long long)B * sp.np) return;
+  const int g = (int)(t / sp.np), p = (int)(t % sp.np);
+  cxk::render_part_env(dyn, B, geom, gstride, sp, p, g, prims + (size_t)g * nprim * 4);
+}
+// SoA [nb*6][B] -> per env [B][nb*6]: each thread one output word; the
+// block's 256 outputs read 256 / (nb*6) envs of every state row
+__global__ void observe_kernel(const float* dyn, int nw, int B, float* obs) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)nw * B) return;
+  const int g = (int)(t / nw), k = (int)(t % nw);
+  obs[t] = dyn[(size_t)k * B + g];
+}
+__global__ void check_state_kernel(const float* dyn, int nb, int B, uint32_t* err) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= B) return;
+  const uint32_t e = cxk::state_check_env(dyn, nb, B, g);
+  if (e) err[g] |= e;
+}
 __global__ void resolve_kernel(int n, float* d1, const float* p1, float* d2, const float* p2, const float* con) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -501,6 +522,61 @@ int cotix_body_aabb(const cotix_scene* scene, const float* dyn, const float* geo
   hipLaunchKernelGGL(body_aabb_kernel, dim3((B + 63) / 64), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), dyn,
                      B, geom, geom_stride, pa, aabb, err);
   return hip_check(hipGetLastError(), "body_aabb_kernel launch");
+}
+
+static int scene_parts(const cotix_scene* scene, cxk::SceneParts* sp) {
+  const SceneDev& s = scene->host;
+  if (s.np > cxk::MAXRP) return fail("more than 32 parts in the scene");
+  sp->np = s.np;
+  int off = 0;
+  for (int p = 0; p < s.np; ++p) {
+    sp->body[p] = (int)s.hot[s.o_pbody + p];
+    sp->kind[p] = (int)s.hot[s.o_pkind + p];
+    sp->nv[p] = (int)s.hot[s.o_pn + p];
+    sp->goff[p] = (int)s.hot[s.o_pgoff + p];
+    sp->poff[p] = off;
+    off += cxk::render_prims(sp->kind[p], sp->nv[p]);
+  }
+  return off;
+}
+
+int cotix_render_count(const cotix_scene* scene) {
+  if (!scene) return fail("null scene");
+  cxk::SceneParts sp;
+  return scene_parts(scene, &sp);
+}
+
+int cotix_render(const cotix_scene* scene, const float* dyn, const float* geom, int geom_stride, int B, float* prims,
+                 cotix_stream_t stream) {
+  if (!scene || !dyn || !geom || !prims) return fail("null argument");
+  if (geom_stride != 0 && geom_stride < scene->host.G) return fail("geom_stride smaller than the scene geometry");
+  if (B <= 0) return B == 0 ? 0 : fail("negative size");
+  cxk::SceneParts sp;
+  const int nprim = scene_parts(scene, &sp);
+  if (nprim < 0) return -1;
+  const long long n = (long long)B * sp.np;
+  hipLaunchKernelGGL(render_kernel, dim3((unsigned)((n + 127) / 128)), dim3(128), 0,
+                     reinterpret_cast<hipStream_t>(stream), dyn, B, geom, geom_stride, sp, nprim, prims);
+  return hip_check(hipGetLastError(), "render_kernel launch");
+}
+
+int cotix_observe(const float* dyn, int n_bodies, int B, float* obs, cotix_stream_t stream) {
+  if (!dyn || !obs) return fail("null argument");
+  if (n_bodies < 0 || B < 0) return fail("negative size");
+  const long long n = (long long)n_bodies * 6 * B;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(observe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), dyn, n_bodies * 6, B, obs);
+  return hip_check(hipGetLastError(), "observe_kernel launch");
+}
+
+int cotix_check_state(const float* dyn, int n_bodies, int B, uint32_t* err, cotix_stream_t stream) {
+  if (!dyn || !err) return fail("null argument");
+  if (n_bodies < 0 || B < 0) return fail("negative size");
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(check_state_kernel, dim3((B + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     dyn, n_bodies, B, err);
+  return hip_check(hipGetLastError(), "check_state_kernel launch");
 }
 
 int cotix_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err, cotix_stream_t stream) {

@@ -37,9 +37,14 @@ class BatchedEnv:
             w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body)
         return self.observation()
 
-    def observation(self):
-        """[B, n_bodies, 6] view-copy of (px, py, vx, vy, angle, angular_velocity)."""
-        return self.world.dyn.permute(2, 0, 1)
+    def observation(self, out=None):
+        """f32 [B, n_bodies, 6] (px, py, vx, vy, angle, angular_velocity),
+        contiguous, from the device transpose kernel (cotix_observe)."""
+        return self.world.observe(out)
+
+    def draw(self, painter, env=0):
+        """The scenario's env.draw(painter) for env `env` (render export)."""
+        return self.scenario.draw(painter, env)
 
     @property
     def err(self):

@@ -93,6 +93,18 @@ class RoboCupEnv:
             self.world.dyn[4] = robocup_perturbation(batch, perturb_seed, device)
         self.dyn_reset = self.world.dyn.clone()
 
+    # field green, goals yellow / blue, ball red; white field outlines, no
+    # outline pass for the ball (cotix/_robocup.py:131-138)
+    colors = [(0, 180, 0)] * 2 + [(255, 255, 0), (0, 128, 255), (255, 0, 0)]
+    edge_colors = [(255, 255, 255)] * 2 + [(255, 255, 0), (0, 128, 255), None]
+
+    def draw(self, painter, env=0, prims=None):
+        """RoboCupEnv.draw(painter) (cotix/_robocup.py:140-150) for one env:
+        the geometry comes from the device render kernel."""
+        from . import render as R
+        cmds = R.commands_bodies(self.bodies, self.colors, self.edge_colors)
+        R.replay(painter, cmds, R.render(self.world) if prims is None else prims, env)
+
 
 # ---------------------------------------------------------------------------
 # LunarLander
@@ -182,3 +194,12 @@ class LunarLander:
         """LunarLander.step(): the joint constraints (cotix/_lunar_lander.py:145-218)."""
         self.world.lunar_constraints()
         return self
+
+    def draw(self, painter, env=0, prims=None):
+        """LunarLander.draw(painter) (cotix/_lunar_lander.py:220-225) for one
+        env: every body with the shapes' default colours, then the two red
+        landing-zone lines."""
+        from . import render as R
+        red = (255, 0, 0)
+        cmds = R.commands_bodies(self.bodies, extra_lines=[((-2, -1.8), (-2, -1.0), red), ((2, -1.8), (2, -1.0), red)])
+        R.replay(painter, cmds, R.render(self.world) if prims is None else prims, env)

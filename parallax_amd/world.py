@@ -162,6 +162,25 @@ class World:
         sep = (a[:, 3] <= b[:, 1]) | (a[:, 2] <= b[:, 0]) | (a[:, 1] >= b[:, 3]) | (a[:, 0] >= b[:, 2])
         return ~sep
 
+    def observe(self, out=None, dyn=None):
+        """f32 [B, n_bodies, 6] (px, py, vx, vy, angle, angular_velocity per
+        body) from the SoA state, one device transpose (cotix_observe)."""
+        d = self.dyn if dyn is None else dyn
+        nb = len(self.bodies)
+        if out is None:
+            out = torch.empty(self.B, nb, 6, dtype=torch.float32, device=self.device)
+        _ffi.check(_ffi.lib.cotix_observe(_ffi.ptr(d), nb, self.B, _ffi.ptr(out), _ffi.stream_ptr(self.device)),
+                   "cotix_observe")
+        return out
+
+    def check_state(self, err=None):
+        """class_invariant of the state (cotix/_design_by_contract.py:80-107):
+        err |= ERR_STATE_NONFINITE for every env with a NaN/inf state word."""
+        e = self.err if err is None else err
+        _ffi.check(_ffi.lib.cotix_check_state(_ffi.ptr(self.dyn), len(self.bodies), self.B, _ffi.ptr(e),
+                                              _ffi.stream_ptr(self.device)), "cotix_check_state")
+        return e
+
     def euler(self, dt):
         _ffi.check(_ffi.lib.cotix_physics_euler(_ffi.ptr(self.dyn), len(self.bodies), self.B, float(dt),
                                                 _ffi.stream_ptr(self.device)), "cotix_physics_euler")

@@ -257,3 +257,28 @@ extern "C" int emu_atan2(const float* y, const float* x, int n, float* out) {
   for (int i = 0; i < n; ++i) out[i] = cx::atan2_32(y[i], x[i]);
   return 0;
 }
+
+// render export and state check (host builds of cotix_render / cotix_check_state)
+extern "C" int emu_render(void* scene, const float* dyn, const float* geom, int gstride, int B, float* prims) {
+  const cxk::SceneDev& s = static_cast<EmuScene*>(scene)->s;
+  if (s.np > cxk::MAXRP) return -1;
+  cxk::SceneParts sp;
+  sp.np = s.np;
+  int off = 0;
+  for (int p = 0; p < s.np; ++p) {
+    sp.body[p] = (int)s.hot[s.o_pbody + p];
+    sp.kind[p] = (int)s.hot[s.o_pkind + p];
+    sp.nv[p] = (int)s.hot[s.o_pn + p];
+    sp.goff[p] = (int)s.hot[s.o_pgoff + p];
+    sp.poff[p] = off;
+    off += cxk::render_prims(sp.kind[p], sp.nv[p]);
+  }
+  if (prims == nullptr) return off;  // count query
+  for (int g = 0; g < B; ++g)
+    for (int p = 0; p < s.np; ++p) cxk::render_part_env(dyn, B, geom, gstride, sp, p, g, prims + (size_t)g * off * 4);
+  return off;
+}
+extern "C" int emu_check_state(const float* dyn, int nb, int B, uint32_t* err) {
+  for (int g = 0; g < B; ++g) err[g] |= cxk::state_check_env(dyn, nb, B, g);
+  return 0;
+}

@@ -556,3 +556,62 @@ def test_body_operators_vs_oracle(torch_cuda):
             # (no "narrowphase implies broadphase" check: through the reference's
             # wrap_local_support a rotated body's support is not its true extreme
             # point, so neither operator bounds the other for rotated bodies)
+
+
+# ---------------------------------------------------------------------------
+# observation / render export and the state contract
+# ---------------------------------------------------------------------------
+def test_observe_and_check_state(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    env = pa.BatchedEnv(pa.RoboCupEnv(batch=1000, device="cuda", perturb=True), autoreset=True)
+    env.reset()
+    env.step(7)
+    obs = env.observation()
+    torch.cuda.synchronize()
+    assert obs.is_contiguous() and tuple(obs.shape) == (1000, 5, 6)
+    assert same_f32(obs.cpu().numpy(), env.world.dyn.permute(2, 0, 1).cpu().numpy())
+    w = env.world
+    w.err.zero_()
+    w.dyn[1, 3, 17] = float("nan")
+    w.dyn[4, 0, 999] = float("inf")
+    w.err[5] = 1
+    w.check_state()
+    want = np.zeros(1000, np.int32)
+    want[5] = 1
+    want[[17, 999]] |= pa._ffi.ERR_STATE_NONFINITE
+    assert np.array_equal(w.err.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("scene", ["robocup", "lunar"])
+def test_render_draw_vs_reference(torch_cuda, scene):
+    """env.draw(painter) through the render kernel == the reference's Painter
+    call sequence (oracle restatement), coordinates bit for bit."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import parallax_amd.render as R
+    from cotix_oracle import physics as P
+    from cotix_oracle import render as OR
+    from cotix_oracle import prng
+    import test_render_contracts_cpu as T
+    if scene == "robocup":
+        sc = pa.RoboCupEnv(batch=64, device="cuda", perturb=True)
+        sc.world.step(5, 1e-2, sc.stages)
+        mk = lambda e: P.robocup_bodies()  # noqa: E731
+        draw = OR.robocup_draw
+    else:
+        keys = pa.random.split(pa.random.PRNGKey(0, "cuda"), 64).contiguous()
+        sc = pa.LunarLander(key=keys, batch=64, device="cuda")
+        sc.world.dyn[:3, 4] += torch.linspace(-1.0, 1.0, 64, device="cuda")  # rotated landers
+        tk = prng.split(prng.PRNGKey(0), 64)
+        mk = lambda e: P.lunar_lander_bodies(tk[e])  # noqa: E731
+        draw = OR.lunar_lander_draw
+    prims = R.render(sc.world)
+    dyn = sc.world.dyn.cpu().numpy()
+    for e in (0, 1, 31, 63):
+        bodies = mk(e)
+        for i, b in enumerate(bodies):
+            b.set_dyn(dyn[i, :, e])
+        p = R.RecordingPainter()
+        sc.draw(p, env=e, prims=prims)
+        T._same_calls(p.calls, draw(bodies))

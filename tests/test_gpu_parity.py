@@ -571,6 +571,7 @@ def test_observe_and_check_state(torch_cuda):
     torch.cuda.synchronize()
     assert obs.is_contiguous() and tuple(obs.shape) == (1000, 5, 6)
     assert same_f32(obs.cpu().numpy(), env.world.dyn.permute(2, 0, 1).cpu().numpy())
+    env.reset()  # a finite state (stepped RoboCup states hold NaN velocities: the reference's error_if trips)
     w = env.world
     w.err.zero_()
     w.dyn[1, 3, 17] = float("nan")

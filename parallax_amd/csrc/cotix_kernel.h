@@ -39,7 +39,7 @@ constexpr int WAVE = 64;
 // in every other build
 #ifdef COTIX_STATS
 struct Stats {
-  unsigned long long wave_steps, active_items, rounds, resolutions, f_items, b_items;
+  unsigned long long wave_steps, active_items, rounds, resolutions, f_items, b_items, draws, valid_draws, r1_left, lvl_env, lvl_wave, e1_slots;
 };
 inline Stats g_stats{};
 #define CXK_STAT(f, v) (cxk::g_stats.f += (unsigned long long)(v))
@@ -844,7 +844,9 @@ CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par, int kso) {
         const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
         const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
         const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
+        CXK_STAT(draws, 1);
         if (!(isn(cpx) || isn(cpy))) {  // a NaN candidate never writes
+          CXK_STAT(valid_draws, 1);
           const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
           const key2 k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
           const key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);   // :254
@@ -1134,6 +1136,9 @@ CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e) {
   }
 }
 
+#ifdef COTIX_STATS
+CX_DEV int L_rp_(const Ctx& c) { return c.L.rp; }
+#endif
 // REC (backward re-play only): record, per resolution, whether the impulses
 // were applied and the pre-resolution velocities of the two bodies.
 template <int EW, bool REC = false>
@@ -1145,6 +1150,26 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g >= a.B) continue;
+#ifdef COTIX_STATS
+    if (a.stages & COTIX_STAGE_COLLIDER) {  // dependency levels of the sequential pass (tools/collider_stats.py)
+      int last[MAXB] = {0}, L = 0;
+      for (int i = 0; i < nb; ++i) {
+        const uint32_t j = t.w(L_rp_(c) + RP_W * i + RP_J, e);
+        if (j == RP_NONE) continue;
+        const int lv = (last[i] > last[j] ? last[i] : last[j]) + 1;
+        last[i] = last[j] = lv;
+        L = lv > L ? lv : L;
+      }
+      static int wmax = 0, wslots = 0;
+      static uint32_t wmask = 0;
+      if (e == 0) { wmax = 0; wmask = 0; }
+      wmax = L > wmax ? L : wmax;
+      for (int i = 0; i < nb; ++i) if (t.w(L_rp_(c) + RP_W * i + RP_J, e) != RP_NONE) wmask |= 1u << i;
+      CXK_STAT(lvl_env, L);
+      if (e == EW - 1) { CXK_STAT(lvl_wave, wmax); CXK_STAT(e1_slots, __builtin_popcount(wmask)); }
+      (void)wslots;
+    }
+#endif
     if (a.stages & COTIX_STAGE_COLLIDER) {
       if (sc.rcp_all) {
         switch (nb) {
@@ -1418,6 +1443,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       if (t.ws[WS_N] == 0u) break;  // uniform: read after the phase barrier
       CXK_STAT(rounds, 1);
       if (par == 0) CXK_STAT(active_items, t.ws[WS_N]);
+      if (par == 1) CXK_STAT(r1_left, t.ws[WS_N]);
       run(PH_C2, [&](int l) { ph_M2<EW>(c, t, l, par); });
     }
   } else if (!(a.dbg_skip & 4) && c.nl > 0) {

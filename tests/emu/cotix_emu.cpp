@@ -243,8 +243,14 @@ extern "C" int emu_stats(unsigned long long* out) {
   out[3] = cxk::g_stats.resolutions;
   out[4] = cxk::g_stats.f_items;
   out[5] = cxk::g_stats.b_items;
+  out[6] = cxk::g_stats.draws;
+  out[7] = cxk::g_stats.valid_draws;
+  out[8] = cxk::g_stats.r1_left;
+  out[9] = cxk::g_stats.lvl_env;
+  out[10] = cxk::g_stats.lvl_wave;
+  out[11] = cxk::g_stats.e1_slots;
   cxk::g_stats = cxk::Stats{};
-  return 6;
+  return 12;
 }
 #endif
 

@@ -59,7 +59,7 @@ def main():
     keys = np.ascontiguousarray(np.array(prng.split(prng.PRNGKey(3), B), np.uint32))
     dyn_reset = dyn.copy()
     err = np.zeros(B, np.uint32)
-    out = (ctypes.c_ulonglong * 8)()
+    out = (ctypes.c_ulonglong * 16)()
     lib.emu_stats(out)
     emu.step(lib, h, dyn, keys, err, geom, gstride, a.steps, stages, E=a.ew, dyn_reset=dyn_reset)
     lib.emu_stats(out)
@@ -67,7 +67,10 @@ def main():
     print({"scenario": a.scenario, "envs": B, "steps": a.steps, "ew": a.ew,
            "active_items_per_wave_step": out[1] / ws, "rounds_per_wave_step": out[2] / ws,
            "resolutions_per_env_step": out[3] / (B * a.steps), "f_items_per_wave_step": out[4] / ws,
-           "b_items_per_wave_step": out[5] / ws})
+           "b_items_per_wave_step": out[5] / ws, "valid_draw_frac": out[7] / max(out[6], 1),
+           "items_left_after_round1_per_wave_step": out[8] / ws,
+           "resolution_levels_per_env_step": out[9] / (B * a.steps), "resolution_levels_per_wave_step": out[10] / ws,
+           "sequential_slots_per_wave_step": out[11] / ws})
 
 
 if __name__ == "__main__":

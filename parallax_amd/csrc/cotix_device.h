@@ -521,12 +521,12 @@ CX_DEV bool gjk(const SA& a, const SB& b, v2 d0, v2* simplex) {
   v2 s0 = minkowski(a, b, d0);
   v2 s1 = minkowski(a, b, neg(s0));
   v2 dir = fnormal(sub(s1, s0));
-  if (dot(dir, neg(s1)) > 0.0f) {
-    v2 t = s0;
-    s0 = s1;
-    s1 = t;
-  } else {
-    dir = neg(dir);
+  {  // orientation fix (:44-53) as selects
+    const bool sw = dot(dir, neg(s1)) > 0.0f;
+    const v2 t0 = s0;
+    s0 = sw ? s1 : s0;
+    s1 = sw ? t0 : s1;
+    dir = sw ? dir : neg(dir);
   }
   v2 s2 = minkowski(a, b, dir);
   for (int step = 0; step < 32; ++step) {
@@ -536,13 +536,10 @@ CX_DEV bool gjk(const SA& a, const SB& b, v2 d0, v2* simplex) {
     if (c1 || (c2 && c3)) break;
     v2 c = s2;
     v2 acn = fnormal(sub(c, s0)), cbn = fnormal(sub(s1, c));
-    if (dot(acn, neg(c)) >= 0.0f) {
-      s1 = c;
-      dir = acn;
-    } else {
-      s0 = c;
-      dir = cbn;
-    }
+    const bool ac = dot(acn, neg(c)) >= 0.0f;
+    s1 = ac ? c : s1;
+    s0 = ac ? s0 : c;
+    dir = ac ? acn : cbn;
     s2 = minkowski(a, b, dir);
   }
   v2 z = v2{0.0f, 0.0f};
@@ -566,28 +563,28 @@ CX_DEV bool gjk(const SA& a, const SB& b, v2 d0, v2* simplex) {
 // Distances are cached per edge (only the two rewritten edges change per
 // iteration); the reference recomputes all of them -- same values.
 // ---------------------------------------------------------------------------
+// (both written as flat selects: every path is evaluated and the reference's
+// one is selected -- same values, no divergent branches in the GJK/EPA loops)
 CX_DEV v2 closest_on_edge_to_origin(v2 a, v2 b) {  // :156-166, point = 0
   v2 p = v2{0.0f, 0.0f};
   float len = sumsq(sub(a, b));
-  if (len == 0.0f) return sub(p, a);
   float t = dot(sub(p, b), sub(a, b)) / len;
   t = clip_(t, 0.0f, 1.0f);
   v2 proj = add(b, scl(sub(a, b), t));
-  return sub(p, proj);
+  const v2 r = sub(p, proj), r0 = sub(p, a);
+  return len == 0.0f ? r0 : r;
 }
 CX_DEV float edge_dist(v2 a, v2 b) {  // distance_to_origin :137-154,168-169
-  if (a.x == 0.0f && a.y == 0.0f && b.x == 0.0f && b.y == 0.0f) {
-    float i = finf();
-    return i * i + i * i;
-  }
+  const bool zero = a.x == 0.0f && a.y == 0.0f && b.x == 0.0f && b.y == 0.0f;
+  const float i = finf();
   v2 p = v2{0.0f, 0.0f};
   float len = sumsq(sub(a, b));
   float t = dot(sub(p, b), sub(a, b)) / len;
   t = clip_(t, 0.0f, 1.0f);
   v2 proj = add(b, scl(sub(a, b), t));
   v2 disp = sub(p, proj);
-  if (len == 0.0f) disp = neg(a);
-  return sumsq(disp);
+  disp = len == 0.0f ? neg(a) : disp;
+  return zero ? i * i + i * i : sumsq(disp);
 }
 
 // EPA edge storage: registers (operator kernels, host; dynamic indices as
@@ -652,20 +649,18 @@ CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters, ES& es) {
   const v2 sim[3] = {simplex[0], simplex[1], simplex[2]};
 #pragma unroll
   for (int k = 0; k < NE; ++k) dist[k] = (k < 3) ? edge_dist(sim[k], sim[(k + 1) % 3]) : ((k < ne) ? edge_dist(z, z) : finf());
-  auto argmin_d = [&]() {
-    int nanidx = -1, b = 0;
+  auto argmin_d = [&]() {  // first NaN, else first minimum, over the ne live edges (selects)
+    int nanidx = NE, b = 0;
     float bv = dist[0];
 #pragma unroll
-    for (int k = 0; k < NE; ++k) {
-      if (k < ne) {
-        if (nanidx < 0 && isn(dist[k])) nanidx = k;
-        if (k > 0 && dist[k] < bv) {
-          bv = dist[k];
-          b = k;
-        }
-      }
+    for (int k = 1; k < NE; ++k) {
+      const bool lt = k < ne && dist[k] < bv;
+      bv = lt ? dist[k] : bv;
+      b = lt ? k : b;
     }
-    return nanidx >= 0 ? nanidx : b;
+#pragma unroll
+    for (int k = NE - 1; k >= 0; --k) nanidx = (k < ne && isn(dist[k])) ? k : nanidx;
+    return nanidx < NE ? nanidx : b;
   };
   int bei = argmin_d();
   v2 best0 = es.g0(bei), best1 = es.g1(bei);

@@ -52,18 +52,21 @@ inline Stats g_stats{};
 // the scalar header (offsets, counts) travels in the kernel arguments, so
 // phases read it from registers, never from global memory
 struct SceneHdr {
-  int nb, np, nc, nl, nt, G, W, ncand;  // bodies, parts, contacts, cells, types, geom/world floats, candidates
-  float d0x, d0y;                       // GJK start direction (constant)
-  int o_par, o_rcp, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
-  int o_ci, o_cj, o_cbeg, o_ccnt, o_tn1, o_tn2, o_cand;
-  int o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts
-  int o_cmask;  // per cell nmw words: bitmask of the cell's distinct contacts
-  int nmw;      // contact-mask words = ceil(nc / 32)
-  int poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
-  int rcp_all;  // 1: every mass and inertia has an exact reciprocal (o_rcp): resolutions multiply
-  int rcp_mask; // bit b: body b's mass and inertia have exact reciprocals (bodies < 32)
-  int fnset;    // FNS_* bits of the contact functions the scene uses (kernel instantiation)
-  int nhot;
+  // 16-bit fields: the header lives in scalar registers for the whole launch
+  // (every table offset is < MAXHOT, every count < 4096), so packing halves
+  // its register footprint
+  uint16_t nb, np, nc, nl, nt, G, W, ncand;  // bodies, parts, contacts, cells, types, geom/world floats, candidates
+  float d0x, d0y;                            // GJK start direction (constant)
+  uint16_t o_par, o_rcp, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
+  uint16_t o_ci, o_cj, o_cbeg, o_ccnt, o_tn1, o_tn2, o_cand;
+  uint16_t o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts
+  uint16_t o_cmask;  // per cell nmw words: bitmask of the cell's distinct contacts
+  uint16_t nmw;      // contact-mask words = ceil(nc / 32)
+  uint16_t poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
+  uint16_t rcp_all;  // 1: every mass and inertia has an exact reciprocal (o_rcp): resolutions multiply
+  uint16_t fnset;    // FNS_* bits of the contact functions the scene uses (kernel instantiation)
+  uint16_t nhot;
+  uint32_t rcp_mask; // bit b: body b's mass and inertia have exact reciprocals (bodies < 32)
 };
 struct SceneDev : SceneHdr {
   uint32_t hot[MAXHOT];
@@ -896,43 +899,43 @@ CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
 // computed by the phase-D item (body i, env e) right after its choice j)
 template <int EW, bool RCP>
 CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid) {
+  // branch-free: the operands are computed from clamped indices for every
+  // item and the partner is set only for a real resolution (the inactive
+  // items' operands are never read: E1 skips RP_NONE)
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
   const int ro = L.rp + RP_W * i;
-  uint32_t jj = RP_NONE;
-  if (!(j == i || j < 0 || j >= c.nb) && cid >= 0) {
-    const int co = L.con + 4 * cid;
-    const v2 cp = v2{t.f(co + 2, e), t.f(co + 3, e)};
-    if (!vnan(cp)) {  // resolve_collision returns unchanged bodies on a NaN contact point
-      const int oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
-      const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
-      const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
-      const Params pj = load_par(t.tb, sc.o_par + 4 * j);
-      const Rcp qj = load_rcp(t.tb, sc.o_rcp + 2 * j);
-      const ResPre p = resolve_pre<RCP>(bi, load_par(t.tb, sc.o_par + 4 * i), load_rcp(t.tb, sc.o_rcp + 2 * i), bj, pj,
-                                        qj, v2{t.f(co, e), t.f(co + 1, e)}, cp);
-      t.f(ro + RP_NX, e) = p.n.x;
-      t.f(ro + RP_NY, e) = p.n.y;
-      t.f(ro + RP_R1X, e) = p.r1.x;
-      t.f(ro + RP_R1Y, e) = p.r1.y;
-      t.f(ro + RP_R2X, e) = p.r2.x;
-      t.f(ro + RP_R2Y, e) = p.r2.y;
-      t.f(ro + RP_PX, e) = p.pen.x;
-      t.f(ro + RP_PY, e) = p.pen.y;
-      t.f(ro + RP_DEN, e) = p.den;
-      t.f(ro + RP_PT, e) = p.pterm;
-      t.f(ro + RP_NE, e) = p.ne;
-      t.f(ro + RP_MU, e) = p.mu;
-      t.f(ro + RP_MJ, e) = pj.mass;
-      t.f(ro + RP_IJ, e) = pj.inertia;
-      t.f(ro + RP_QMJ, e) = qj.m;
-      t.f(ro + RP_QIJ, e) = qj.i;
-      jj = (uint32_t)j;
-      CXK_STAT(resolutions, 1);
-    }
-  }
-  t.w(ro + RP_J, e) = jj;
+  const bool pair = !(j == i || j < 0 || j >= c.nb) && cid >= 0;
+  const int jc = pair ? j : i, co = L.con + 4 * (pair ? cid : 0);
+  const v2 cp = v2{t.f(co + 2, e), t.f(co + 3, e)};
+  const int oi = L.dyn + 6 * i, oj = L.dyn + 6 * jc;
+  const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
+  const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
+  const Params pj = load_par(t.tb, sc.o_par + 4 * jc);
+  const Rcp qj = load_rcp(t.tb, sc.o_rcp + 2 * jc);
+  const ResPre p = resolve_pre<RCP>(bi, load_par(t.tb, sc.o_par + 4 * i), load_rcp(t.tb, sc.o_rcp + 2 * i), bj, pj, qj,
+                                    v2{t.f(co, e), t.f(co + 1, e)}, cp);
+  t.f(ro + RP_NX, e) = p.n.x;
+  t.f(ro + RP_NY, e) = p.n.y;
+  t.f(ro + RP_R1X, e) = p.r1.x;
+  t.f(ro + RP_R1Y, e) = p.r1.y;
+  t.f(ro + RP_R2X, e) = p.r2.x;
+  t.f(ro + RP_R2Y, e) = p.r2.y;
+  t.f(ro + RP_PX, e) = p.pen.x;
+  t.f(ro + RP_PY, e) = p.pen.y;
+  t.f(ro + RP_DEN, e) = p.den;
+  t.f(ro + RP_PT, e) = p.pterm;
+  t.f(ro + RP_NE, e) = p.ne;
+  t.f(ro + RP_MU, e) = p.mu;
+  t.f(ro + RP_MJ, e) = pj.mass;
+  t.f(ro + RP_IJ, e) = pj.inertia;
+  t.f(ro + RP_QMJ, e) = qj.m;
+  t.f(ro + RP_QIJ, e) = qj.i;
+  // resolve_collision returns unchanged bodies on a NaN contact point
+  const bool res = pair && !vnan(cp);
+  if (res) CXK_STAT(resolutions, 1);
+  t.w(ro + RP_J, e) = res ? (uint32_t)j : RP_NONE;
 }
 
 // one (body i, env) item of phase D; NB > 0: the body count at compile time
@@ -955,10 +958,10 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
     }
   }
   int ch = i;
-  if (cnt > 0) {
+  {  // evaluated for every item (branch-free); kept only when cnt > 0
     float p[MB], cs[MB];
     // p = notnan / count (:280-283): 1/count or 0/count == +0 (count > 0)
-    const float inv = 1.0f / (float)cnt;
+    const float inv = 1.0f / (float)(cnt > 0 ? cnt : 1);
 #pragma unroll
     for (int j = 0; j < MB; ++j) p[j] = ((good >> j) & 1u) ? inv : 0.0f;
     if (NB > 0)
@@ -978,10 +981,10 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
     for (int j = 1; j < MB; ++j)
       if (j < nb) last = cs[j];
     float r = last * (1.0f - u);
-    ch = nb;
+    int cj = nb;
 #pragma unroll
-    for (int j = MB - 1; j >= 0; --j)
-      if (j < nb && !(cs[j] < r)) ch = j;  // first j with r <= cumsum[j]
+    for (int j = MB - 1; j >= 0; --j) cj = (j < nb && !(cs[j] < r)) ? j : cj;  // first j with r <= cumsum[j]
+    ch = cnt > 0 ? cj : i;
   }
   t.w(L.ch + i, e) = (uint32_t)ch;
   int cid = -1;  // all_contacts[i, ch], picked from the loaded row

@@ -165,8 +165,8 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   s.nl = (int)cells.size();
   // pack the hot tables (word offsets into s.hot, copied to LDS per launch)
   std::vector<uint32_t> hot;
-  auto put = [&](int& off, const std::vector<int>& v) {
-    off = (int)hot.size();
+  auto put = [&](uint16_t& off, const std::vector<int>& v) {
+    off = (uint16_t)hot.size();
     for (int x : v) hot.push_back((uint32_t)x);
   };
   {

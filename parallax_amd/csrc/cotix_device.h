@@ -332,7 +332,10 @@ CX_DEV bool circle_contains(const Shape& c, v2 p) {  // :28-29
 CX_DEV bool aabb_contains(const Shape& a, v2 p) {  // :105-106
   return (p.x >= a.d(0) - 1e-6f) && (p.y >= a.d(1) - 1e-6f) && (p.x <= a.d(2) + 1e-6f) && (p.y <= a.d(3) + 1e-6f);
 }
-CX_DEV float fsign(float x) { return isn(x) ? x : (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x)); }
+CX_DEV float fsign(float x) {  // jnp.sign: NaN and +-0 map to themselves (flat selects)
+  float r = x > 0.0f ? 1.0f : x;
+  return x < 0.0f ? -1.0f : r;
+}
 CX_DEV bool poly_contains(const Shape& s, v2 p) {  // :168-175, edge k = (v_k, v_{k-1})
   float s0 = 0.0f;
   bool ok = true;
@@ -366,16 +369,23 @@ CX_DEV Poly order_clockwise(const Poly& q, int n) {
     }
   const float fn = (float)n;
   const float mx = sx / fn, my = sy / fn;
-  float ang[MAXV];
+  // sort keys: atan2 lies in [-pi, pi] or is NaN, so NaN -> 4 (after every
+  // angle, all NaN equal) makes sort_lt(a, b) == key(a) < key(b) (-0 == +0
+  // under <): one compare per pair
+  float key[MAXV];
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) ang[k] = k < n ? atan2_32(q.y[k] - my, q.x[k] - mx) : 0.0f;
+  for (int k = 0; k < MAXV; ++k) {
+    const float a = k < n ? atan2_32(q.y[k] - my, q.x[k] - mx) : 0.0f;
+    key[k] = isn(a) ? 4.0f : a;
+  }
+  // stable rank: j before k if key_j < key_k, or j < k and not key_k < key_j
   int rank[MAXV];
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     int r = 0;
 #pragma unroll
     for (int j = 0; j < MAXV; ++j)
-      if (j != k && j < n) r += (sort_lt(ang[j], ang[k]) || (j < k && !sort_lt(ang[k], ang[j]))) ? 1 : 0;
+      if (j != k && j < n) r += (j < k ? !(key[k] < key[j]) : (key[j] < key[k])) ? 1 : 0;
     rank[k] = r;
   }
   Poly out;

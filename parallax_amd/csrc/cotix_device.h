@@ -911,13 +911,16 @@ template <class VFA, class VFB>
 CX_DEV v2 cfe_term(const Shape& A, const Shape& B, int s, VFA va, VFB vb) {
   const int na = cvx_count(A), nb = cvx_count(B);
   const v2 nanv = v2{qnan(), qnan()};
-  if (s < na) {
-    const v2 v = cvx_vert_d(A, s, va);
-    return shape_contains(B, v) ? v : nanv;
-  }
-  if (s < na + nb) {
-    const v2 v = cvx_vert_d(B, s - na, vb);
-    return shape_contains(A, v) ? v : nanv;
+  if (s < na + nb) {  // a vertex of A tested in B, or of B in A: one containment test on the selected pair
+    const bool fa = s < na;
+    const v2 vA = cvx_vert_d(A, fa ? s : 0, va), vB = cvx_vert_d(B, fa ? 0 : s - na, vb);
+    const v2 v = fa ? vA : vB;
+    Shape S;
+    S.kind = fa ? B.kind : A.kind;
+    S.n = fa ? B.n : A.n;
+#pragma unroll
+    for (int q = 0; q < 2 * MAXV; ++q) S.w[q] = fa ? B.w[q] : A.w[q];
+    return shape_contains(S, v) ? v : nanv;
   }
   const int q = s - na - nb, jb = q / na, ia = q - jb * na;
   v2 a0, a1, b0, b1;

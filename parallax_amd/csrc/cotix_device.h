@@ -296,15 +296,28 @@ CX_DEV v2 support(const Shape& s, v2 d) {
   // (a guarded/branchy form of this loop was miscompiled by hipcc 7.2 at -O2+).
   float bv = s.w[0] * d.x + s.w[1] * d.y;
   float bx = s.w[0], by = s.w[1];
-#pragma unroll
-  for (int k = 1; k < MAXV; ++k) {
+  auto step = [&](int k) {
     const float x = s.w[2 * k], y = s.w[2 * k + 1];
     const float t = x * d.x + y * d.y;
     const bool take = (k < s.n) && !isn(bv) && (isn(t) || t > bv);
     bv = take ? t : bv;
     bx = take ? x : bx;
     by = take ? y : by;
+  };
+  // vertices 1..3 always (n >= 3); 4..5 and 6..7 only when some lane of the
+  // wave has that many (the select chain itself stays branch-free)
+  step(1);
+  step(2);
+  step(3);
+  if (s.n > 4) {
+    step(4);
+    step(5);
   }
+  if (s.n > 6) {
+    step(6);
+    step(7);
+  }
+  static_assert(MAXV == 8, "support() unrolls for MAXV == 8");
   return v2{bx, by};
 }
 // a part inside its body's frame, as UniversalShape.wrap_local_support sees it
@@ -374,10 +387,25 @@ CX_DEV Poly order_clockwise(const Poly& q, int n) {
   // under <): one compare per pair
   float key[MAXV];
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
+  for (int k = 0; k < MAXV; ++k) key[k] = 0.0f;
+  auto angle = [&](int k) {
     const float a = k < n ? atan2_32(q.y[k] - my, q.x[k] - mx) : 0.0f;
     key[k] = isn(a) ? 4.0f : a;
+  };
+  // vertices 4..5 / 6..7 only when some lane of the wave has that many
+  angle(0);
+  angle(1);
+  angle(2);
+  angle(3);
+  if (n > 4) {
+    angle(4);
+    angle(5);
   }
+  if (n > 6) {
+    angle(6);
+    angle(7);
+  }
+  static_assert(MAXV == 8, "order_clockwise unrolls for MAXV == 8");
   // stable rank: j before k if key_j < key_k, or j < k and not key_k < key_j
   int rank[MAXV];
 #pragma unroll

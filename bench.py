@@ -111,7 +111,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world_size > 1:
+    # COTIX_BENCH_FORCE_DIST=1: the collective path at world size 1 too (tests the RCCL code on one GPU)
+    if world_size > 1 or os.environ.get("COTIX_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -131,8 +132,14 @@ def main():
         bytes_per_env = 4 * 6 * 4 * 2 + 16 + 8 + 84 * 4
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
-    obs_all = torch.empty(world_size * B, len(scen.bodies), 6, device=dev) if dist else None
-    obs_local = torch.empty(B, len(scen.bodies), 6, device=dev) if dist else None
+    # observation all-gather, double-buffered and asynchronous: the RCCL
+    # collective of launch i runs on its own stream while launch i+1 computes;
+    # a buffer is rewritten only after the collective that read it is done
+    nbody = len(scen.bodies)
+    obs_all = [torch.empty(world_size * B, nbody, 6, device=dev) for _ in range(2)] if dist else None
+    obs_local = [torch.empty(B, nbody, 6, device=dev) for _ in range(2)] if dist else None
+    pending = [None, None]
+    launches = [0]
 
     # HIP events around every step-kernel launch, on the stream it runs on
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
@@ -144,10 +151,22 @@ def main():
         if i is not None:
             evs[i][1].record()
         if dist is not None:  # north star: RCCL all-gather of the observation tensor
-            dist.all_gather_into_tensor(obs_all, env.observation(obs_local))
+            k = launches[0] % 2
+            launches[0] += 1
+            if pending[k] is not None:
+                pending[k].wait()  # the current stream waits for the collective that read buffer k
+            env.observation(obs_local[k])
+            pending[k] = dist.all_gather_into_tensor(obs_all[k], obs_local[k], async_op=True)
+
+    def drain():
+        for k in range(2):
+            if pending[k] is not None:
+                pending[k].wait()
+                pending[k] = None
 
     for _ in range(a.warmup):
         one_step()
+    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -155,6 +174,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         one_step(i)
+    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -273,6 +293,7 @@ def main_grad(a):
 
     for _ in range(a.warmup):
         one_step()
+    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -280,6 +301,7 @@ def main_grad(a):
     t0 = time.perf_counter()
     for i in range(a.steps):
         one_step(i)
+    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

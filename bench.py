@@ -293,7 +293,6 @@ def main_grad(a):
 
     for _ in range(a.warmup):
         one_step()
-    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -301,7 +300,6 @@ def main_grad(a):
     t0 = time.perf_counter()
     for i in range(a.steps):
         one_step(i)
-    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

@@ -616,3 +616,76 @@ def test_render_draw_vs_reference(torch_cuda, scene):
         p = R.RecordingPainter()
         sc.draw(p, env=e, prims=prims)
         T._same_calls(p.calls, draw(bodies))
+
+
+# ---------------------------------------------------------------------------
+# ragged batches: B not a multiple of the envs-per-wave tile (4), a wave
+# whose tail lanes hold no env, and B = 0 / negative sizes through the C-ABI
+# ---------------------------------------------------------------------------
+def _subset_check(torch, make, big, stages, T, sizes):
+    """Each env's result is independent of its batch: a world of
+    the first b envs must reproduce those envs of the big run bit for bit,
+    and must not write past B (keys/err live in larger sentinel buffers)."""
+    init = big.dyn.clone()
+    keys0 = big.keys.clone()
+    big.step(T, 1e-2, stages)
+    torch.cuda.synchronize()
+    for b in sizes:
+        w = make(b)
+        w.dyn.copy_(init[:, :, :b])
+        kbuf = torch.full((b + 8, 2), 0x5A5A5A5A, dtype=keys0.dtype, device="cuda")
+        kbuf[:b] = keys0[:b]
+        ebuf = torch.full((b + 8,), 0x5A5A5A5A, dtype=big.err.dtype, device="cuda")
+        ebuf[:b] = 0
+        dyn = w.dyn.clone()
+        w.step_state(dyn, kbuf[:b], ebuf[:b], T, 1e-2, stages)
+        torch.cuda.synchronize()
+        assert same_f32(dyn.cpu().numpy(), big.dyn[:, :, :b].cpu().numpy()), "B=%d" % b
+        assert torch.equal(kbuf[:b], big.keys[:b]) and torch.equal(ebuf[:b], big.err[:b]), "B=%d" % b
+        assert bool((kbuf[b:] == 0x5A5A5A5A).all()) and bool((ebuf[b:] == 0x5A5A5A5A).all()), "B=%d wrote past B" % b
+
+
+@pytest.mark.parametrize("ew", ["1", "2", "4", "8"])
+def test_ragged_batches_robocup(torch_cuda, monkeypatch, ew):
+    torch = torch_cuda
+    monkeypatch.setenv("COTIX_ENVS_PER_WAVE", ew)  # read by the library at every launch
+    import parallax_amd as pa
+    env = pa.RoboCupEnv(batch=64, device="cuda", perturb=True)
+    keys = env.world.keys.clone()
+    _subset_check(torch, lambda b: pa.RoboCupEnv(batch=b, device="cuda", keys=keys[:b].clone()).world,
+                  env.world, env.stages, 8, [1, 3, 5, 13, 63])
+
+
+def test_ragged_batches_lunar(torch_cuda):
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import prng
+    tkeys = torch.tensor(u32_to_i32(prng.split(prng.PRNGKey(0), 64)), device="cuda")
+    ll = pa.LunarLander(key=tkeys, batch=64, device="cuda")
+    for i in range(3):  # drop every other lander onto the ground so GJK/EPA contacts fire
+        ll.world.dyn[i, 1, ::2] -= 6.3
+        ll.world.dyn[i, 3, ::2] = -0.3
+    ck = ll.world.keys.clone()
+    _subset_check(torch, lambda b: pa.LunarLander(key=tkeys[:b].clone(), batch=b, device="cuda",
+                                                  collider_keys=ck[:b].clone()).world,
+                  ll.world, ll.stages, 4, [1, 2, 7, 33])
+
+
+def test_empty_and_negative_sizes(torch_cuda):
+    torch = torch_cuda
+    import ctypes
+    import parallax_amd as pa
+    from parallax_amd import _ffi
+    env = pa.RoboCupEnv(batch=4, device="cuda", perturb=True)
+    w = env.world
+    before = w.dyn.clone()
+    s = _ffi.stream_ptr(w.device)
+    args = lambda B, n: (w.scene.handle, _ffi.ptr(w.dyn), _ffi.ptr(w.keys), _ffi.ptr(w.err), _ffi.ptr(w.geom),
+                         w.geom_stride, B, n, ctypes.c_float(1e-2), int(env.stages), None, 0, s)
+    assert _ffi.lib.cotix_step(*args(0, 5)) == 0
+    assert _ffi.lib.cotix_step(*args(4, 0)) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(w.dyn, before)
+    assert _ffi.lib.cotix_step(*args(-1, 1)) < 0
+    assert b"negative" in _ffi.lib.cotix_last_error()
+    assert _ffi.lib.cotix_step(*args(4, -1)) < 0

@@ -689,3 +689,29 @@ def test_empty_and_negative_sizes(torch_cuda):
     assert _ffi.lib.cotix_step(*args(-1, 1)) < 0
     assert b"negative" in _ffi.lib.cotix_last_error()
     assert _ffi.lib.cotix_step(*args(4, -1)) < 0
+
+
+def test_rank_shards_concatenate_to_single_run(torch_cuda):
+    """SURVEY 8(e) on the GPU: the envs of a 4-rank run (rank r owns global
+    envs [r*B/4, (r+1)*B/4) with its slice of the global key split, as
+    bench.py shards them) concatenate to the single-device run bit for bit."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    B, R, T = 256, 4, 8
+    keys = pa.random.split(pa.random.PRNGKey(3, torch.device("cuda")), B)
+    full = pa.RoboCupEnv(batch=B, device="cuda", keys=keys.clone(), perturb=True)
+    init = full.world.dyn.clone()
+    full.world.step(T, 1e-2, full.stages)
+    parts_dyn, parts_keys, parts_err = [], [], []
+    n = B // R
+    for r in range(R):
+        sh = pa.RoboCupEnv(batch=n, device="cuda", keys=keys[r * n:(r + 1) * n].clone(), perturb=True)
+        sh.world.dyn.copy_(init[:, :, r * n:(r + 1) * n])
+        sh.world.step(T, 1e-2, sh.stages)
+        parts_dyn.append(sh.world.dyn)
+        parts_keys.append(sh.world.keys)
+        parts_err.append(sh.world.err)
+    torch.cuda.synchronize()
+    assert same_f32(torch.cat(parts_dyn, 2).cpu().numpy(), full.world.dyn.cpu().numpy())
+    assert torch.equal(torch.cat(parts_keys), full.world.keys)
+    assert torch.equal(torch.cat(parts_err), full.world.err)

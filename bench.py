@@ -3,18 +3,36 @@
 One bench "step" = one launch of the fused HIP step kernel advancing every
 env by --substeps driver steps (examples/test_viz.py:61-69: Euler ->
 RandomizedCollider -> identity constraint pass -> key split), with episode
-restarts on the reference's error_if trip (DESIGN.md "Benchmark").  Inputs are
-resident in HBM before the timed region.  value = envs * substeps * steps *
-n_gpus / max-over-ranks wall time.
+restarts on the reference's error_if trip (DESIGN.md "Measurement").  Inputs
+are resident in HBM before the timed region.  value = envs * substeps * steps
+* n_gpus / max-over-ranks wall time.
 
   python bench.py [--gpus N --steps K --warmup W --substeps S --scenario robocup|lunar]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
 
---mode grad (BASELINE config 5): one bench step = a differentiable --substeps
-(64) step RoboCup rollout from a fixed start state, forward (cotix_rollout)
-+ backward (cotix_rollout_backward) -> d(sum_t ball x)/d(action) for every
-env; value = envs * substeps * steps * n_gpus / wall (env-steps with
-gradient per second).
+Rank r owns the envs with global ids [r*B, (r+1)*B) of the N*B-env run and
+builds them from those ids (RoboCupEnv(env_offset, total_envs)).  After each
+launch the observation tensor is all-gathered over RCCL (asynchronous, double
+buffered), the north star's one collective.
+
+The JSON line also carries, measured in the same process after the headline
+(rank 0, --extras auto):
+  workload_stats  finite-env fraction and restarts per env-step of the headline
+                  workload (the reference's RoboCup goes NaN at step 1)
+  k1              the headline scene with ONE driver step per launch (the launch
+                  rate an RL loop with per-step actions sees)
+  finite_scene    BoxWorld (balls in a box, finite dynamics) at the same size
+  lunar           BASELINE config 2 (LunarLander, 4096 envs, GJK/EPA)
+  grad            BASELINE config 5 (64-step differentiable rollout, fwd + bwd)
+  config1         BASELINE config 1 (one LunarLander env, 10,000 steps): GPU
+                  and the C port on one core
+  roofline        primary bound = VALU issue (SQ_INSTS_VALU of the committed
+                  rocprofv3 pass of this workload / live launch time), HBM
+                  figures as the north star asks
+
+--mode grad (BASELINE config 5) as its own line: one bench step = a
+differentiable --substeps (64) step RoboCup rollout, forward (cotix_rollout)
++ backward (cotix_rollout_backward) -> d(sum_t ball x)/d(action) for every env.
 """
 import argparse
 import json
@@ -22,12 +40,17 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per
+# 2 cycles (SIMD-32) at 2.4 GHz (MI355X_MICROARCH.md); one wave alone issues
+# one per 4 cycles, so at one wave per SIMD the ceiling is half of this.
+VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2
 
 
 def parse():
@@ -37,47 +60,160 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--substeps", type=int, default=64)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--scenario", default="robocup", choices=["robocup", "lunar"])
+    ap.add_argument("--scenario", default="robocup", choices=["robocup", "lunar", "box"])
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--extras", default="auto", choices=["auto", "off"])
     ap.add_argument("--mode", default="step", choices=["step", "grad"])
+    ap.add_argument("--dump-gather", default=None, help="save the last all-gathered and local observation (.npz)")
     return ap.parse_args()
 
 
-def cpu_baseline(scenario, seconds):
-    """Oracle port timed on this host (bounded sample).  Prefers the C port
-    (oracle/build/libcotix_oracle.so, OpenMP over envs), else the Python
-    oracle on one core."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+# ---------------------------------------------------------------------------
+# scenarios (global env ids [offset, offset+B) of a `total`-env run)
+# ---------------------------------------------------------------------------
+def make_scenario(pa, name, dev, B, offset=0, total=None):
+    total = B if total is None else total
+    sl = slice(offset, offset + B)
+    if name == "robocup":
+        return pa.RoboCupEnv(batch=B, device=dev, perturb=True, env_offset=offset, total_envs=total)
+    if name == "box":
+        return pa.BoxWorld(batch=B, device=dev, env_offset=offset, total_envs=total)
+    tk = pa.random.split(pa.random.PRNGKey(0, dev), total)[sl].contiguous()
+    ck = pa.random.split(pa.random.PRNGKey(1, dev), total)[sl].contiguous()
+    return pa.LunarLander(key=tk, batch=B, device=dev, collider_keys=ck)
+
+
+def bytes_per_env(name, nb):
+    """Algorithmic HBM bytes per env per launch (state in + out, key in + out,
+    err in + out; LunarLander: + per-env terrain read)."""
+    b = nb * 6 * 4 * 2 + 16 + 8
+    return b + (84 * 4 if name == "lunar" else 0)
+
+
+WORKLOAD = {"robocup": "RoboCup (cotix/_robocup.py) %d envs/GPU",
+            "lunar": "LunarLander (cotix/_lunar_lander.py) %d envs/GPU",
+            "box": "BoxWorld (balls in a box, finite dynamics; not a reference scenario) %d envs/GPU"}
+
+
+def timed_launches(fn, steps, warmup):
+    """`warmup` untimed calls, then `steps` calls bracketed by synchronize;
+    HIP events around each call on the current stream.  Returns (wall s,
+    mean event ms per call)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record()
+        fn()
+        e1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    return wall, sum(a.elapsed_time(b) for a, b in evs) / steps
+
+
+def finite_stats(pa, scen, substeps, launches):
+    """Diagnostics of a workload, outside any timed region: the same
+    trajectory as the timed run (the fused kernel == one-step launches bit for
+    bit, tests), stepped one driver step per launch with the state contract
+    check after each step.  finite_env_fraction = fraction of env-steps that
+    end on an all-finite state; restarts_per_env_step from the restart
+    counters."""
+    env = pa.BatchedEnv(scen, autoreset=True)
+    env.reset()
+    w = env.world
+    chk = torch.zeros(w.B, dtype=torch.int32, device=w.device)
+    finite = torch.zeros((), dtype=torch.float64, device=w.device)
+    n = substeps * launches
+    for _ in range(n):
+        env.step(1)
+        chk.zero_()
+        w.check_state(chk)
+        finite += (chk == 0).sum()
+    torch.cuda.synchronize()
+    return {"finite_env_fraction": float(finite.item()) / (n * w.B),
+            "restarts_per_env_step": float(env.resets.sum().item()) / (n * w.B),
+            "sample": "%d envs x %d driver steps (one per launch + cotix_check_state)" % (w.B, n)}
+
+
+def valu_roofline(scenario, B, substeps, launch_ms):
+    """Primary roofline: VALU issue.  SQ_INSTS_VALU per launch from the
+    committed rocprofv3 PMC pass of the same workload
+    (profiles/latest_pmc_<scenario>.json, tools/gpu_round.sh) over the live
+    launch time, against the chip's VALU issue peak.  HBM traffic per launch
+    from the same pass (FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM")."""
     try:
-        from cotix_oracle import cport
-        return cport.time_baseline(scenario, seconds)
-    except (ImportError, OSError):
-        pass
-    from cotix_oracle import geometry as G
+        pmc = json.load(open(os.path.join(ROOT, "profiles", "latest_pmc_%s.json" % scenario)))
+        c = pmc["config"]
+        if not (c.get("envs_per_gpu") == B and c.get("substeps_per_launch") == substeps):
+            return None
+        return {"valu_instr_per_launch": pmc["counters_per_launch"]["SQ_INSTS_VALU"],
+                "traffic": pmc["hbm_bytes_per_launch_corrected"],
+                "source": "profiles/%s_%s_summary.json" % (pmc["tag"], scenario),
+                "valu_active_frac_of_wave_cycles": pmc["valu_active_frac_of_wave_cycles"],
+                "pmc_avg_launch_ms": pmc["avg_launch_ns"] * 1e-6}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def roofline(scenario, B, substeps, launch_ms, nb):
+    alg = bytes_per_env(scenario, nb) * B
+    hbm = alg / (launch_ms * 1e-3) / 1e9
+    out = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_WAVE_INSTR_S / 1e9, "unit": "G wave-instr/s",
+           "frac": None, "traffic": None, "kernel": "step_kernel", "launch_ms": launch_ms,
+           "hbm": {"achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm / HBM_PEAK_GBS,
+                   "alg_bytes_per_launch": alg},
+           "note": "VALU/latency-bound path (threefry integer rounds + f32 geometry, no dense contraction): "
+                   "achieved = SQ_INSTS_VALU per launch / live launch time; peak = 256 CU x 4 SIMD x 2.4 GHz / "
+                   "2 cycles per wave64 instruction (one wave per SIMD issues at most half of it); "
+                   "hbm = algorithmic bytes / launch time, reported because north_star asks"}
+    v = valu_roofline(scenario, B, substeps, launch_ms)
+    if v is not None:
+        ach = v["valu_instr_per_launch"] / (launch_ms * 1e-3)
+        out.update(achieved=ach / 1e9, frac=ach / VALU_PEAK_WAVE_INSTR_S, traffic=v["traffic"],
+                   traffic_source=v["source"], valu_active_frac_of_wave_cycles=v["valu_active_frac_of_wave_cycles"],
+                   pmc_avg_launch_ms=v["pmc_avg_launch_ms"])
+    return out
+
+
+# ---------------------------------------------------------------------------
+# CPU baselines (oracle C port: test infrastructure, timed here as the
+# reported non-target baseline; never on the product path)
+# ---------------------------------------------------------------------------
+def cpu_baseline(scenario, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from cotix_oracle import cport
+    return cport.time_baseline(scenario, seconds)
+
+
+def cpu_config1(seconds=3.0):
+    """Config 1 on ONE core: the C port runs the single LunarLander env
+    (terrain PRNGKey(0), key chain from PRNGKey(0)) for 10,000 steps, repeated
+    until `seconds` of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from cotix_oracle import cport
     from cotix_oracle import physics as P
     from cotix_oracle import prng
-    d0 = prng.gjk_initial_direction()
-    mk = P.robocup_bodies if scenario == "robocup" else (lambda: P.lunar_lander_bodies(prng.PRNGKey(0)))
-    step = P.robocup_step if scenario == "robocup" else P.lunar_lander_step
+    lib = cport.load()
+    bodies = P.lunar_lander_bodies(prng.PRNGKey(0))
+    sc = cport.Scene(lib, bodies)
+    geom = sc.geom[None].copy()
+    d0 = np.ascontiguousarray(np.array([b.dyn() for b in bodies], np.float32)[:, :, None])
     n, t0 = 0, time.perf_counter()
-    bodies, key = mk(), prng.PRNGKey(0)
-    while time.perf_counter() - t0 < seconds:
-        err = G.ErrorFlag()
-        bodies, key = step(bodies, key, d0, err)
-        if err.bits:
-            bodies = mk()
-        n += 1
+    while time.perf_counter() - t0 < seconds or n == 0:
+        dyn, keys, err = d0.copy(), np.zeros((1, 2), np.uint32), np.zeros(1, np.uint32)
+        sc.step(dyn, keys, err, 10000, cport.STAGES_LUNAR, geom, nthreads=1)
+        n += 10000
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "%d sequential env-steps of one %s env (python oracle, autoreset), %.1f s" % (n, scenario, dt)}
+            "sample": "%d x the 10,000-step trajectory, C oracle port, 1 thread, %.1f s" % (n // 10000, dt)}
 
 
 def cpu_baseline_grad(T, seconds):
     """Central finite differences (eps=1e-3) of the C oracle port (SURVEY.md
-    8(d) config 5): 4T perturbed rollouts per env, OpenMP over all of them.
-    Bounded sample sized from a short probe to ~`seconds`."""
-    import numpy as np
+    8(d) config 5): 4T perturbed rollouts per env, OpenMP over all of them."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from cotix_oracle import cport
     from cotix_oracle import physics as P
@@ -95,7 +231,7 @@ def cpu_baseline_grad(T, seconds):
         return time.perf_counter() - t0
 
     B, dt = 8, run(8)
-    while dt < 0.5 * seconds and B < 4096:  # grow the sample to ~`seconds` of CPU work
+    while dt < 0.5 * seconds and B < 4096:
         B = int(min(4096, max(2 * B, B * seconds / max(dt, 1e-3))))
         dt = run(B)
     return {"value": B * T / dt, "unit": "env-steps/s (with d ret/d action)", "cores": nthreads, "kind": "port",
@@ -103,45 +239,82 @@ def cpu_baseline_grad(T, seconds):
                       "per env) of the C oracle port, OpenMP %d threads, %.1f s" % (B, T, 4 * T, nthreads, dt)}
 
 
-def main():
-    a = parse()
-    if a.mode == "grad":
-        return main_grad(a)
+# ---------------------------------------------------------------------------
+# secondary figures (rank 0, after the headline)
+# ---------------------------------------------------------------------------
+def sub_step(pa, dev, name, B, substeps, steps, warmup):
+    scen = make_scenario(pa, name, dev, B)
+    env = pa.BatchedEnv(scen, autoreset=True)
+    env.reset()
+    wall, ev_ms = timed_launches(lambda: env.step(substeps), steps, warmup)
+    out = {"workload": WORKLOAD[name] % B, "substeps_per_launch": substeps, "launches": steps,
+           "value": B * substeps * steps / wall, "unit": "env-steps/s", "launch_ms": ev_ms,
+           "hbm_GBs": bytes_per_env(name, len(scen.bodies)) * B / (ev_ms * 1e-3) / 1e9}
+    out.update(finite_stats(pa, make_scenario(pa, name, dev, B), 1, 64))
+    return out
+
+
+def sub_grad(pa, dev, B, T, steps, warmup):
+    r = run_grad(pa, dev, B, T, steps, warmup, rank=0, world_size=1)
+    return {"workload": "RoboCup %d envs, %d-step differentiable rollout, fwd + bwd (BASELINE config 5)" % (B, T),
+            "value": r["value"], "unit": "env-steps/s with d(return)/d(action)", "fwd_ms": r["fwd_ms"],
+            "bwd_ms": r["bwd_ms"], "finite_grad_env_fraction": r["finite"]}
+
+
+def sub_config1(pa, dev):
+    """BASELINE config 1: one LunarLander env (PRNGKey(0) terrain and key
+    chain), 10,000 driver steps in one launch (latency-bound: one wave)."""
+    ll = pa.LunarLander(batch=1, device=dev)
+    dyn0, keys0 = ll.world.dyn.clone(), ll.world.keys.clone()
+
+    def run():
+        ll.world.dyn.copy_(dyn0)
+        ll.world.keys.copy_(keys0)
+        ll.world.err.zero_()
+        ll.world.step(10000, 1e-2, ll.stages)
+
+    wall, ev_ms = timed_launches(run, 3, 1)
+    return {"workload": "LunarLander single env, 10,000 steps in one launch (BASELINE config 1)",
+            "value": 10000 / (ev_ms * 1e-3), "unit": "env-steps/s", "ms_per_10000_steps": ev_ms,
+            "cpu_1core": cpu_config1()}
+
+
+# ---------------------------------------------------------------------------
+# headline
+# ---------------------------------------------------------------------------
+def init_dist(force=False):
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    # COTIX_BENCH_FORCE_DIST=1: the collective path at world size 1 too (tests the RCCL code on one GPU)
-    if world_size > 1 or os.environ.get("COTIX_BENCH_FORCE_DIST") == "1":
+    # COTIX_BENCH_FORCE_DIST=1: the collective path at world size 1 too (needs
+    # RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT, as torchrun sets them)
+    if world_size > 1 or force:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+    return dist, rank, world_size, torch.device("cuda", local_rank)
+
+
+def main():
+    a = parse()
+    if a.mode == "grad":
+        return main_grad(a)
+    dist, rank, world_size, dev = init_dist(os.environ.get("COTIX_BENCH_FORCE_DIST") == "1")
     import parallax_amd as pa
 
     B = a.envs
-    # global env ids [rank*B, (rank+1)*B): keys split(PRNGKey(seed), B*world)[ids]
-    if a.scenario == "robocup":
-        keys = pa.random.split(pa.random.PRNGKey(3, dev), B * world_size)[rank * B:(rank + 1) * B].contiguous()
-        scen = pa.RoboCupEnv(batch=B, device=dev, keys=keys, perturb=True)
-        bytes_per_env = 5 * 6 * 4 * 2 + 16 + 8
-    else:
-        tk = pa.random.split(pa.random.PRNGKey(0, dev), B * world_size)[rank * B:(rank + 1) * B].contiguous()
-        ck = pa.random.split(pa.random.PRNGKey(1, dev), B * world_size)[rank * B:(rank + 1) * B].contiguous()
-        scen = pa.LunarLander(key=tk, batch=B, device=dev, collider_keys=ck)
-        bytes_per_env = 4 * 6 * 4 * 2 + 16 + 8 + 84 * 4
+    scen = make_scenario(pa, a.scenario, dev, B, rank * B, world_size * B)
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
+    nbody = len(scen.bodies)
     # observation all-gather, double-buffered and asynchronous: the RCCL
     # collective of launch i runs on its own stream while launch i+1 computes;
     # a buffer is rewritten only after the collective that read it is done
-    nbody = len(scen.bodies)
     obs_all = [torch.empty(world_size * B, nbody, 6, device=dev) for _ in range(2)] if dist else None
     obs_local = [torch.empty(B, nbody, 6, device=dev) for _ in range(2)] if dist else None
     pending = [None, None]
     launches = [0]
-
-    # HIP events around every step-kernel launch, on the stream it runs on
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
 
     def one_step(i=None):
@@ -186,15 +359,21 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     wall = float(tmax.item())
     resets = int(env.resets.sum().item())
+    gather = None
+    if dist is not None:  # the gathered tensor holds this rank's local observation in its slice
+        last = (launches[0] - 1) % 2
+        local = env.observation()
+        mine = obs_all[last][rank * B:(rank + 1) * B]
+        gather = "ok" if torch.equal(mine.view(torch.int32), local.view(torch.int32)) else "MISMATCH"
+        if a.dump_gather and rank == 0:
+            np.savez(a.dump_gather, gathered=obs_all[last].cpu().numpy(), local=local.cpu().numpy(),
+                     dyn=env.world.dyn.cpu().numpy())
 
-    # per-launch kernel time from HIP events on the launch stream (timed region)
     launch_ms = ev_ms / a.steps
-    alg_bytes = bytes_per_env * B  # HBM bytes one launch must move (state in + out)
-    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
     env_steps = B * a.substeps * a.steps * world_size
     out = {
         "metric": "env steps/sec (whole node), RoboCup 4096 envs/GPU, at 1/2/4/8 MI355X"
-        if a.scenario == "robocup" else "env steps/sec (whole node), LunarLander 4096 envs/GPU",
+        if a.scenario == "robocup" else "env steps/sec (whole node), %s" % (WORKLOAD[a.scenario] % B),
         "value": env_steps / wall,
         "unit": "env-steps/s",
         "n_gpus": world_size,
@@ -205,75 +384,50 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (reference scenario constructors; per-env perturbation/terrain from threefry keys)",
+        "data": "synthetic (reference scenario constructors; per-env perturbation/terrain from threefry keys "
+                "of the global env id)",
         "config": {
-            "workload": ("RoboCup (cotix/_robocup.py) %d envs/GPU" if a.scenario == "robocup"
-                         else "LunarLander (cotix/_lunar_lander.py) %d envs/GPU") % B,
+            "workload": WORKLOAD[a.scenario] % B,
             "envs_per_gpu": B,
             "substeps_per_launch": a.substeps,
             "autoreset_on_error": True,
             "episode_restarts": resets,
-            "parallelism": "dp%d (independent env shards, RCCL obs all-gather)" % world_size,
+            "restarts_per_env_step": resets / (B * a.substeps * (a.steps + a.warmup)),
+            "parallelism": "dp%d (independent env shards by global env id, RCCL obs all-gather)" % world_size,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
-            "kernel": "step_kernel",
-            "launch_ms": launch_ms,
-            "alg_bytes_per_launch": alg_bytes,
-            "note": "VALU/latency-bound path (no dense contraction); HBM figure reported because north_star asks",
-        },
+        "roofline": roofline(a.scenario, B, a.substeps, launch_ms, nbody),
     }
-    # HBM traffic per launch from the committed rocprofv3 PMC pass of the same
-    # workload (profiles/latest_pmc_<scenario>.json, tools/gpu_round.sh);
-    # FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM" (gfx950 reports half
-    # the bytes).  The same pass gives the VALU issue fraction -- the bound
-    # that actually limits this path.
-    try:
-        pmc = json.load(open(os.path.join(ROOT, "profiles", "latest_pmc_%s.json" % a.scenario)))
-        c = pmc["config"]
-        if (c.get("envs_per_gpu") == B and c.get("substeps_per_launch") == a.substeps
-                and c.get("workload", "").split()[0] == out["config"]["workload"].split()[0]):
-            out["roofline"]["traffic"] = pmc["hbm_bytes_per_launch_corrected"]
-            out["roofline"]["traffic_source"] = "profiles/%s_%s_summary.json" % (pmc["tag"], a.scenario)
-            out["roofline"]["valu_issue_frac"] = pmc["valu_active_frac_of_wave_cycles"]
-    except (OSError, KeyError, ValueError):
-        pass
+    if gather is not None:
+        out["config"]["obs_all_gather_check"] = gather
+    if rank == 0 and a.extras == "auto":
+        out["workload_stats"] = finite_stats(pa, make_scenario(pa, a.scenario, dev, B), 1, 64)
     if rank == 0 and a.cpu_baseline == "auto":
-        out["cpu_baseline"] = cpu_baseline(a.scenario, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(a.scenario if a.scenario != "box" else "robocup", a.cpu_seconds)
+    if rank == 0 and a.extras == "auto" and a.scenario == "robocup":
+        out["k1"] = sub_step(pa, dev, "robocup", B, 1, 200, 10)
+        out["finite_scene"] = sub_step(pa, dev, "box", B, a.substeps, 10, 2)
+        out["lunar"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 2)
+        out["grad"] = sub_grad(pa, dev, B, 64, 5, 1)
+        out["config1"] = sub_config1(pa, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
+        dist.barrier()
         dist.destroy_process_group()
 
 
-def main_grad(a):
-    """BASELINE config 5: differentiable RoboCup rollout, forward + backward."""
-    import numpy as np
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world_size > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    import parallax_amd as pa
-    B, T = a.envs, a.substeps
-    keys = pa.random.split(pa.random.PRNGKey(3, dev), B * world_size)[rank * B:(rank + 1) * B].contiguous()
-    scen = pa.RoboCupEnv(batch=B, device=dev, keys=keys, perturb=True)
+# ---------------------------------------------------------------------------
+# config 5 as its own line
+# ---------------------------------------------------------------------------
+def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None):
+    scen = pa.RoboCupEnv(batch=B, device=dev, perturb=True, env_offset=rank * B, total_envs=world_size * B)
     world = scen.world
     dyn0, keys0 = world.dyn.clone(), world.keys.clone()
     gen = torch.Generator(device="cpu").manual_seed(1234 + rank)
     actions = (torch.randn(T, B, 2, generator=gen) * 0.1).to(dev)  # SURVEY 8(d): ball dv ~ N(0, 0.1^2)
     w = pa.rollout.ball_x_weights(5, 4)
-    evf = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    evb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    evf = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    evb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     state = {}
 
     def one_step(i=None):
@@ -291,14 +445,14 @@ def main_grad(a):
             evb[i][1].record()
         state["ret"], state["ga"] = ret, ga
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         one_step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
+    for i in range(steps):
         one_step(i)
     torch.cuda.synchronize()
     if dist:
@@ -309,22 +463,31 @@ def main_grad(a):
     if dist:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     wall = float(tmax.item())
-    fwd_ms = sum(e0.elapsed_time(e1) for e0, e1 in evf) / a.steps
-    bwd_ms = sum(e0.elapsed_time(e1) for e0, e1 in evb) / a.steps
     ga = state["ga"]
-    finite = float(torch.isfinite(ga).all(dim=2).all(dim=0).float().mean().item())
+    return {"value": B * T * steps * world_size / wall, "wall": wall,
+            "fwd_ms": sum(e0.elapsed_time(e1) for e0, e1 in evf) / steps,
+            "bwd_ms": sum(e0.elapsed_time(e1) for e0, e1 in evb) / steps,
+            "finite": float(torch.isfinite(ga).all(dim=2).all(dim=0).float().mean().item())}
+
+
+def main_grad(a):
+    """BASELINE config 5: differentiable RoboCup rollout, forward + backward."""
+    dist, rank, world_size, dev = init_dist()
+    import parallax_amd as pa
+    B, T = a.envs, a.substeps
+    r = run_grad(pa, dev, B, T, a.steps, a.warmup, rank, world_size, dist)
     # algorithmic HBM bytes of the backward launch per env-step: saved state
     # (5x6 f32) + key (2 u32) + action (2 f32) read, grad_action (2 f32) written
     bwd_bytes = (5 * 6 * 4 + 8 + 8 + 8) * B * T
-    achieved = bwd_bytes / (bwd_ms * 1e-3) / 1e9
+    achieved = bwd_bytes / (r["bwd_ms"] * 1e-3) / 1e9
     out = {
         "metric": "differentiable 64-step RoboCup rollout, 4096 envs/GPU: env-steps/s with d(return)/d(action)",
-        "value": B * T * a.steps * world_size / wall,
+        "value": r["value"],
         "unit": "env-steps/s",
         "n_gpus": world_size,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": wall * 1e3 / a.steps,
+        "ms_per_step": r["wall"] * 1e3 / a.steps,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -335,22 +498,23 @@ def main_grad(a):
                         "w.r.t. per-step ball dv (BASELINE config 5)" % (B, T),
             "envs_per_gpu": B,
             "rollout_steps": T,
-            "fwd_ms": fwd_ms,
-            "bwd_ms": bwd_ms,
-            "finite_grad_env_fraction": finite,
+            "fwd_ms": r["fwd_ms"],
+            "bwd_ms": r["bwd_ms"],
+            "finite_grad_env_fraction": r["finite"],
             "parallelism": "dp%d (independent env shards)" % world_size,
         },
         "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "bound": "valu",
+            "achieved": None,
+            "peak": VALU_PEAK_WAVE_INSTR_S / 1e9,
+            "unit": "G wave-instr/s",
+            "frac": None,
             "traffic": None,
-            "kernel": "step_kernel<4,1,true> (backward re-play)",
-            "launch_ms": bwd_ms,
-            "alg_bytes_per_launch": bwd_bytes,
-            "note": "VALU/latency-bound (the backward re-plays each step's forward); HBM figure for completeness",
+            "kernel": "step_kernel<4,1,2> (backward re-play)",
+            "launch_ms": r["bwd_ms"],
+            "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                    "alg_bytes_per_launch": bwd_bytes},
+            "note": "VALU/latency-bound (the backward re-plays each step's forward); no PMC pass of this mode",
         },
     }
     if rank == 0 and a.cpu_baseline == "auto":

@@ -13,6 +13,8 @@
  *   cotix_step            examples/test_viz.py:24-44 (LunarLander f) and :61-69
  *                         (RoboCup f): Euler -> [gravity] -> collider ->
  *                         [LunarLander.step] -> key = split(key)[0], n_steps times
+ *   cotix_step_ex         the same + restarts + actions + the collider's contact
+ *                         choices (cotix/_colliders.py:208-295) as a trace
  *   cotix_physics_euler   ExplicitEulerPhysics.step   cotix/_physics_solvers.py:16-33
  *   cotix_collider_resolve RandomizedCollider.resolve cotix/_colliders.py:74-351
  *   cotix_lunar_constraints LunarLander.step          cotix/_lunar_lander.py:145-218
@@ -119,6 +121,25 @@ int cotix_step(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, co
 int cotix_step_autoreset(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
                          int geom_stride, int B, int n_steps, float dt, int stages, const float* dyn_reset,
                          uint32_t* resets, cotix_stream_t stream);
+
+/* The fused step with every option (all pointers nullable):
+ *   action [n_steps][B][2]  added to body action_body's velocity after Euler
+ *   dyn_reset/resets        episode restarts as cotix_step_autoreset (the
+ *                           action keeps applying to a restarted env)
+ *   chosen  device i32 [n_steps][n_bodies][B]: the collider's chosen partner
+ *           j* of body i at each step (choose_random_contact,
+ *           cotix/_colliders.py:274-295; i itself when the body has no
+ *           contact; -1 when the collider stage is off)
+ *   cells   device i32 [n_steps][n_bodies][n_bodies][B]: for cell (i, j) the
+ *           candidate of the reference's scan whose contact all_contacts[i, j]
+ *           holds after the scan (the LAST passing one, :208-268), encoded
+ *           ind1 | ind2 << 9 | type << 18 (type = index of the (Ta, Tb) key in
+ *           dict-insertion order, ind1/ind2 = positions in its two candidate
+ *           lists, :86-113); -1 for an empty (NaN) cell or collider stage off.
+ * Both traces describe the step BEFORE a restart replaces the state. */
+int cotix_step_ex(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
+                  int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                  const float* dyn_reset, uint32_t* resets, int32_t* chosen, int32_t* cells, cotix_stream_t stream);
 
 /* Differentiable rollout (BASELINE config 5: grad(return)/d(action) through a
  * fused n_steps RoboCup rollout).  The reference has no return or action

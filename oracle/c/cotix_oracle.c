@@ -514,8 +514,13 @@ static void world_shape(const OScene* s, int p, const Dyn* d, const float* lg, S
 
 /* RandomizedCollider.resolve, faithful (forward scan over the full cross product) */
 typedef struct { Contact* cur; K2* keys2; K2* keys1; } Work;
-static void collider(const OScene* s, Dyn* d, const float* geom, K2 rkey, V2 d0, uint32_t* err, Work* wk) {
+/* tr_ch [nb] / tr_cells [nb*nb] (nullable): the chosen partner per body and
+ * the winning candidate per cell (ind1 | ind2 << 9 | type << 18, -1 empty) */
+static void collider(const OScene* s, Dyn* d, const float* geom, K2 rkey, V2 d0, uint32_t* err, Work* wk,
+                     int* tr_ch, int* tr_cells) {
   int nb = s->nb;
+  int win[MAXB][MAXB];
+  for (int i = 0; i < nb; ++i) for (int j = 0; j < nb; ++j) win[i][j] = -1;
   Shape world[MAXP];
   for (int p = 0; p < s->np; ++p) world_shape(s, p, d, geom + s->pgoff[p], &world[p]);
   V2 pen[MAXB][MAXB], cp[MAXB][MAXB];
@@ -544,6 +549,7 @@ static void collider(const OScene* s, Dyn* d, const float* geom, K2 rkey, V2 d0,
         if ((bits1(split0(keys1[i1])) >> 31) == 0u) {
           int bi = s->l1b[k][i1], bj = s->l2b[k][i2];
           pen[bi][bj] = c.pen; cp[bi][bj] = c.cp;
+          win[bi][bj] = i1 | (i2 << 9) | (k << 18);
         }
       }
     }
@@ -563,6 +569,8 @@ static void collider(const OScene* s, Dyn* d, const float* geom, K2 rkey, V2 d0,
     ch[i] = nb;
     for (int j = 0; j < nb; ++j) if (!(c[j] < r)) { ch[i] = j; break; }
   }
+  if (tr_ch) for (int i = 0; i < nb; ++i) tr_ch[i] = ch[i];
+  if (tr_cells) for (int i = 0; i < nb; ++i) for (int j = 0; j < nb; ++j) tr_cells[i * nb + j] = win[i][j];
   for (int i = 0; i < nb; ++i) {
     int j = ch[i];
     if (j == i || j >= nb) continue;
@@ -575,7 +583,8 @@ static void collider(const OScene* s, Dyn* d, const float* geom, K2 rkey, V2 d0,
  * stages as include/cotix_amd.h; dyn_reset nullable (autoreset like the bench). */
 static int drive(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
                  int n_steps, float dt, int stages, const float* dyn_reset, uint32_t* resets, const float* action,
-                 int action_body, const float* ret_w, float* ret, int nthreads) {
+                 int action_body, const float* ret_w, float* ret, int32_t* tr_chosen, int32_t* tr_cells,
+                 int nthreads) {
   const OScene* s = (const OScene*)scene;
   const V2 d0 = {bitsf(0xbd56c50bu), bitsf(0x3f7fa5d9u)};
 #ifdef _OPENMP
@@ -608,7 +617,17 @@ static int drive(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, c
         d[action_body].vx = d[action_body].vx + ac[0];
         d[action_body].vy = d[action_body].vy + ac[1];
       }
-      if (stages & 4) collider(s, d, gg, key, d0, &e, &wk);
+      if (stages & 4) {
+        int tch[MAXB], tcl[MAXB * MAXB];
+        collider(s, d, gg, key, d0, &e, &wk, tch, tcl);
+        if (tr_chosen)
+          for (int i = 0; i < nb; ++i) tr_chosen[((size_t)t * nb + i) * B + g] = tch[i];
+        if (tr_cells)
+          for (int q = 0; q < nb * nb; ++q) tr_cells[((size_t)t * nb * nb + q) * B + g] = tcl[q];
+      } else {
+        if (tr_chosen) for (int i = 0; i < nb; ++i) tr_chosen[((size_t)t * nb + i) * B + g] = -1;
+        if (tr_cells) for (int q = 0; q < nb * nb; ++q) tr_cells[((size_t)t * nb * nb + q) * B + g] = -1;
+      }
       if (stages & 8) lunar(&d[0], &d[1], &d[2], &s->par[0], &s->par[1], &s->par[2]);
       if (stages & 16) key = split0(key);
       if (dyn_reset && e) {
@@ -646,7 +665,16 @@ static int drive(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, c
 int oracle_step(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
                 int n_steps, float dt, int stages, const float* dyn_reset, uint32_t* resets, int nthreads) {
   return drive(scene, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, dyn_reset, resets, NULL, 0, NULL, NULL,
-               nthreads);
+               NULL, NULL, nthreads);
+}
+
+/* the step with actions (nullable, [n_steps][B][2]), restarts and the collider
+ * trace (chosen [n_steps][nb][B], cells [n_steps][nb][nb][B], both nullable) */
+int oracle_step_ex(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
+                   int n_steps, float dt, int stages, const float* action, int action_body, const float* dyn_reset,
+                   uint32_t* resets, int32_t* chosen, int32_t* cells, int nthreads) {
+  return drive(scene, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, dyn_reset, resets, action, action_body,
+               NULL, NULL, chosen, cells, nthreads);
 }
 
 /* forward of the differentiable rollout: action [n_steps][B][2], ret [B] += */
@@ -654,7 +682,7 @@ int oracle_rollout(const void* scene, float* dyn, uint32_t* keys, uint32_t* err,
                    int B, int n_steps, float dt, int stages, const float* action, int action_body, const float* ret_w,
                    float* ret, int nthreads) {
   return drive(scene, dyn, keys, err, geom, gstride, B, n_steps, dt, stages, NULL, NULL, action, action_body, ret_w,
-               ret, nthreads);
+               ret, NULL, NULL, nthreads);
 }
 
 int oracle_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err) {

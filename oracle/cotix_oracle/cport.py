@@ -24,6 +24,8 @@ def load():
     lib.oracle_scene_init.argtypes = [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P, _P]
     lib.oracle_step.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                 ctypes.c_int, _P, _P, ctypes.c_int]
+    lib.oracle_step_ex.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                   ctypes.c_int, _P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int]
     lib.oracle_contacts.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P]
     lib.oracle_rollout.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                    ctypes.c_int, _P, ctypes.c_int, _P, _P, ctypes.c_int]
@@ -72,6 +74,21 @@ class Scene:
         self.lib.oracle_step(self.mem, _p(dyn), _p(keys), _p(err), _p(g), gstride, B, n_steps, dt, stages,
                              _p(dyn_reset), _p(resets), nthreads)
 
+    def step_ex(self, dyn, keys, err, n_steps, stages, geom=None, action=None, action_body=0, dyn_reset=None,
+                resets=None, trace=False, nthreads=0, dt=1e-2):
+        """step() with actions [n_steps, B, 2] and the collider trace: returns
+        (chosen i32 [n_steps, nb, B], cells i32 [n_steps, nb, nb, B]) or None."""
+        B = dyn.shape[2]
+        g = self.geom if geom is None else np.ascontiguousarray(geom, np.float32)
+        gstride = 0 if geom is None else g.shape[1]
+        ch = cl = None
+        if trace:
+            ch = np.full((n_steps, self.n_bodies, B), -7, np.int32)
+            cl = np.full((n_steps, self.n_bodies, self.n_bodies, B), -7, np.int32)
+        act = None if action is None else np.ascontiguousarray(action, np.float32)
+        self.lib.oracle_step_ex(self.mem, _p(dyn), _p(keys), _p(err), _p(g), gstride, B, n_steps, dt, stages,
+                                _p(act), action_body, _p(dyn_reset), _p(resets), _p(ch), _p(cl), nthreads)
+        return (ch, cl) if trace else None
 
     def rollout(self, dyn, keys, err, stages, actions, action_body, ret_w, geom=None, nthreads=0, dt=1e-2):
         """Forward of the differentiable rollout; returns ret [B]."""
@@ -105,15 +122,20 @@ def fd_action_grad(sc, dyn0, keys0, actions, action_body, ret_w, stages, eps=1e-
     return g.reshape(T, 2, B).transpose(0, 2, 1)
 
 
-def robocup_batch(B, seed_keys=3):
-    """The bench's RoboCup batch (perturbed ball per env, keys split(PRNGKey(3), B))."""
+def robocup_batch(B, seed_keys=3, offset=0, total=None):
+    """The bench's RoboCup batch for global env ids offset .. offset+B-1 of a
+    `total`-env run (perturbed ball per env from split(PRNGKey(2), total),
+    keys split(PRNGKey(3), total); global env 0 unperturbed)."""
     from . import geometry  # noqa: F401
-    keys = np.ascontiguousarray(prng.split(prng.PRNGKey(seed_keys), B)).astype(np.uint32)
+    total = B if total is None else total
+    keys = np.ascontiguousarray(prng.split(prng.PRNGKey(seed_keys), total)[offset:offset + B]).astype(np.uint32)
     base = np.array([b.dyn() for b in P.robocup_bodies()], np.float32)
     dyn = np.repeat(base[:, :, None], B, axis=2)
-    pk = prng.split(prng.PRNGKey(2), B)
-    for e in range(1, B):
-        kp, kv, kw = prng.split(pk[e], 3)
+    pk = prng.split(prng.PRNGKey(2), total)
+    for e in range(B):
+        if offset + e == 0:
+            continue
+        kp, kv, kw = prng.split(pk[offset + e], 3)
         u = prng.uniform(kp, (2,))
         lo, hi = np.array([-4.4, -2.9], np.float32), np.array([4.4, 2.9], np.float32)
         pos = np.maximum(lo, u * (hi - lo) + lo)

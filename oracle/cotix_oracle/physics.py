@@ -165,8 +165,9 @@ def collider_resolve(bodies, rkey, d0, err=None, trace=None):
     pen = [[(ZERO, ZERO) for _ in range(n)] for _ in range(n)]
     cp = [[(NAN, NAN) for _ in range(n)] for _ in range(n)]
     src = [[None for _ in range(n)] for _ in range(n)]  # (contact fn, (body, part) of s1, of s2)
+    win = [[-1 for _ in range(n)] for _ in range(n)]  # winning candidate: ind1 | ind2 << 9 | type << 18
     skey = prng.split(rkey)[0]  # :142
-    for key_t, (l1, l2) in type_to.items():
+    for ti, (key_t, (l1, l2)) in enumerate(type_to.items()):
         N1, N2 = len(l1), len(l2)
         fname = CONTACT_FUNCS[key_t]
         # cross product of contacts :149-173
@@ -199,6 +200,7 @@ def collider_resolve(bodies, rkey, d0, err=None, trace=None):
                     pen[bi][bj] = c[0]
                     cp[bi][bj] = c[1]
                     src[bi][bj] = srcs[(i1, i2)]
+                    win[bi][bj] = i1 | (i2 << 9) | (ti << 18)
     # choose_random_contact :274-295
     ckeys = prng.split(skey, n)
     chosen = []
@@ -214,6 +216,7 @@ def collider_resolve(bodies, rkey, d0, err=None, trace=None):
         trace["chosen"] = list(chosen)
         trace["contacts"] = [[(pen[i][j], cp[i][j]) for j in range(n)] for i in range(n)]
         trace["src"] = src
+        trace["cells"] = [row[:] for row in win]
     # sequential resolution :310-336
     for i in range(n):
         j = chosen[i]

@@ -30,6 +30,7 @@ SIGNATURES = {
     "cotix_scene_info": (_I, [_P, _P, _P, _P, _P]),
     "cotix_step": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P]),
     "cotix_step_autoreset": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
+    "cotix_step_ex": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P, _P]),
     "cotix_rollout": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P, _P]),
     "cotix_rollout_backward": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P]),
     "cotix_body_penetration": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),

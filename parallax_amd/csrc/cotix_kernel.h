@@ -88,6 +88,11 @@ struct KArgs {
   const float* dyn_reset;  // [nb][6][B] or null
   uint32_t* resets;        // [B] or null
   int dbg_skip;            // timing only: skip phase T=1, B=2, C=4, D=8, A's key splits=16, E=32
+  // collider trace (cotix_step_ex; null = off): per step, body and env the
+  // chosen partner j* (cotix/_colliders.py:274-295), and per cell (i, j) the
+  // reference-scan candidate whose contact all_contacts[i, j] holds (:208-268)
+  int32_t* trace_chosen;   // [n_steps][nb][B]
+  int32_t* trace_cells;    // [n_steps][nb][nb][B]: i1 | i2 << 9 | type << 18, -1 = empty cell
   // differentiable rollout (cotix_rollout / cotix_rollout_backward)
   float* save_dyn;         // [n_steps][nb*6][B]: state before each step, or null
   uint32_t* save_keys;     // [n_steps][B][2]
@@ -115,7 +120,7 @@ CX_HD Lay layout(int nb, int W, int nc, int nt, int G) {
   L.dyn = 0;
   L.world = L.dyn + nb * 6;
   L.con = L.world + W + 2 * cx::MAXV;  // slack: shape fetches read 2*MAXV words
-  L.m = L.con + nc * 4;
+  L.m = L.con + nc * 4;  // all_contacts cells: the winning candidate word (o_cand format), ~0 = empty
   L.ch = L.m + nb * nb;
   L.key = L.ch + nb;
   L.sk0 = L.key + 2;
@@ -772,7 +777,7 @@ CX_DEV void ph_C2(const Ctx& c, Tile<EW> t, int lane, int par) {
     if (bits != 0ull) {
       const int idx = (int)pos + __builtin_ctzll(bits);
       const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
-      t.w(c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = (cd >> 18) & 511u;
+      t.w(c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = cd;  // the winning candidate word
     } else {
       pos = pos + (uint32_t)G;
       t.ws[WS_KEEP + slot] = (int)pos < t.ti(sc.o_ccnt + l) ? 1u : 0u;
@@ -877,7 +882,7 @@ CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
     if (bits != 0ull) {
       const int idx = (int)pos + __builtin_ctzll(bits);
       const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
-      t.w(c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = (cd >> 18) & 511u;
+      t.w(c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = cd;  // the winning candidate word
     } else {
       pos = pos + (uint32_t)G;
       keep = (int)pos < t.ti(sc.o_ccnt + l) ? 1u : 0u;
@@ -987,9 +992,10 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
     ch = cnt > 0 ? cj : i;
   }
   t.w(L.ch + i, e) = (uint32_t)ch;
-  int cid = -1;  // all_contacts[i, ch], picked from the loaded row
+  int cid = -1;  // all_contacts[i, ch], picked from the loaded row (candidate word -> distinct contact)
 #pragma unroll
   for (int j = 0; j < MB; ++j) cid = j == ch ? mm[j] : cid;
+  cid = cid < 0 ? -1 : (cid >> 18) & 511;
   e0_item<EW, RCP>(c, t, e, i, ch, cid);
 }
 template <int EW, bool PRE = false>
@@ -1228,6 +1234,28 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   }
 }
 
+// collider trace of step `step` (cotix_step_ex): chosen partner per body and
+// the winning candidate per cell, item = (word, env); -1 where the collider
+// stage is off or the cell is empty
+template <int EW>
+CX_DEV void ph_trace(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+  const Lay& L = c.L;
+  const int nb = c.nb;
+  const bool col = (a.stages & COTIX_STAGE_COLLIDER) != 0;
+  if (a.trace_chosen != nullptr)
+    for (int w = lane; w < nb * EW; w += WAVE) {
+      const int e = w % EW, i = w / EW, g = env0 + e;
+      if (g < a.B) a.trace_chosen[((size_t)step * nb + i) * a.B + g] = col ? (int32_t)t.w(L.ch + i, e) : -1;
+    }
+  if (a.trace_cells != nullptr)
+    for (int w = lane; w < nb * nb * EW; w += WAVE) {
+      const int e = w % EW, k = w / EW, g = env0 + e;
+      const uint32_t cd = t.w(L.m + k, e);
+      const int32_t code = (!col || cd == 0xFFFFFFFFu) ? -1 : (int32_t)((cd & 0x3FFFFu) | ((cd >> 27) << 18));
+      if (g < a.B) a.trace_cells[((size_t)step * nb * nb + k) * a.B + g] = code;
+    }
+}
+
 // phase R (autoreset launches): restore the restarting envs' state,
 // item = (state word, env)
 template <int EW>
@@ -1331,7 +1359,7 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         const int ro = L.rec + REC_W * i;
         if (t.w(ro, e) == 0u) continue;
         const int j = (int)t.w(L.ch + i, e);
-        const int cid = (int)t.w(L.m + i * nb + j, e);
+        const int cid = (int)((t.w(L.m + i * nb + j, e) >> 18) & 511u);
         const int co = L.con + 4 * cid, oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
         const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), t.f(ro + 1, e), t.f(ro + 2, e), t.f(oi + 4, e), t.f(ro + 3, e)};
         const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), t.f(ro + 4, e), t.f(ro + 5, e), t.f(oj + 4, e), t.f(ro + 6, e)};
@@ -1418,7 +1446,7 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // emulation of the tests R loops over the 64 lanes.  The phase id is used
 // only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
-             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_COUNT };
+             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_TRACE, PH_COUNT };
 // ---------------------------------------------------------------------------
 // kso: tile offset of this step's sk0 (skt follows): the key window slot, or
 // L.sk0 where phase A splits the keys (backward re-play)
@@ -1489,6 +1517,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     const int kso = c.L.kw + slot * c.L.kww;  // this step's sk0, skt in the key window
     run(PH_A, [&](int l) { ph_A<EW, true>(a, c, t, env0, l, step, slot); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso);
+    if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
+      run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!(a.dbg_skip & 32)) {
       run(PH_E1, [&](int l) { ph_E<EW>(a, c, t, env0, l, kso); });
       if (a.dyn_reset != nullptr) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });

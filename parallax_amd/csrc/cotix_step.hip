@@ -1,6 +1,8 @@
-// cotix_step.hip -- MI355X (gfx950) kernels of the cotix per-step hot path and
-// the C-ABI declared in include/cotix_amd.h.  The fused step kernel's phases
-// live in cotix_kernel.h (design notes there and in DESIGN.md).
+// cotix_step.hip -- MI355X (gfx950) operator kernels of the cotix per-step hot
+// path and the C-ABI declared in include/cotix_amd.h.  The fused step kernel
+// is cotix_step_kernel.hip (one translation unit per envs-per-wave tiling,
+// compiled in parallel); its phases live in cotix_kernel.h (design notes there
+// and in DESIGN.md).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -12,6 +14,7 @@
 #include "cotix_device.h"
 #include "cotix_body.h"
 #include "cotix_kernel.h"
+#include "cotix_launch.h"
 #include "cotix_scene.h"
 
 using cxk::FNS_ANALYTIC;
@@ -39,72 +42,6 @@ struct cotix_scene {
 };
 
 namespace {
-
-// ---------------------------------------------------------------------------
-// the fused step kernel: WPB independent waves per workgroup, EW envs per wave
-// ---------------------------------------------------------------------------
-constexpr int WPB = 4;
-#ifdef COTIX_PHASE_PROF
-__device__ unsigned long long g_phase_cycles[cxk::PH_COUNT];
-#endif
-// one phase on this lane, then wave-local ordering before the next phase
-struct WaveRun {
-  int lane;
-#ifdef COTIX_PHASE_PROF
-  unsigned long long* acc;  // per-phase cycle accumulators (registers after inlining)
-  template <class F>
-  __device__ __forceinline__ void operator()(int ph, F f) const {
-    const unsigned long long t0 = clock64();
-    f(lane);
-    cxk::wave_sync();
-    acc[ph] += clock64() - t0;
-  }
-#elif defined(COTIX_ASM_MARKERS)  // tooling: phase markers in the ISA (tools/isa_phases.py)
-  template <class F>
-  __device__ __forceinline__ void operator()(int ph, F f) const {
-    asm volatile(";#PHASE_BEGIN %0" ::"s"(ph));
-    f(lane);
-    cxk::wave_sync();
-    asm volatile(";#PHASE_END %0" ::"s"(ph));
-  }
-#else
-  template <class F>
-  __device__ __forceinline__ void operator()(int, F f) const {
-    f(lane);
-    cxk::wave_sync();
-  }
-#endif
-};
-// MODE 0: step, 1: rollout forward (saves + return), 2: rollout backward
-template <int EW, int FNSET, int MODE>
-__global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
-  extern __shared__ uint32_t lds[];
-  const SceneDev* sc = a.sc;
-  const int nhot = a.sh.nhot;
-  for (int i = threadIdx.x; i < nhot; i += WPB * 64) lds[i] = sc->hot[i];
-  __syncthreads();
-  const cxk::Ctx c = cxk::make_ctx<EW>(a.sh);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int env0 = (blockIdx.x * WPB + wave) * EW;
-  if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
-  uint32_t* wbase = lds + nhot + wave * (c.L.S * EW + c.W.words);
-  const cxk::Tile<EW> t{wbase, lds, wbase + c.L.S * EW};
-#ifdef COTIX_PHASE_PROF
-  unsigned long long acc[cxk::PH_COUNT];
-  for (int q = 0; q < cxk::PH_COUNT; ++q) acc[q] = 0ull;
-  const WaveRun run{lane, acc};
-#else
-  const WaveRun run{lane};
-#endif
-  if (MODE == 2)
-    cxk::run_wave_backward<EW, FNSET>(a, c, t, env0, run);
-  else
-    cxk::run_wave<EW, FNSET, MODE == 1>(a, c, t, env0, run);
-#ifdef COTIX_PHASE_PROF
-  if (lane == 0)
-    for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);
-#endif
-}
 
 // ---------------------------------------------------------------------------
 // operator kernels
@@ -251,18 +188,6 @@ extern "C" {
 const char* cotix_last_error(void) { return g_err.c_str(); }
 const char* cotix_version(void) { return "cotix_amd 0.1 (gfx950)"; }
 
-#ifdef COTIX_PHASE_PROF
-// profiling build only: per-phase cycles summed over waves since the last call (then reset)
-int cotix_phase_cycles(unsigned long long* out, int n) {
-  unsigned long long h[cxk::PH_COUNT] = {};
-  if (hip_check(hipDeviceSynchronize(), "sync")) return -1;
-  if (hip_check(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase_cycles), sizeof(h)), "read phase cycles")) return -1;
-  unsigned long long z[cxk::PH_COUNT] = {};
-  if (hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)), "reset phase cycles")) return -1;
-  for (int q = 0; q < n && q < cxk::PH_COUNT; ++q) out[q] = h[q];
-  return cxk::PH_COUNT;
-}
-#endif
 
 int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,
                        const int* part_type, const int* part_nverts, cotix_scene** out) {
@@ -323,50 +248,37 @@ static int check_step_args(const cotix_scene* scene, const float* dyn, const uin
 // launch the fused step kernel (mode 0 step, 1 rollout forward, 2 backward re-play)
 static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_stream_t stream) {
   if (scene_upload(scene)) return -1;
+#ifdef COTIX_EW4_ONLY
+  const int EW = 4;
+#else
   const int EW = envs_per_wave();
-  const size_t lds = cxk::lds_bytes(scene->host, WPB, EW);
+#endif
+  const size_t lds = cxk::lds_bytes(scene->host, cxl::WPB, EW);
   if (lds > 160 * 1024) return fail("scene too large for the LDS tile");
   cxk::KArgs ka = ka0;
   ka.sc = scene->dev;
   ka.sh = scene->host;  // the header by value (kernel arguments)
   const char* dbg = getenv("COTIX_DEBUG_SKIP");
   ka.dbg_skip = dbg ? atoi(dbg) : 0;
-  dim3 grid((ka.B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int fs = scene->fnset;
-#define COTIX_LAUNCH(EE, FS, BW) hipLaunchKernelGGL((step_kernel<EE, FS, BW>), grid, block, lds, st, ka)
-#ifdef COTIX_EW4_ONLY  // tooling builds (phase profile): the default tiling only, compiles faster
-#define COTIX_LAUNCH_E(FS, BW) COTIX_LAUNCH(4, FS, BW);
+  hipError_t e;
+#ifdef COTIX_EW4_ONLY  // tooling builds (phase profile, ISA markers): the default tiling only
+  e = cxl::launch_step_ew4(ka, fs, mode, lds, st);
 #else
-#define COTIX_LAUNCH_E(FS, BW)                \
-  if (EW == 1) COTIX_LAUNCH(1, FS, BW);       \
-  else if (EW == 8) COTIX_LAUNCH(8, FS, BW);  \
-  else if (EW == 2) COTIX_LAUNCH(2, FS, BW);  \
-  else COTIX_LAUNCH(4, FS, BW);
+  if (EW == 1) e = cxl::launch_step_ew1(ka, fs, mode, lds, st);
+  else if (EW == 2) e = cxl::launch_step_ew2(ka, fs, mode, lds, st);
+  else if (EW == 8) e = cxl::launch_step_ew8(ka, fs, mode, lds, st);
+  else e = cxl::launch_step_ew4(ka, fs, mode, lds, st);
 #endif
-  if (mode == 2) {
-    COTIX_LAUNCH_E(FNS_ANALYTIC, 2)  // the host admits analytic scenes only
-  } else if (mode == 1) {
-    if ((fs & ~FNS_ANALYTIC) == 0) {
-      COTIX_LAUNCH_E(FNS_ANALYTIC, 1)
-    } else {
-      COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, 1)
-    }
-  } else if ((fs & ~FNS_ANALYTIC) == 0) {
-    COTIX_LAUNCH_E(FNS_ANALYTIC, 0)
-  } else if ((fs & FNS_CIRCLE_POLY) == 0) {
-    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX, 0)
-  } else {
-    COTIX_LAUNCH_E(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, 0)
-  }
-#undef COTIX_LAUNCH_E
-#undef COTIX_LAUNCH
+  if (e != hipSuccess) return hip_check(e, "step_kernel launch");
   return hip_check(hipGetLastError(), "step_kernel launch");
 }
 
 static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
                      int geom_stride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
-                     const float* dyn_reset, uint32_t* resets, cotix_stream_t stream) {
+                     const float* dyn_reset, uint32_t* resets, int32_t* chosen, int32_t* cells,
+                     cotix_stream_t stream) {
   if (check_step_args(scene, dyn, keys, geom, geom_stride, B, n_steps, stages, action, action_body)) return -1;
   if (!err) return fail("null argument");
   if (B == 0 || n_steps == 0) return 0;
@@ -384,6 +296,8 @@ static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* e
   ka.action_body = action_body;
   ka.dyn_reset = dyn_reset;
   ka.resets = resets;
+  ka.trace_chosen = chosen;
+  ka.trace_cells = cells;
   return launch(scene, ka, 0, stream);
 }
 
@@ -391,7 +305,7 @@ int cotix_step(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, co
                int B, int n_steps, float dt, int stages, const float* action, int action_body,
                cotix_stream_t stream) {
   return step_impl(scene, dyn, keys, err, geom, geom_stride, B, n_steps, dt, stages, action, action_body, nullptr,
-                   nullptr, stream);
+                   nullptr, nullptr, nullptr, stream);
 }
 
 int cotix_step_autoreset(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
@@ -399,7 +313,14 @@ int cotix_step_autoreset(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_
                          uint32_t* resets, cotix_stream_t stream) {
   if (!dyn_reset) return fail("dyn_reset required");
   return step_impl(scene, dyn, keys, err, geom, geom_stride, B, n_steps, dt, stages, nullptr, 0, dyn_reset, resets,
-                   stream);
+                   nullptr, nullptr, stream);
+}
+
+int cotix_step_ex(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
+                  int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                  const float* dyn_reset, uint32_t* resets, int32_t* chosen, int32_t* cells, cotix_stream_t stream) {
+  return step_impl(scene, dyn, keys, err, geom, geom_stride, B, n_steps, dt, stages, action, action_body, dyn_reset,
+                   resets, chosen, cells, stream);
 }
 
 int cotix_rollout(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,

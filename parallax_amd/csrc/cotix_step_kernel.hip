@@ -1,0 +1,125 @@
+// cotix_step_kernel.hip -- the fused step kernel (gfx950) for ONE envs-per-wave
+// tiling: compiled once per EW with -DCOTIX_EW=N (see cotix_launch.h); the
+// phase programs live in cotix_kernel.h, design notes there and in DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include "../../include/cotix_amd.h"
+#include "cotix_device.h"
+#include "cotix_kernel.h"
+#include "cotix_launch.h"
+
+#ifndef COTIX_EW
+#error "compile with -DCOTIX_EW=1|2|4|8"
+#endif
+
+using cxk::FNS_ANALYTIC;
+using cxk::FNS_CIRCLE_POLY;
+using cxk::FNS_CONVEX;
+using cxk::SceneDev;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// the fused step kernel: WPB independent waves per workgroup, EW envs per wave
+// ---------------------------------------------------------------------------
+using cxl::WPB;
+#ifdef COTIX_PHASE_PROF
+__device__ unsigned long long g_phase_cycles[cxk::PH_COUNT];
+#endif
+// one phase on this lane, then wave-local ordering before the next phase
+struct WaveRun {
+  int lane;
+#ifdef COTIX_PHASE_PROF
+  unsigned long long* acc;  // per-phase cycle accumulators (registers after inlining)
+  template <class F>
+  __device__ __forceinline__ void operator()(int ph, F f) const {
+    const unsigned long long t0 = clock64();
+    f(lane);
+    cxk::wave_sync();
+    acc[ph] += clock64() - t0;
+  }
+#elif defined(COTIX_ASM_MARKERS)  // tooling: phase markers in the ISA (tools/isa_phases.py)
+  template <class F>
+  __device__ __forceinline__ void operator()(int ph, F f) const {
+    asm volatile(";#PHASE_BEGIN %0" ::"s"(ph));
+    f(lane);
+    cxk::wave_sync();
+    asm volatile(";#PHASE_END %0" ::"s"(ph));
+  }
+#else
+  template <class F>
+  __device__ __forceinline__ void operator()(int, F f) const {
+    f(lane);
+    cxk::wave_sync();
+  }
+#endif
+};
+// MODE 0: step, 1: rollout forward (saves + return), 2: rollout backward
+template <int EW, int FNSET, int MODE>
+__global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
+  extern __shared__ uint32_t lds[];
+  const SceneDev* sc = a.sc;
+  const int nhot = a.sh.nhot;
+  for (int i = threadIdx.x; i < nhot; i += WPB * 64) lds[i] = sc->hot[i];
+  __syncthreads();
+  const cxk::Ctx c = cxk::make_ctx<EW>(a.sh);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int env0 = (blockIdx.x * WPB + wave) * EW;
+  if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
+  uint32_t* wbase = lds + nhot + wave * (c.L.S * EW + c.W.words);
+  const cxk::Tile<EW> t{wbase, lds, wbase + c.L.S * EW};
+#ifdef COTIX_PHASE_PROF
+  unsigned long long acc[cxk::PH_COUNT];
+  for (int q = 0; q < cxk::PH_COUNT; ++q) acc[q] = 0ull;
+  const WaveRun run{lane, acc};
+#else
+  const WaveRun run{lane};
+#endif
+  if (MODE == 2)
+    cxk::run_wave_backward<EW, FNSET>(a, c, t, env0, run);
+  else
+    cxk::run_wave<EW, FNSET, MODE == 1>(a, c, t, env0, run);
+#ifdef COTIX_PHASE_PROF
+  if (lane == 0)
+    for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);
+#endif
+}
+
+}  // namespace
+
+#define CXL_NAME2(n) launch_step_ew##n
+#define CXL_NAME(n) CXL_NAME2(n)
+hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st) {
+  constexpr int EW = COTIX_EW;
+  const dim3 grid((ka.B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);
+#define COTIX_LAUNCH(FS, BW) hipLaunchKernelGGL((step_kernel<EW, FS, BW>), grid, block, lds, st, ka)
+  if (mode == 2) {
+    COTIX_LAUNCH(FNS_ANALYTIC, 2);  // the host admits analytic scenes only
+  } else if (mode == 1) {
+    if ((fs & ~FNS_ANALYTIC) == 0)
+      COTIX_LAUNCH(FNS_ANALYTIC, 1);
+    else
+      COTIX_LAUNCH(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, 1);
+  } else if ((fs & ~FNS_ANALYTIC) == 0) {
+    COTIX_LAUNCH(FNS_ANALYTIC, 0);
+  } else if ((fs & FNS_CIRCLE_POLY) == 0) {
+    COTIX_LAUNCH(FNS_ANALYTIC | FNS_CONVEX, 0);
+  } else {
+    COTIX_LAUNCH(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, 0);
+  }
+#undef COTIX_LAUNCH
+  return hipGetLastError();
+}
+
+#ifdef COTIX_PHASE_PROF
+// profiling build only: per-phase cycles summed over waves since the last call (then reset)
+extern "C" int cotix_phase_cycles(unsigned long long* out, int n) {
+  unsigned long long h[cxk::PH_COUNT] = {};
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase_cycles), sizeof(h)) != hipSuccess) return -1;
+  unsigned long long z[cxk::PH_COUNT] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)) != hipSuccess) return -1;
+  for (int q = 0; q < n && q < cxk::PH_COUNT; ++q) out[q] = h[q];
+  return cxk::PH_COUNT;
+}
+#endif

@@ -26,15 +26,18 @@ class BatchedEnv:
         self.resets.zero_()
         return self.observation()
 
-    def step(self, n_steps=1, action=None, action_body=None):
+    def step(self, n_steps=1, action=None, action_body=None, trace=None):
+        """n_steps fused driver steps; action f32 [n_steps, B, 2] is added to the
+        velocity of `action_body` (default: the last body, the RoboCup ball)
+        after Euler.  With autoreset an env whose error bits trip restarts from
+        its reset state and keeps receiving actions.  trace: see World.step."""
         w = self.world
+        body = len(w.bodies) - 1 if action_body is None else action_body
         if self.autoreset:
-            if action is not None:
-                raise ValueError("autoreset and action are exclusive")
-            w.step(n_steps, self.dt, self.scenario.stages, dyn_reset=self.scenario.dyn_reset, resets=self.resets)
+            w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body,
+                   dyn_reset=self.scenario.dyn_reset, resets=self.resets, trace=trace)
         else:
-            body = len(w.bodies) - 1 if action_body is None else action_body
-            w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body)
+            w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body, trace=trace)
         return self.observation()
 
     def observation(self, out=None):

@@ -59,13 +59,18 @@ def robocup_bodies():
     ]
 
 
-def robocup_perturbation(B, seed=2, device="cuda"):
-    """The build's batched-reset scheme: env 0 is the
-    exact reference state; env e >= 1 gets, from split(PRNGKey(seed), B)[e] ->
-    (kp, kv, kw) = split(., 3): ball position U([-4.4,4.4] x [-2.9,2.9]),
-    velocity U([-2,2]^2), angular velocity U(-10,10).  Returns the ball's
-    [6, B] dynamic columns."""
-    k = jr.split(jr.PRNGKey(seed, device), B)
+def robocup_perturbation(B, seed=2, device="cuda", offset=0, total=None):
+    """The build's batched-reset scheme for the envs
+    with GLOBAL ids offset .. offset+B-1 of a `total`-env batch (default: B,
+    offset 0), so a rank's shard equals the same envs of one big run: global
+    env 0 is the exact reference state; env g >= 1 gets, from
+    split(PRNGKey(seed), total)[g] -> (kp, kv, kw) = split(., 3): ball position
+    U([-4.4,4.4] x [-2.9,2.9]), velocity U([-2,2]^2), angular velocity
+    U(-10,10).  Returns the ball's [6, B] dynamic columns."""
+    total = B if total is None else int(total)
+    if offset < 0 or offset + B > total:
+        raise ValueError("env range [offset, offset+B) outside the global batch")
+    k = jr.split(jr.PRNGKey(seed, device), total)[offset:offset + B].contiguous()
     kk = jr.split(k, 3)
     u = jr.uniform(kk[:, 0], 2)
     lo = torch.tensor([-4.4, -2.9], dtype=torch.float32, device=device)
@@ -74,23 +79,29 @@ def robocup_perturbation(B, seed=2, device="cuda"):
     vel = jr.uniform(kk[:, 1], 2, -2.0, 2.0)
     w = jr.uniform(kk[:, 2], None, -10.0, 10.0)
     cols = torch.stack([pos[:, 0], pos[:, 1], vel[:, 0], vel[:, 1], torch.zeros_like(w), w], 0)
-    cols[:, 0] = torch.tensor([0.0, 0.0, 1.0, 0.01, 0.0, 10.0], dtype=torch.float32, device=device)
+    if offset == 0 and B > 0:
+        cols[:, 0] = torch.tensor([0.0, 0.0, 1.0, 0.01, 0.0, 10.0], dtype=torch.float32, device=device)
     return cols
 
 
 class RoboCupEnv:
     """RoboCupEnv with a batch dimension.  ``keys``: collider keys [B, 2]
-    (default split(PRNGKey(3), B)); ``perturb``: apply robocup_perturbation."""
+    (default split(PRNGKey(3), total)[offset:offset+B]); ``perturb``: apply
+    robocup_perturbation.  ``env_offset`` / ``total_envs``: this batch holds the
+    envs with global ids env_offset .. env_offset+B-1 of a total_envs-env run
+    (a rank's shard); defaults: 0 and B."""
 
     stages = _ffi.STAGES_ROBOCUP
 
-    def __init__(self, batch=1, device="cuda", keys=None, perturb=False, perturb_seed=2):
+    def __init__(self, batch=1, device="cuda", keys=None, perturb=False, perturb_seed=2, env_offset=0,
+                 total_envs=None):
         self.bodies = robocup_bodies()
+        total = batch if total_envs is None else int(total_envs)
         if keys is None:
-            keys = jr.split(jr.PRNGKey(3, device), batch)
+            keys = jr.split(jr.PRNGKey(3, device), total)[env_offset:env_offset + batch].contiguous()
         self.world = World(self.bodies, batch, device, keys)
         if perturb:
-            self.world.dyn[4] = robocup_perturbation(batch, perturb_seed, device)
+            self.world.dyn[4] = robocup_perturbation(batch, perturb_seed, device, env_offset, total)
         self.dyn_reset = self.world.dyn.clone()
 
     # field green, goals yellow / blue, ball red; white field outlines, no
@@ -104,6 +115,58 @@ class RoboCupEnv:
         from . import render as R
         cmds = R.commands_bodies(self.bodies, self.colors, self.edge_colors)
         R.replay(painter, cmds, R.render(self.world) if prims is None else prims, env)
+
+
+# ---------------------------------------------------------------------------
+# BoxWorld: a generic finite-dynamics scene (NOT a reference scenario)
+# ---------------------------------------------------------------------------
+def box_world_bodies():
+    """Balls in an open box, built from the reference's own body/shape API
+    (AnyBody, UniversalShape, AABB, Circle): 3 static non-overlapping walls
+    (floor, left, right; elasticity 0.8, friction 0.3) and 4 balls of finite
+    mass and inertia.  Unlike RoboCup (whose overlapping static bodies drive
+    every env to NaN within two steps) every contact here has
+    finite operands, so it times the full-cost contact/resolution path.  The
+    ball parameters are env 0 of tests/golden/make_golden.box_world_bodies."""
+    walls = [AABB([-3.0, -3.2], [3.0, -2.0]), AABB([-4.0, -1.9], [-3.0, 3.0]), AABB([3.0, -1.9], [4.0, 3.0])]
+    bodies = [AnyBody(shape=UniversalShape(w), mass=INF, elasticity=0.8, friction_coefficient=0.3) for w in walls]
+    rng = np.random.default_rng(100)
+    for _ in range(4):
+        rng.uniform(size=4)  # (position, velocity: drawn per env on the device instead)
+        r, m, i = F(rng.uniform(0.3, 0.7)), F(rng.uniform(0.5, 2.0)), F(rng.uniform(0.2, 1.0))
+        rng.uniform(-5, 5)
+        e, f = F(rng.uniform(0.3, 1.0)), F(rng.uniform(0.1, 0.9))
+        bodies.append(AnyBody(shape=UniversalShape(Circle(r, [0.0, 0.0])), mass=float(m), inertia=float(i),
+                              elasticity=float(e), friction_coefficient=float(f)))
+    return bodies
+
+
+class BoxWorld:
+    """BoxWorld with a batch dimension: per env (global ids env_offset ..
+    env_offset+B-1 of total_envs) the 4 balls start at uniform positions in
+    [-2.8, 2.8] x [-1.5, 2.5], velocities U(-3, 3)^2 and spins U(-5, 5) drawn
+    from split(PRNGKey(seed), total)[id]; collider keys split(PRNGKey(seed+1),
+    total)[id].  Driver stages as RoboCup (Euler -> collider -> key split)."""
+
+    stages = _ffi.STAGES_ROBOCUP
+
+    def __init__(self, batch=1, device="cuda", seed=9, env_offset=0, total_envs=None):
+        self.bodies = box_world_bodies()
+        total = batch if total_envs is None else int(total_envs)
+        sl = slice(env_offset, env_offset + batch)
+        keys = jr.split(jr.PRNGKey(seed + 1, device), total)[sl].contiguous()
+        self.world = World(self.bodies, batch, device, keys)
+        kb = jr.split(jr.split(jr.PRNGKey(seed, device), total)[sl].contiguous(), 4)  # [B, 4, 2]: one key per ball
+        for k in range(4):
+            u = jr.uniform(kb[:, k].contiguous(), 5)
+            d = self.world.dyn[3 + k]
+            d[0] = u[:, 0] * 5.6 - 2.8
+            d[1] = u[:, 1] * 4.0 - 1.5
+            d[2] = u[:, 2] * 6.0 - 3.0
+            d[3] = u[:, 3] * 6.0 - 3.0
+            d[4] = 0.0
+            d[5] = u[:, 4] * 10.0 - 5.0
+        self.dyn_reset = self.world.dyn.clone()
 
 
 # ---------------------------------------------------------------------------

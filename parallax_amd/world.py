@@ -98,23 +98,38 @@ class World:
 
     # -- hot path ---------------------------------------------------------
     def step(self, n_steps=1, dt=1e-2, stages=_ffi.STAGES_ROBOCUP, action=None, action_body=0,
-             dyn_reset=None, resets=None):
-        """Fused driver step (examples/test_viz.py:24-44 / :61-69), n_steps times."""
+             dyn_reset=None, resets=None, trace=None):
+        """Fused driver step (examples/test_viz.py:24-44 / :61-69), n_steps times.
+
+        dyn_reset/resets: episode restarts on an error trip (cotix_step_autoreset
+        semantics; combinable with `action`).  trace: a dict that receives the
+        collider's per-step choices, "chosen" i32 [n_steps, n_bodies, B] (j* of
+        body i, cotix/_colliders.py:274-295) and "cells" i32 [n_steps, n_bodies,
+        n_bodies, B] (the winning scan candidate of all_contacts[i, j],
+        ind1 | ind2 << 9 | type << 18, -1 = empty; :208-268)."""
         s = _ffi.stream_ptr(self.device)
-        if dyn_reset is not None:
-            _ffi.check(_ffi.lib.cotix_step_autoreset(
-                self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.keys), _ffi.ptr(self.err), _ffi.ptr(self.geom),
-                self.geom_stride, self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(dyn_reset),
-                _ffi.ptr(resets), s), "cotix_step_autoreset")
-            return self
         if action is not None:
             action = action.to(self.device, torch.float32).contiguous()
             if action.shape != (n_steps, self.B, 2):
                 raise ValueError("action must be [n_steps, B, 2]")
-        _ffi.check(_ffi.lib.cotix_step(
+        if dyn_reset is not None and tuple(dyn_reset.shape) != tuple(self.dyn.shape):
+            raise ValueError("dyn_reset must have the state's shape [n_bodies, 6, B]")
+        chosen = cells = None
+        if trace is not None:
+            nb = len(self.bodies)
+            chosen = torch.empty(n_steps, nb, self.B, dtype=torch.int32, device=self.device)
+            cells = torch.empty(n_steps, nb, nb, self.B, dtype=torch.int32, device=self.device)
+            trace["chosen"], trace["cells"] = chosen, cells
+        if dyn_reset is None and trace is None:
+            _ffi.check(_ffi.lib.cotix_step(
+                self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.keys), _ffi.ptr(self.err),
+                _ffi.ptr(self.geom), self.geom_stride, self.B, int(n_steps), float(dt), int(stages),
+                _ffi.ptr(action), int(action_body), s), "cotix_step")
+            return self
+        _ffi.check(_ffi.lib.cotix_step_ex(
             self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.keys), _ffi.ptr(self.err), _ffi.ptr(self.geom),
-            self.geom_stride, self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(action), int(action_body), s),
-            "cotix_step")
+            self.geom_stride, self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(action), int(action_body),
+            _ffi.ptr(dyn_reset), _ffi.ptr(resets), _ffi.ptr(chosen), _ffi.ptr(cells), s), "cotix_step_ex")
         return self
 
     def step_state(self, dyn, keys, err, n_steps=1, dt=1e-2, stages=_ffi.STAGES_ROBOCUP, action=None,

@@ -106,6 +106,31 @@ int emu_step(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float
   return 0;
 }
 
+int emu_step_ex(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
+                int n_steps, float dt, int stages, const float* action, int action_body, const float* dyn_reset,
+                uint32_t* resets, int32_t* chosen, int32_t* cells, int E) {
+  EmuScene* s = static_cast<EmuScene*>(scene);
+  cxk::KArgs a{};
+  a.sc = &s->s;
+  a.dyn = dyn;
+  a.keys = keys;
+  a.err = err;
+  a.geom = geom;
+  a.gstride = gstride;
+  a.B = B;
+  a.n_steps = n_steps;
+  a.dt = dt;
+  a.stages = stages;
+  a.action = action;
+  a.action_body = action_body;
+  a.dyn_reset = dyn_reset;
+  a.resets = resets;
+  a.trace_chosen = chosen;
+  a.trace_cells = cells;
+  run_any(a, E, 0);
+  return 0;
+}
+
 int emu_rollout(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
                 int n_steps, float dt, int stages, const float* action, int action_body, const float* ret_w, float* ret,
                 float* saved_dyn, uint32_t* saved_keys, int E) {

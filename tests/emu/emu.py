@@ -15,6 +15,8 @@ def load(asan=False):
     lib.emu_scene_create.argtypes = [ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.POINTER(P_)]
     lib.emu_step.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                              ctypes.c_int, P_, ctypes.c_int, P_, P_, ctypes.c_int]
+    lib.emu_step_ex.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, ctypes.c_int]
     lib.emu_contacts.argtypes = [ctypes.c_int, ctypes.c_int, P_, P_, P_, P_]
     lib.emu_order_clockwise.argtypes = [P_, ctypes.c_int, ctypes.c_int]
     lib.emu_body_penetration.argtypes = [P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_]
@@ -67,6 +69,19 @@ def step(lib, h, dyn, keys, err, geom, gstride, n_steps, stages, dt=1e-2, E=16, 
         assert a.flags.c_contiguous
     lib.emu_step(h, _p(dyn), _p(keys), _p(err), _p(geom), gstride, B, n_steps, dt, stages, None, 0,
                  _p(dyn_reset), _p(resets), E)
+
+
+def step_ex(lib, h, dyn, keys, err, geom, gstride, n_steps, stages, nb, dt=1e-2, E=4, action=None, action_body=0,
+            dyn_reset=None, resets=None):
+    """step() with actions and the collider trace; returns (chosen i32
+    [n_steps, nb, B], cells i32 [n_steps, nb, nb, B])."""
+    B = dyn.shape[2]
+    ch = np.full((n_steps, nb, B), -7, np.int32)
+    cl = np.full((n_steps, nb, nb, B), -7, np.int32)
+    act = None if action is None else np.ascontiguousarray(action, np.float32)
+    lib.emu_step_ex(h, _p(dyn), _p(keys), _p(err), _p(geom), gstride, B, n_steps, dt, stages, _p(act), action_body,
+                    _p(dyn_reset), _p(resets), _p(ch), _p(cl), E)
+    return ch, cl
 
 
 def rollout(lib, h, dyn, keys, err, geom, gstride, stages, actions, action_body, w, dt=1e-2, E=4):

@@ -148,7 +148,7 @@ def robocup_perturb(B, seed=2):
 
 def trace(make_bodies, step_fn, keys, T, init=None):
     B = len(keys)
-    dyn, ks, errs, chosen = [], [], [], []
+    dyn, ks, errs, chosen, cells = [], [], [], [], []
     envs = []
     for e in range(B):
         b = make_bodies(e)
@@ -160,18 +160,20 @@ def trace(make_bodies, step_fn, keys, T, init=None):
     d_t = [[np.array([x.dyn() for x in envs[e]], F) for e in range(B)]]
     k_t = [np.array(cur)]
     for _ in range(T):
-        er_t, ch_t = [], []
+        er_t, ch_t, cl_t = [], [], []
         for e in range(B):
             err, tr = G.ErrorFlag(), {}
             envs[e], cur[e] = step_fn(envs[e], cur[e], D0, err, tr)
             er_t.append(err.bits)
             ch_t.append(tr["chosen"])
+            cl_t.append(tr["cells"])
         d_t.append([np.array([x.dyn() for x in envs[e]], F) for e in range(B)])
         k_t.append(np.array(cur))
         errs.append(er_t)
         chosen.append(ch_t)
+        cells.append(cl_t)
     return dict(dyn=np.array(d_t, F), keys=np.array(k_t, np.uint32), err=np.array(errs, np.int32),
-                chosen=np.array(chosen, np.int32))
+                chosen=np.array(chosen, np.int32), cells=np.array(cells, np.int32))
 
 
 def make_robocup(B=8, T=12):

@@ -1,7 +1,9 @@
 """Kernel-logic parity on CPU: the fused step kernel's phase code
 (parallax_amd/csrc/cotix_kernel.h), compiled for the host by the test-only
 emulation harness (tests/emu), must reproduce the golden oracle traces bit
-for bit -- the same bar as the GPU tests -- for every envs-per-wave tiling."""
+for bit -- the same bar as the GPU tests -- for every envs-per-wave tiling,
+including the collider's contact choices (j* per body and the winning
+candidate of every all_contacts cell, cotix/_colliders.py:208-295)."""
 import os
 import subprocess
 import sys
@@ -40,8 +42,11 @@ def run_trace(emu, lib, bodies, geom_rows, tr, stages, EW, per_env_geom):
     dyn = np.ascontiguousarray(tr["dyn"][0].transpose(1, 2, 0))
     keys = np.ascontiguousarray(tr["keys"][0]).astype(np.uint32)
     err = np.zeros(B, np.uint32)
+    nb = len(bodies)
     for t in range(T):
-        emu.step(lib, h, dyn, keys, err, geom, gstride, 1, stages, E=EW)
+        ch, cl = emu.step_ex(lib, h, dyn, keys, err, geom, gstride, 1, stages, nb, E=EW)
+        assert np.array_equal(ch[0].T, tr["chosen"][t]), "chosen step %d" % t
+        assert np.array_equal(cl[0].transpose(2, 0, 1), tr["cells"][t]), "cells step %d" % t
         got = dyn.transpose(2, 0, 1)
         assert same_f32(got, tr["dyn"][t + 1]), "step %d" % t
         assert np.array_equal(keys, tr["keys"][t + 1]), "keys step %d" % t
@@ -73,7 +78,7 @@ def test_emu_box_world_trace(emu_lib):
     import make_golden as mg
     tr = np.load(os.path.join(GOLD, "box_world_trace.npz"))
     for e in range(tr["dyn"].shape[1]):
-        sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err")}
+        sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err", "chosen", "cells")}
         run_trace(emu, lib, mg.box_world_bodies(e), None, sub, 1 | 4 | 16, 2, False)
 
 
@@ -156,6 +161,71 @@ def test_emu_robocup_autoreset_vs_cport(emu_lib):
     assert same_f32(got[0], want[0])
     for g, w in zip(got[1:], want[1:]):
         assert np.array_equal(g, w)
+
+
+@pytest.mark.parametrize("EW", [2, 4, 8])
+def test_emu_trace_actions_autoreset_vs_cport(emu_lib, EW):
+    """cotix_step_ex on CPU: actions + episode restarts + the collider trace
+    (chosen partner per body, winning candidate per cell) of the kernel logic
+    == the C port, 96 perturbed RoboCup envs x 2 launches of 18 fused steps."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    from cotix_oracle import physics as P
+    if not os.path.exists(cport.LIB):
+        pytest.skip("oracle C port not built (make -C oracle)")
+    clib = cport.load()
+    B, T = 96, 18
+    dyn, keys = cport.robocup_batch(B)
+    dyn, keys = np.ascontiguousarray(dyn, np.float32), np.ascontiguousarray(keys, np.uint32)
+    reset = dyn.copy()
+    h, geom = emu.oracle_scene(lib, P.robocup_bodies())
+    sc = cport.Scene(clib, P.robocup_bodies())
+    rng = np.random.default_rng(EW)
+    got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32), np.zeros(B, np.uint32)]
+    for _ in range(2):
+        act = np.ascontiguousarray((rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32))
+        gch, gcl = emu.step_ex(lib, h, got[0], got[1], got[2], geom, 0, T, 1 | 4 | 16, 5, E=EW, action=act,
+                               action_body=4, dyn_reset=reset, resets=got[3])
+        wch, wcl = sc.step_ex(want[0], want[1], want[2], T, cport.STAGES_ROBOCUP, None, act, 4, reset, want[3],
+                              trace=True)
+        assert np.array_equal(gch, wch)
+        assert np.array_equal(gcl, wcl)
+    assert want[3].sum() > 0 and (wcl >= 0).any()
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)
+
+
+def test_emu_lunar_trace_vs_cport(emu_lib):
+    """LunarLander (GJK/EPA contacts) collider trace of the kernel logic == the
+    C port: 24 envs with terrain per env, half of them dropped onto the ground."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    if not os.path.exists(cport.LIB):
+        pytest.skip("oracle C port not built (make -C oracle)")
+    clib = cport.load()
+    B, T = 24, 10
+    tk = prng.split(prng.PRNGKey(0), B)
+    rows = np.ascontiguousarray(np.stack([emu.oracle_scene(lib, P.lunar_lander_bodies(k))[1] for k in tk]))
+    h, _ = emu.oracle_scene(lib, P.lunar_lander_bodies(tk[0]))
+    sc = cport.Scene(clib, P.lunar_lander_bodies(tk[0]))
+    base = np.array([b.dyn() for b in P.lunar_lander_bodies(tk[0])], np.float32)
+    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
+    dyn[:3, 1, ::2] -= np.float32(6.3)
+    dyn[:3, 3, ::2] = np.float32(-0.3)
+    keys = np.ascontiguousarray(prng.split(prng.PRNGKey(1), B)).astype(np.uint32)
+    got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    gch, gcl = emu.step_ex(lib, h, *got, rows, rows.shape[1], T, cport.STAGES_LUNAR, 4, E=4)
+    wch, wcl = sc.step_ex(*want, T, cport.STAGES_LUNAR, rows, trace=True)
+    assert (wcl >= 0).sum() > B  # contacts were found
+    assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+    assert same_f32(got[0], want[0])
 
 
 def test_perfect_vertex_threshold():

@@ -2,8 +2,12 @@
 
 Bar (DESIGN.md "Parity"): float32 results bit-identical to the oracle --
 equal bit patterns, and NaN exactly where the oracle has NaN (NaN payloads
-are not compared) -- plus identical error bits, keys and contact choices.
-This is stricter than north_star's 1e-5 relative tolerance.
+are not compared) -- plus identical error bits, keys and contact choices:
+the collider trace of cotix_step_ex (the chosen partner j* of every body at
+every step, cotix/_colliders.py:274-295, and the winning scan candidate of
+every all_contacts cell, :208-268) is compared with the golden traces and
+the C port wherever a trajectory is.  This is stricter than north_star's
+1e-5 relative tolerance.
 """
 import os
 
@@ -124,10 +128,13 @@ def test_order_clockwise_operator(torch_cuda):
 # multi-step traces (fused kernel) vs the golden oracle traces
 # ---------------------------------------------------------------------------
 def _check_trace(world, tr, stages, T, per_step=True):
+    """State, keys, error bits AND the collider's choices (j* per body, winning
+    candidate per cell) of every step against the golden oracle trace."""
     import torch
     if per_step:
         for t in range(T):
-            world.step(1, 1e-2, stages)
+            trc = {}
+            world.step(1, 1e-2, stages, trace=trc)
             torch.cuda.synchronize()
             dyn = world.dyn.permute(2, 0, 1).cpu().numpy()
             assert same_f32(dyn, tr["dyn"][t + 1]), "step %d: %s" % (t, diff_report(dyn, tr["dyn"][t + 1]))
@@ -136,12 +143,17 @@ def _check_trace(world, tr, stages, T, per_step=True):
             err = world.err.cpu().numpy()
             want_err = np.bitwise_or.reduce(tr["err"][: t + 1], axis=0)
             assert np.array_equal(err, want_err), "step %d err %s vs %s" % (t, err, want_err)
+            assert np.array_equal(trc["chosen"][0].T.cpu().numpy(), tr["chosen"][t]), "step %d chosen" % t
+            assert np.array_equal(trc["cells"][0].permute(2, 0, 1).cpu().numpy(), tr["cells"][t]), "step %d cells" % t
     else:
-        world.step(T, 1e-2, stages)
+        trc = {}
+        world.step(T, 1e-2, stages, trace=trc)
         torch.cuda.synchronize()
         dyn = world.dyn.permute(2, 0, 1).cpu().numpy()
         assert same_f32(dyn, tr["dyn"][T]), diff_report(dyn, tr["dyn"][T])
         assert np.array_equal(world.keys.cpu().numpy().view(np.uint32), tr["keys"][T])
+        assert np.array_equal(trc["chosen"].permute(0, 2, 1).cpu().numpy(), tr["chosen"][:T]), "fused chosen"
+        assert np.array_equal(trc["cells"].permute(0, 3, 1, 2).cpu().numpy(), tr["cells"][:T]), "fused cells"
 
 
 @pytest.mark.parametrize("per_step", [True, False])
@@ -207,7 +219,7 @@ def test_box_world_trace(torch_cuda):
                                      angular_velocity=b.angular_velocity, elasticity=b.elasticity,
                                      friction_coefficient=b.friction_coefficient))
         w = pa.World(bodies, 1, "cuda", torch.tensor(u32_to_i32(tr["keys"][0][e:e + 1]), device="cuda"))
-        sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err")}
+        sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err", "chosen", "cells")}
         _check_trace(w, sub, pa._ffi.STAGES_ROBOCUP, T, per_step=True)
 
 
@@ -325,31 +337,81 @@ def cport_lib():
     return cport, cport.load()
 
 
+def _robocup_vs_cport(torch, pa, cport, lib, env, dyn, keys, launches, T, actions=None):
+    """Steps a BatchedEnv (autoreset) and the C port side by side; compares
+    state, keys, err, restart counts and the collider trace of every launch."""
+    from cotix_oracle import physics as P
+    B = dyn.shape[2]
+    reset = dyn.copy()
+    err = np.zeros(B, np.uint32)
+    resets = np.zeros(B, np.uint32)
+    sc = cport.Scene(lib, P.robocup_bodies())
+    for q in range(launches):
+        act = None if actions is None else actions[q]
+        trc = {}
+        env.step(T, action=None if act is None else torch.tensor(act, device="cuda"), trace=trc)
+        wch, wcl = sc.step_ex(dyn, keys, err, T, cport.STAGES_ROBOCUP, None, act, 4, reset, resets, trace=True,
+                              nthreads=16)
+        torch.cuda.synchronize()
+        assert np.array_equal(trc["chosen"].cpu().numpy(), wch), "launch %d chosen" % q
+        assert np.array_equal(trc["cells"].cpu().numpy(), wcl), "launch %d cells" % q
+    got = env.world.dyn.cpu().numpy()
+    assert same_f32(got, dyn), diff_report(got, dyn)
+    assert np.array_equal(env.world.keys.cpu().numpy().view(np.uint32), keys)
+    assert np.array_equal(env.world.err.cpu().numpy().view(np.uint32), err)
+    assert np.array_equal(env.resets.cpu().numpy().view(np.uint32), resets)
+    assert resets.sum() > 0
+    return wch, wcl
+
+
 def test_robocup_4096_all_envs_vs_cport_autoreset(torch_cuda, cport_lib):
     """The bench workload itself: 4096 perturbed envs, 3 launches x 16 fused
-    steps with episode restarts, compared for every env."""
+    steps with episode restarts, compared for every env -- state, keys, error
+    bits, restarts and every contact choice (j* per body, winner per cell)."""
     torch = torch_cuda
     import parallax_amd as pa
-    from cotix_oracle import physics as P
     cport, lib = cport_lib
     B = 4096
     env = pa.BatchedEnv(pa.RoboCupEnv(batch=B, device="cuda", perturb=True), autoreset=True)
     env.reset()
     dyn = np.ascontiguousarray(env.world.dyn.cpu().numpy())
     keys = np.ascontiguousarray(env.world.keys.cpu().numpy().view(np.uint32))
-    reset = dyn.copy()
-    err = np.zeros(B, np.uint32)
-    resets = np.zeros(B, np.uint32)
-    sc = cport.Scene(lib, P.robocup_bodies())
-    for _ in range(3):
-        env.step(16)
-        sc.step(dyn, keys, err, 16, cport.STAGES_ROBOCUP, None, reset, resets, nthreads=8)
-    torch.cuda.synchronize()
-    assert same_f32(env.world.dyn.cpu().numpy(), dyn), diff_report(env.world.dyn.cpu().numpy(), dyn)
-    assert np.array_equal(env.world.keys.cpu().numpy().view(np.uint32), keys)
-    assert np.array_equal(env.world.err.cpu().numpy().view(np.uint32), err)
-    assert np.array_equal(env.resets.cpu().numpy().view(np.uint32), resets)
-    assert resets.sum() > 0
+    ch, cl = _robocup_vs_cport(torch, pa, cport, lib, env, dyn, keys, 3, 16)
+    assert (ch != np.arange(5)[None, :, None]).any() and (cl >= 0).any()
+
+
+def test_robocup_actions_with_autoreset_vs_cport(torch_cuda, cport_lib):
+    """An RL loop: BatchedEnv.step(action) with autoreset (ball dv actions
+    N(0, 0.1^2)), 4096 envs, 2 launches x 12 steps, vs the C port."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    cport, lib = cport_lib
+    B, T = 4096, 12
+    env = pa.BatchedEnv(pa.RoboCupEnv(batch=B, device="cuda", perturb=True), autoreset=True)
+    env.reset()
+    dyn = np.ascontiguousarray(env.world.dyn.cpu().numpy())
+    keys = np.ascontiguousarray(env.world.keys.cpu().numpy().view(np.uint32))
+    rng = np.random.default_rng(12)
+    acts = [np.ascontiguousarray((rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32)) for _ in range(2)]
+    _robocup_vs_cport(torch, pa, cport, lib, env, dyn, keys, 2, T, acts)
+
+
+def test_config4_shard_8192_vs_cport(torch_cuda, cport_lib):
+    """BASELINE config 4 on one GPU: the per-GPU shard of the 65,536-env run
+    (B = 8192, global ids 3*8192 .. 4*8192-1, built from those ids as bench.py
+    --gpus 8 builds rank 3) with restarts, every env vs the C port fed the
+    same global ids; 2 launches x 16 steps."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    cport, lib = cport_lib
+    B, rank, world = 8192, 3, 8
+    env = pa.BatchedEnv(pa.RoboCupEnv(batch=B, device="cuda", perturb=True, env_offset=rank * B,
+                                      total_envs=world * B), autoreset=True)
+    env.reset()
+    dyn, keys = cport.robocup_batch(B, offset=rank * B, total=world * B)
+    assert same_f32(env.world.dyn.cpu().numpy(), dyn), "shard reset state"
+    assert np.array_equal(env.world.keys.cpu().numpy().view(np.uint32), keys), "shard keys"
+    _robocup_vs_cport(torch, pa, cport, lib, env, np.ascontiguousarray(dyn), np.ascontiguousarray(keys), 2, 16)
 
 
 def test_lunar_4096_all_envs_vs_cport(torch_cuda, cport_lib):
@@ -370,13 +432,55 @@ def test_lunar_4096_all_envs_vs_cport(torch_cuda, cport_lib):
     keys = np.ascontiguousarray(ll.world.keys.cpu().numpy().view(np.uint32))
     geom = np.ascontiguousarray(ll.world.geom.cpu().numpy())
     err = np.zeros(B, np.uint32)
-    ll.world.step(T, 1e-2, ll.stages)
+    trc = {}
+    ll.world.step(T, 1e-2, ll.stages, trace=trc)
     sc = cport.Scene(lib, P.lunar_lander_bodies(tkeys[0]))
-    sc.step(dyn, keys, err, T, cport.STAGES_LUNAR, geom, nthreads=8)
+    wch, wcl = sc.step_ex(dyn, keys, err, T, cport.STAGES_LUNAR, geom, trace=True, nthreads=16)
     torch.cuda.synchronize()
     got = ll.world.dyn.cpu().numpy()
     assert same_f32(got, dyn), diff_report(got, dyn)
     assert np.array_equal(ll.world.keys.cpu().numpy().view(np.uint32), keys)
+    assert np.array_equal(ll.world.err.cpu().numpy().view(np.uint32), err)
+    assert (wcl >= 0).sum() > B
+    assert np.array_equal(trc["chosen"].cpu().numpy(), wch)
+    assert np.array_equal(trc["cells"].cpu().numpy(), wcl)
+
+
+def test_config1_lunar_single_env_10000_steps_vs_cport(torch_cuda, cport_lib):
+    """BASELINE config 1 (examples/test_viz.py:24-48): one LunarLander env,
+    terrain PRNGKey(0), collider key chain from PRNGKey(0), dt 1e-2, gravity
+    0.002, 10,000 driver steps -- the GPU (20 launches x 500 fused steps) vs
+    the C port bit for bit: the state after every launch and the collider's
+    choices at every one of the 10,000 steps."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    cport, lib = cport_lib
+    ll = pa.LunarLander(batch=1, device="cuda")  # key PRNGKey(0); collider key PRNGKey(0)
+    sc = cport.Scene(lib, P.lunar_lander_bodies(prng.PRNGKey(0)))
+    dyn = np.ascontiguousarray(ll.world.dyn.cpu().numpy())
+    want0 = np.array([b.dyn() for b in P.lunar_lander_bodies(prng.PRNGKey(0))], np.float32)[:, :, None]
+    assert same_f32(dyn, want0)
+    keys = np.ascontiguousarray(ll.world.keys.cpu().numpy().view(np.uint32))
+    assert keys.tolist() == [[0, 0]]
+    geom = np.ascontiguousarray(ll.world.geom.cpu().numpy()[None] if ll.world.geom.dim() == 1
+                                else ll.world.geom.cpu().numpy())
+    err = np.zeros(1, np.uint32)
+    contacts = 0
+    for q in range(20):
+        trc = {}
+        ll.world.step(500, 1e-2, ll.stages, trace=trc)
+        wch, wcl = sc.step_ex(dyn, keys, err, 500, cport.STAGES_LUNAR, geom, trace=True, nthreads=1)
+        torch.cuda.synchronize()
+        got = ll.world.dyn.cpu().numpy()
+        assert same_f32(got, dyn), "after step %d: %s" % (500 * (q + 1), diff_report(got, dyn))
+        assert np.array_equal(ll.world.keys.cpu().numpy().view(np.uint32), keys)
+        assert np.array_equal(ll.world.err.cpu().numpy().view(np.uint32), err)
+        assert np.array_equal(trc["chosen"].cpu().numpy(), wch), "chosen, launch %d" % q
+        assert np.array_equal(trc["cells"].cpu().numpy(), wcl), "cells, launch %d" % q
+        contacts += int((wcl >= 0).sum())
+    assert contacts > 0  # the lander reached the terrain (GJK/EPA contacts)
 
 
 # ---------------------------------------------------------------------------
@@ -692,26 +796,29 @@ def test_empty_and_negative_sizes(torch_cuda):
 
 
 def test_rank_shards_concatenate_to_single_run(torch_cuda):
-    """SURVEY 8(e) on the GPU: the envs of a 4-rank run (rank r owns global
-    envs [r*B/4, (r+1)*B/4) with its slice of the global key split, as
-    bench.py shards them) concatenate to the single-device run bit for bit."""
+    """SURVEY 8(e) on the GPU: each of 4 ranks BUILDS its shard from its global
+    env ids with bench.py's constructor (RoboCupEnv(env_offset=r*n,
+    total_envs=B): keys and ball perturbations sliced from one global split,
+    only global env 0 unperturbed) and steps it; the shards concatenate to the
+    single-device run bit for bit, collider choices included."""
     torch = torch_cuda
     import parallax_amd as pa
     B, R, T = 256, 4, 8
-    keys = pa.random.split(pa.random.PRNGKey(3, torch.device("cuda")), B)
-    full = pa.RoboCupEnv(batch=B, device="cuda", keys=keys.clone(), perturb=True)
-    init = full.world.dyn.clone()
-    full.world.step(T, 1e-2, full.stages)
-    parts_dyn, parts_keys, parts_err = [], [], []
+    full = pa.RoboCupEnv(batch=B, device="cuda", perturb=True)
+    ftr = {}
+    full.world.step(T, 1e-2, full.stages, trace=ftr)
+    parts = []
     n = B // R
     for r in range(R):
-        sh = pa.RoboCupEnv(batch=n, device="cuda", keys=keys[r * n:(r + 1) * n].clone(), perturb=True)
-        sh.world.dyn.copy_(init[:, :, r * n:(r + 1) * n])
-        sh.world.step(T, 1e-2, sh.stages)
-        parts_dyn.append(sh.world.dyn)
-        parts_keys.append(sh.world.keys)
-        parts_err.append(sh.world.err)
+        sh = pa.RoboCupEnv(batch=n, device="cuda", perturb=True, env_offset=r * n, total_envs=B)
+        tr = {}
+        sh.world.step(T, 1e-2, sh.stages, trace=tr)
+        parts.append((sh.world.dyn, sh.world.keys, sh.world.err, tr["chosen"], tr["cells"]))
     torch.cuda.synchronize()
-    assert same_f32(torch.cat(parts_dyn, 2).cpu().numpy(), full.world.dyn.cpu().numpy())
-    assert torch.equal(torch.cat(parts_keys), full.world.keys)
-    assert torch.equal(torch.cat(parts_err), full.world.err)
+    assert same_f32(torch.cat([p[0] for p in parts], 2).cpu().numpy(), full.world.dyn.cpu().numpy())
+    assert torch.equal(torch.cat([p[1] for p in parts]), full.world.keys)
+    assert torch.equal(torch.cat([p[2] for p in parts]), full.world.err)
+    assert torch.equal(torch.cat([p[3] for p in parts], 2), ftr["chosen"])
+    assert torch.equal(torch.cat([p[4] for p in parts], 3), ftr["cells"])
+    # rank 1..3 shards are not copies of rank 0's (the bug bench.py once had)
+    assert not torch.equal(parts[0][0][4], parts[1][0][4])

@@ -1,6 +1,7 @@
 """Multi-GPU path on CPU: world_size-2 gloo.  Each rank owns a contiguous env
-range (global ids rank*B .. rank*B+B-1, collider keys from ONE global
-split, as bench.py does), steps it with the fused kernel's logic (host
+range (global ids rank*B .. rank*B+B-1) and BUILDS it itself from those ids
+(collider keys and ball perturbations from ONE global split, only global env
+0 unperturbed -- the sharded constructor bench.py uses), steps it with the fused kernel's logic (host
 emulation, tests/emu) and all-gathers the observation tensor (the north
 star's RCCL all-gather, here over gloo).  The gathered result must equal a
 single-rank run over all envs bit for bit: envs are independent, so the
@@ -26,7 +27,8 @@ def _setup_paths():
 
 
 def _initial_state(B):
-    """RoboCup reset state for B envs (ball perturbed per env) + global keys."""
+    """RoboCup reset state for B envs (ball perturbed per env) + global keys,
+    built by the golden generator (independent of the sharded constructor)."""
     _setup_paths()
     import make_golden as mg
     from cotix_oracle import physics as P
@@ -39,6 +41,14 @@ def _initial_state(B):
         dyn[:, :, e] = np.array(d, np.float32)
     keys = np.ascontiguousarray(prng.split(prng.PRNGKey(3), B)).astype(np.uint32)
     return dyn, keys
+
+
+def _shard_state(rank):
+    """This rank's shard from its global env ids only (cport.robocup_batch with
+    offset/total: the oracle side of RoboCupEnv(env_offset, total_envs))."""
+    _setup_paths()
+    from cotix_oracle import cport
+    return cport.robocup_batch(B_LOCAL, offset=rank * B_LOCAL, total=B_LOCAL * WORLD)
 
 
 def _run(dyn, keys):
@@ -58,9 +68,7 @@ def _worker(rank, port, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
-    dyn_all, keys_all = _initial_state(B_LOCAL * WORLD)
-    sl = slice(rank * B_LOCAL, (rank + 1) * B_LOCAL)
-    dyn, keys, err = _run(dyn_all[:, :, sl], keys_all[sl])
+    dyn, keys, err = _run(*_shard_state(rank))
     obs = torch.from_numpy(np.ascontiguousarray(dyn.transpose(2, 0, 1)))  # [B_local, nb, 6]
     gathered = torch.empty(WORLD * B_LOCAL, 5, 6)
     dist.all_gather_into_tensor(gathered, obs)
@@ -81,6 +89,21 @@ def test_two_rank_shards_equal_single_rank(tmp_path):
     na, nb = np.isnan(gathered), np.isnan(ref)
     assert np.array_equal(na, nb)
     assert np.array_equal(gathered[~na].view(np.uint32), ref[~nb].view(np.uint32))
+
+
+def test_sharded_constructor_matches_global_batch():
+    """Each rank's self-built shard is exactly its slice of the global batch:
+    rank 1's envs are perturbed (not copies of rank 0's), and only global env
+    0 holds the reference state."""
+    dyn_all, keys_all = _initial_state(B_LOCAL * WORLD)
+    for r in range(WORLD):
+        d, k = _shard_state(r)
+        sl = slice(r * B_LOCAL, (r + 1) * B_LOCAL)
+        assert np.array_equal(d.view(np.uint32), dyn_all[:, :, sl].view(np.uint32))
+        assert np.array_equal(k, keys_all[sl])
+    d1, _ = _shard_state(1)
+    d0, _ = _shard_state(0)
+    assert not np.array_equal(d0[4], d1[4])
 
 
 def test_global_key_slicing_matches_bench():

@@ -1,5 +1,7 @@
 """The C port of the oracle (bench's CPU baseline and fast checker) must
-reproduce the Python oracle's golden traces and contact fixtures bit for bit."""
+reproduce the Python oracle's golden traces -- state, keys, error bits and
+the collider's contact choices (chosen partner per body, winning candidate
+per cell) -- and contact fixtures bit for bit."""
 import os
 import subprocess
 
@@ -28,7 +30,9 @@ def _trace(sc, tr, stages, geom=None):
     keys = np.ascontiguousarray(tr["keys"][0]).astype(np.uint32)
     err = np.zeros(dyn.shape[2], np.uint32)
     for t in range(tr["err"].shape[0]):
-        sc.step(dyn, keys, err, 1, stages, geom, nthreads=2)
+        ch, cl = sc.step_ex(dyn, keys, err, 1, stages, geom, trace=True, nthreads=2)
+        assert np.array_equal(ch[0].T, tr["chosen"][t]), "chosen step %d" % t
+        assert np.array_equal(cl[0].transpose(2, 0, 1), tr["cells"][t]), "cells step %d" % t
         assert same_f32(dyn.transpose(2, 0, 1), tr["dyn"][t + 1]), "step %d" % t
         assert np.array_equal(keys, tr["keys"][t + 1])
         assert np.array_equal(err, np.bitwise_or.reduce(tr["err"][: t + 1], axis=0))
@@ -56,7 +60,7 @@ def test_cport_box_world(cp):
     import make_golden as mg
     tr = np.load(os.path.join(GOLD, "box_world_trace.npz"))
     for e in range(tr["dyn"].shape[1]):
-        sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err")}
+        sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err", "chosen", "cells")}
         _trace(cport.Scene(lib, mg.box_world_bodies(e)), sub, cport.STAGES_ROBOCUP)
 
 

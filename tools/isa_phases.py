@@ -1,14 +1,14 @@
 """Static instruction counts per phase of the step kernel (perf tooling).
 Build the ISA with phase markers, then split it:
   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -std=c++17 --cuda-device-only -S \
-      -DCOTIX_ASM_MARKERS -DCOTIX_EW4_ONLY parallax_amd/csrc/cotix_step.hip -o /tmp/m.s
+      -DCOTIX_ASM_MARKERS -DCOTIX_EW=4 parallax_amd/csrc/cotix_step_kernel.hip -o /tmp/m.s
   python tools/isa_phases.py /tmp/m.s step_kernelILi4ELi1ELi0E"""
 import re
 import sys
 from collections import Counter, defaultdict
 
 NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
-         "adj", "F", "K", "E1", "R"]
+         "adj", "F", "K", "E1", "R", "trace"]
 src, pat = sys.argv[1], sys.argv[2]
 lines = open(src).read().split("\n")
 body, cur = [], False

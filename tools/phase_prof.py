@@ -6,20 +6,18 @@ import argparse
 import ctypes
 import json
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "parallax_amd", "_lib", "libcotix_amd_prof.so")
 NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
-         "adj", "F", "K", "E1", "R"]
+         "adj", "F", "K", "E1", "R", "trace"]
 
 
 def build():
-    src = os.path.join(ROOT, "parallax_amd", "csrc", "cotix_step.hip")
-    cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", "-std=c++17",
-           "-fPIC", "-shared", "-DCOTIX_PHASE_PROF", "-DCOTIX_EW4_ONLY", src, "-o", LIB]
-    subprocess.run(cmd, check=True)
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+    g.build_hip(out=LIB, defines=("COTIX_PHASE_PROF", "COTIX_EW4_ONLY"), ews=(4,))
 
 
 def main():

@@ -73,6 +73,14 @@ enum {
   COTIX_STAGE_COLLIDER = 4,     /* RandomizedCollider.resolve(bodies, key)    */
   COTIX_STAGE_LUNAR = 8,        /* LunarLander.step joint constraints          */
   COTIX_STAGE_ADVANCE_KEY = 16, /* key = split(key)[0]                        */
+  /* broadphase of the collider's polygon contacts (opt-in, results unchanged):
+   * a polygon x polygon / AABB x polygon pair whose world AABBs are separated
+   * by more than 2^-8 * S + 2^-16 (S = the pair's largest |coordinate|)
+   * skips GJK, EPA and the contact points -- such a pair's reference contact
+   * point is NaN.  The caller certifies that every polygon's interior angles
+   * are >= 0.5 degrees (the condition of the argument);
+   * parallax_amd.World checks its geometry and sets the bit itself. */
+  COTIX_STAGE_BROADPHASE = 32,
   COTIX_STAGES_ROBOCUP = 1 | 4 | 16,
   COTIX_STAGES_LUNAR = 1 | 2 | 4 | 8 | 16
 };

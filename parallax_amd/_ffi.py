@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("COTIX_AMD_LIB", os.path.join(_HERE, "_lib", "libcotix
 CIRCLE, AABB, POLYGON, POLYGON3, POLYGON4, POLYGON5, POLYGON6 = range(7)
 FN_AABB_AABB, FN_CIRCLE_CIRCLE, FN_CIRCLE_AABB, FN_POLY_POLY, FN_AABB_POLY, FN_CIRCLE_POLY = range(6)
 STAGE_EULER, STAGE_GRAVITY, STAGE_COLLIDER, STAGE_LUNAR, STAGE_ADVANCE_KEY = 1, 2, 4, 8, 16
+STAGE_BROADPHASE = 32  # polygon-pair broadphase, results unchanged (include/cotix_amd.h)
 STAGES_ROBOCUP = STAGE_EULER | STAGE_COLLIDER | STAGE_ADVANCE_KEY
 STAGES_LUNAR = STAGE_EULER | STAGE_GRAVITY | STAGE_COLLIDER | STAGE_LUNAR | STAGE_ADVANCE_KEY
 ERR_CIRCLE_AABB_CCP = 1

@@ -234,6 +234,13 @@ CX_DEV uint32_t f2u(float f) {
   memcpy(&u, &f, 4);
   return u;
 }
+// c ? a : b on the bit patterns (a select between two elements of a private
+// array can be rewritten by LLVM into a select of their ADDRESSES and a load
+// from a scratch copy; the masked OR keeps both operands in registers)
+CX_DEV float bsel(bool c, float a, float b) {
+  const uint32_t m = 0u - (uint32_t)c;
+  return __uint_as_float((f2u(a) & m) | (f2u(b) & ~m));
+}
 // vertex k, k varying per lane (0 <= k < MAXV): masked OR of the bit
 // patterns (a plain select chain gets rewritten by LLVM into an indexed
 // load from a scratch copy of the array); constant-folds for constant k
@@ -923,8 +930,8 @@ CX_DEV int cfe_terms(const Shape& A, const Shape& B) {
 template <class VF>
 CX_DEV v2 cvx_vert_d(const Shape& s, int k, VF vf) {
   if (s.kind == KIND_AABB) {
-    const float x = (k == 0 || k == 1) ? s.w[2] : s.w[0];
-    const float y = (k == 0 || k == 3) ? s.w[3] : s.w[1];
+    const float x = bsel(k == 0 || k == 1, s.w[2], s.w[0]);
+    const float y = bsel(k == 0 || k == 3, s.w[3], s.w[1]);
     return v2{x, y};
   }
   return vf(k);
@@ -947,7 +954,7 @@ CX_DEV v2 cfe_term(const Shape& A, const Shape& B, int s, VFA va, VFB vb) {
     S.kind = fa ? B.kind : A.kind;
     S.n = fa ? B.n : A.n;
 #pragma unroll
-    for (int q = 0; q < 2 * MAXV; ++q) S.w[q] = fa ? B.w[q] : A.w[q];
+    for (int q = 0; q < 2 * MAXV; ++q) S.w[q] = bsel(fa, B.w[q], A.w[q]);
     return shape_contains(S, v) ? v : nanv;
   }
   const int q = s - na - nb, jb = q / na, ia = q - jb * na;

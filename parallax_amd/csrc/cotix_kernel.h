@@ -40,6 +40,7 @@ constexpr int WAVE = 64;
 #ifdef COTIX_STATS
 struct Stats {
   unsigned long long wave_steps, active_items, rounds, resolutions, f_items, b_items, draws, valid_draws, r1_left, lvl_env, lvl_wave, e1_slots;
+  unsigned long long valid_cands, fit64;  // valid candidates of the active items; wave-steps where they fit 64 lanes
 };
 inline Stats g_stats{};
 #define CXK_STAT(f, v) (cxk::g_stats.f += (unsigned long long)(v))
@@ -150,7 +151,7 @@ constexpr int CFB = 8;                           // items per batch
 constexpr int CFS = 2 * cx::MAXV + cx::MAXV * cx::MAXV;  // max terms per item
 constexpr int EPA_NE = 20;                        // EPA edge column length (epa<20> bound)
 struct WsLay {
-  int cf_flag, cf_list, cf_n, cf_s, cf_res, epa, words;
+  int cf_flag, cf_list, cf_n, cf_s, cf_res, epa, bl_flag, bl_list, bl_n, bl_pad, words;
 };
 CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly) {
   WsLay w;
@@ -161,7 +162,12 @@ CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly) {
   w.cf_s = w.cf_n + 1;
   w.cf_res = w.cf_s + CFB;
   w.epa = w.cf_res + CFB * CFS * 2;  // per-lane EPA edge columns, [4*EPA_NE][64]
-  w.words = poly ? w.epa + 4 * EPA_NE * 64 : w.cf_flag;
+  // broadphase (polygon scenes): per-item keep flags (padded to 64) and the B list
+  w.bl_pad = pad;
+  w.bl_flag = w.epa + 4 * EPA_NE * 64;
+  w.bl_list = w.bl_flag + pad;
+  w.bl_n = w.bl_list + pad;
+  w.words = poly ? w.bl_n + 1 : w.cf_flag;
   return w;
 }
 CX_HD int ws_words(const SceneHdr& s, int ew) { return ws_layout(s.nl, s.nc, ew, s.poly).words; }
@@ -522,16 +528,48 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   }
 }
 
-// phase B: distinct contacts (cotix/_colliders.py:149-173)
+// phase B: distinct contacts (cotix/_colliders.py:149-173); item w =
+// (contact, env), env fastest
+// _contact_from_edges(P, P) (cotix/_contacts.py:205-267) of a polygon with
+// itself has a finite contact point when every coordinate is finite with
+// |x| < 2^60 and some pair of adjacent edges is not parallel: for edge a =
+// edge k = (v_k, v_{k-1}) and edge b = edge k-1 = (v_{k-1}, v_{k-2}) the
+// reference computes q - p = v_{k-1} - v_k = r with the same rounding, so t =
+// cross(r, s) / cross(r, s) = 1 and u = cross(r, r) / c = +-0: the
+// intersection v_k + r is a term; every term is bounded by the coordinates,
+// so their sum cannot overflow.  Returns false when it cannot decide (the
+// caller then runs phase F on the item).
+CX_DEV bool self_cp_finite(const cx::Shape& P) {
+  using namespace cx;
+  bool ok = true, any = false;
+  const float lim = 1.152921504606846976e18f;  // 2^60
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (k < P.n) ok = ok && __builtin_fabsf(P.w[2 * k]) < lim && __builtin_fabsf(P.w[2 * k + 1]) < lim;
+  // vertex k - 1 and k - 2 (cyclic): v_{k-1} is the previous slot, or the
+  // last vertex for k = 0; v_{k-2} the one before that
+  v2 prev2 = vert(P, P.n - 2), prev = vert(P, P.n - 1);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (k < P.n) {
+      const v2 vk = v2{P.w[2 * k], P.w[2 * k + 1]};
+      const v2 r = sub(prev, vk), sv = sub(prev2, prev);
+      prev2 = prev;
+      prev = vk;
+      const float cr = r.x * sv.y - sv.x * r.y;
+      any = any || cr != 0.0f;
+    }
+  return ok && any;
+}
+
 template <int EW, int FNSET>
-CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int w) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const v2 d0 = v2{sc.d0x, sc.d0y};
-  for (int w = lane; w < c.nc * EW; w += WAVE) {
+  {
     int e = w % EW, ci = w / EW, g = env0 + e;
-    if ((FNSET & FNS_CONVEX) != 0 && sc.poly) t.ws[c.W.cf_flag + w] = 0u;
-    if (g >= a.B) continue;
+    if (g >= a.B) return;
     const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
     CXK_STAT(b_items, 1);
     const int fn = (int)((d0w >> 20) & 7u);
@@ -553,10 +591,16 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     Contact ct;
     if ((FNSET & FNS_CONVEX) != 0 && (fn == FN_POLY_POLY || fn == FN_AABB_POLY)) {
       // GJK (+EPA); the contact point is deferred to phase F (wave-cooperative)
-      const bool hit = convex_vs_polygon_pen_col(A, Bs, d0, ((d0w >> 27) & 1u) == 0u, &ct.pen,
+      const bool self = ((d0w >> 27) & 1u) != 0u;
+      const bool hit = convex_vs_polygon_pen_col(A, Bs, d0, !self, &ct.pen,
                                                  reinterpret_cast<float*>(t.ws + c.W.epa + lane), WAVE);
       ct.cp = v2{qnan(), qnan()};
-      if (hit) t.ws[c.W.cf_flag + w] = 1u;
+      // a part paired with itself: only the NaN-ness of its contact point is
+      // observable (such a cell is only ever chosen as j == i, which
+      // resolution skips), and it is decided here exactly (self_cp_finite)
+      // instead of by phase F
+      if (hit && self && self_cp_finite(A)) ct.cp = v2{0.0f, 0.0f};
+      else if (hit) t.ws[c.W.cf_flag + w] = 1u;
     } else {
       ct = run_contact_set<FNSET>(fn, A, Bs, d0, &er, ((d0w >> 27) & 1u) != 0u);
     }
@@ -580,6 +624,118 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
 #endif
     }
   }
+}
+template <int EW, int FNSET>
+CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  for (int w = lane; w < c.nc * EW; w += WAVE) {
+    if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly) t.ws[c.W.cf_flag + w] = 0u;
+    b_item<EW, FNSET>(a, c, t, env0, lane, w);
+  }
+}
+
+// phase B with the broadphase (COTIX_STAGE_BROADPHASE, polygon scenes; the
+// exactness argument is in DESIGN.md section 3).  BP0: a polygon pair
+// (polygon x polygon, AABB x polygon) whose world AABBs are separated by
+// more than the margin 2^-8 * S + 2^-16 (S = the largest coordinate
+// magnitude of the two shapes) gets the no-contact result without GJK, EPA
+// or contact points -- _contact_from_edges (cotix/_contacts.py:205-267)
+// cannot find a contained vertex or an edge intersection across that gap,
+// so the reference's contact point is NaN and the candidate never writes.
+// Every other item is flagged for the B list (BP1) that BP2 runs at full
+// lane width.
+// world AABB of a shape in the tile: (lo.x, lo.y, up.x, up.y), NaN-propagating
+template <int EW>
+CX_DEV void shape_box(Tile<EW> t, int wo, int e, int kind, int n, float* bx) {
+  using namespace cx;
+  if (kind != KIND_POLY) {
+    const float g0 = t.f(wo, e), g1 = t.f(wo + 1, e), g2 = t.f(wo + 2, e), g3 = t.f(wo + 3, e);
+    // circle (r, cx, cy): center -+ r; AABB (lo, up)
+    const bool circ = kind == KIND_CIRCLE;
+    bx[0] = circ ? g1 - g0 : g0;
+    bx[1] = circ ? g2 - g0 : g1;
+    bx[2] = circ ? g1 + g0 : g2;
+    bx[3] = circ ? g2 + g0 : g3;
+    return;
+  }
+  // all 2*MAXV words loaded unconditionally (the world region has 2*MAXV
+  // words of slack), so the reads issue back to back; vertices k >= n are
+  // masked by selects
+  float xs[MAXV], ys[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    xs[k] = t.f(wo + 2 * k, e);
+    ys[k] = t.f(wo + 2 * k + 1, e);
+  }
+  // hardware min/max (a NaN operand yields the other one): a NaN vertex
+  // contributes only NaN terms to _contact_from_edges, so the box of the
+  // other vertices is the one that matters; an all-NaN shape gives a NaN box
+  // and is never culled
+  float lx = xs[0], ly = ys[0], ux = lx, uy = ly;
+#pragma unroll
+  for (int k = 1; k < MAXV; ++k) {
+    const bool in = k < n;
+    lx = in ? __builtin_fminf(lx, xs[k]) : lx;
+    ly = in ? __builtin_fminf(ly, ys[k]) : ly;
+    ux = in ? __builtin_fmaxf(ux, xs[k]) : ux;
+    uy = in ? __builtin_fmaxf(uy, ys[k]) : uy;
+  }
+  bx[0] = lx;
+  bx[1] = ly;
+  bx[2] = ux;
+  bx[3] = uy;
+}
+template <int EW>
+CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  for (int w = lane; w < c.W.bl_pad; w += WAVE) {
+    uint32_t keep = 0u;
+    if (w < c.nc * EW) {
+      t.ws[c.W.cf_flag + w] = 0u;
+      const int e = w % EW, ci = w / EW;
+      if (env0 + e < a.B) {
+        keep = 1u;
+        const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
+        const int fn = (int)((d0w >> 20) & 7u);
+        if (fn == FN_POLY_POLY || fn == FN_AABB_POLY) {
+          float A[4], B[4];
+          shape_box<EW>(t, c.L.world + (int)(d0w & 1023u), e, (int)((d0w >> 23) & 3u), (int)(d1w & 255u), A);
+          shape_box<EW>(t, c.L.world + (int)((d0w >> 10) & 1023u), e, (int)((d0w >> 25) & 3u),
+                        (int)((d1w >> 8) & 255u), B);
+          // S and the gap with NaN-propagating max: any NaN box word keeps the full path
+          float S = 0.0f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) S = cx::fmax_(S, cx::fmax_(__builtin_fabsf(A[k]), __builtin_fabsf(B[k])));
+          const float margin = S * 0.00390625f + 1.52587890625e-05f;  // 2^-8 S + 2^-16
+          const float gap = cx::fmax_(cx::fmax_(B[0] - A[2], A[0] - B[2]), cx::fmax_(B[1] - A[3], A[1] - B[3]));
+          if (gap > margin) {  // false for NaN
+            keep = 0u;
+            const int co = c.L.con + 4 * ci;
+            t.f(co + 0, e) = 0.0f;
+            t.f(co + 1, e) = 0.0f;
+            t.f(co + 2, e) = qnan();
+            t.f(co + 3, e) = qnan();
+          }
+        }
+      }
+    }
+    t.ws[c.W.bl_flag + w] = keep;
+  }
+}
+// BP1: append chunk `chunk`'s flagged items to the B list
+template <int EW>
+CX_DEV void ph_BP1(const Ctx& c, Tile<EW> t, int lane, int chunk) {
+  const uint64_t mask = wave_ballot(t.ws + c.W.bl_flag + chunk * WAVE, lane);
+  const uint32_t base = chunk == 0 ? 0u : t.ws[c.W.bl_n];
+  if (t.ws[c.W.bl_flag + chunk * WAVE + lane] != 0u)
+    t.ws[c.W.bl_list + base + popc64(mask & lanes_below(lane))] = (uint32_t)(chunk * WAVE + lane);
+  if (lane == WAVE - 1) t.ws[c.W.bl_n] = base + (uint32_t)popc64(mask);
+}
+// BP2: round r of the B list, one item per lane
+template <int EW, int FNSET>
+CX_DEV void ph_BP2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int r) {
+  const int k = r * WAVE + lane;
+  if (k < (int)t.ws[c.W.bl_n]) b_item<EW, FNSET>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k]);
 }
 
 // phase F: deferred polygon contact points (contact_from_edges,
@@ -831,6 +987,24 @@ CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
       }
     }
   }
+#ifdef COTIX_STATS
+  {
+    static unsigned long long wsum = 0;
+    if (lane == 0) wsum = 0;
+    if (flag) {
+      const int e = lane % EW, l = lane / EW;
+      for (int idx = 0; idx < t.ti(sc.o_ccnt + l); ++idx) {
+        const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
+        const int cid = (cd >> 18) & 511u;
+        if (!(cx::isn(t.f(c.L.con + 4 * cid + 2, e)) || cx::isn(t.f(c.L.con + 4 * cid + 3, e)))) ++wsum;
+      }
+    }
+    if (lane == WAVE - 1) {
+      CXK_STAT(valid_cands, wsum);
+      CXK_STAT(fit64, wsum <= 64 ? 1 : 0);
+    }
+  }
+#endif
   t.ws[WS_KEEP + lane] = flag;
 }
 // M1: the pending count (read after the phase: 0 ends the scan), then every
@@ -1446,24 +1620,33 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // emulation of the tests R loops over the 64 lanes.  The phase id is used
 // only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
-             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_TRACE, PH_COUNT };
+             PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_TRACE, PH_BP0, PH_BP1, PH_F0, PH_F1, PH_F2, PH_F3,
+             PH_COUNT };
 // ---------------------------------------------------------------------------
 // kso: tile offset of this step's sk0 (skt follows): the key window slot, or
 // L.sk0 where phase A splits the keys (backward re-play)
 template <int EW, int FNSET, bool PRE, class R>
 CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso) {
   if (!(a.dbg_skip & 1)) run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
-  if (!(a.dbg_skip & 2)) run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
+  if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !(a.dbg_skip & 2)) {
+    run(PH_BP0, [&](int l) { ph_BP0<EW>(a, c, t, env0, l); });
+    for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_BP1, [&](int l) { ph_BP1<EW>(c, t, l, ch); });
+    const int n = (int)t.ws[c.W.bl_n];  // uniform: read after the phase barrier
+    CXK_STAT(b_items, 0);
+    for (int r = 0; r * WAVE < n; ++r) run(PH_B, [&](int l) { ph_BP2<EW, FNSET>(a, c, t, env0, l, r); });
+  } else if (!(a.dbg_skip & 2)) {
+    run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
+  }
   if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && !(a.dbg_skip & 2)) {
-    for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_F, [&](int l) { ph_F0<EW>(c, t, l, ch); });
+    for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_F0, [&](int l) { ph_F0<EW>(c, t, l, ch); });
     const int n = (int)t.ws[c.W.cf_n];
     CXK_STAT(f_items, n);
     for (int b = 0; b < n; b += CFB) {
-      run(PH_F, [&](int l) { ph_F1<EW>(c, t, l, b); });
+      run(PH_F1, [&](int l) { ph_F1<EW>(c, t, l, b); });
       int T = 0;
       for (int i = 0; i < CFB; ++i) T += (int)t.ws[c.W.cf_s + i];
-      for (int r = 0; r * WAVE < T; ++r) run(PH_F, [&](int l) { ph_F2<EW>(c, t, l, b, r); });
-      run(PH_F, [&](int l) { ph_F3<EW>(c, t, l, b); });
+      for (int r = 0; r * WAVE < T; ++r) run(PH_F2, [&](int l) { ph_F2<EW>(c, t, l, b, r); });
+      run(PH_F3, [&](int l) { ph_F3<EW>(c, t, l, b); });
     }
   }
   if (!(a.dbg_skip & 4) && c.nl > 0 && c.nl * EW <= WAVE) {

@@ -89,6 +89,28 @@ class World:
         assert off == self.scene.geom_floats
         return geom
 
+    def polygon_min_angle(self):
+        """Smallest interior angle (degrees) of any polygon part of the uploaded
+        geometry, over every env (180 when the scene has no polygon; NaN
+        geometry gives NaN)."""
+        g = self.geom.detach().to("cpu", torch.float64)
+        amin, off = 180.0, 0
+        for p in self.scene.parts:
+            n = p.geom_floats()
+            if isinstance(p, AbstractPolygon):
+                v = g[..., off:off + n].reshape(*g.shape[:-1], n // 2, 2)
+                a, b = v.roll(1, -2) - v, v.roll(-1, -2) - v
+                cr = (a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]).abs()
+                m = float(torch.rad2deg(torch.atan2(cr, (a * b).sum(-1))).min())
+                amin = m if not (m >= amin) else amin  # NaN sticks
+            off += n
+        return amin
+
+    def broadphase_ok(self):
+        """The condition COTIX_STAGE_BROADPHASE asks its caller to certify:
+        every polygon interior angle >= 0.5 degrees (include/cotix_amd.h)."""
+        return self.polygon_min_angle() >= 0.5
+
     # -- state access -----------------------------------------------------
     def body(self, i):
         return BodyView(self, i)

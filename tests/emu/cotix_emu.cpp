@@ -274,6 +274,8 @@ extern "C" int emu_stats(unsigned long long* out) {
   out[9] = cxk::g_stats.lvl_env;
   out[10] = cxk::g_stats.lvl_wave;
   out[11] = cxk::g_stats.e1_slots;
+  out[12] = cxk::g_stats.valid_cands;
+  out[13] = cxk::g_stats.fit64;
   cxk::g_stats = cxk::Stats{};
   return 12;
 }

@@ -61,8 +61,11 @@ def test_emu_robocup_trace(emu_lib, EW):
     run_trace(emu, lib, P.robocup_bodies(), None, tr, 1 | 4 | 16, EW, False)
 
 
+@pytest.mark.parametrize("bp", [0, 32], ids=["full", "broadphase"])
 @pytest.mark.parametrize("EW", [1, 2, 4])
-def test_emu_lunar_trace(emu_lib, EW):
+def test_emu_lunar_trace(emu_lib, EW, bp):
+    """bp = 32: COTIX_STAGE_BROADPHASE (separated polygon pairs skip GJK/EPA),
+    the same golden trace bit for bit, choices included."""
     emu, lib = emu_lib
     from cotix_oracle import physics as P
     tr = np.load(os.path.join(GOLD, "lunar_trace.npz"))
@@ -70,7 +73,7 @@ def test_emu_lunar_trace(emu_lib, EW):
     for k in tr["terrain_keys"]:
         _, g = emu.oracle_scene(lib, P.lunar_lander_bodies(k))
         rows.append(g)
-    run_trace(emu, lib, P.lunar_lander_bodies(tr["terrain_keys"][0]), rows, tr, 1 | 2 | 4 | 8 | 16, EW, True)
+    run_trace(emu, lib, P.lunar_lander_bodies(tr["terrain_keys"][0]), rows, tr, 1 | 2 | 4 | 8 | 16 | bp, EW, True)
 
 
 def test_emu_box_world_trace(emu_lib):
@@ -123,7 +126,7 @@ def test_emu_fused_equals_single_steps(emu_lib, EW, scenario):
         rows = [emu.oracle_scene(lib, P.lunar_lander_bodies(k))[1] for k in tr["terrain_keys"]]
         h, _ = emu.oracle_scene(lib, P.lunar_lander_bodies(tr["terrain_keys"][0]))
         geom = np.ascontiguousarray(np.stack(rows).astype(np.float32))
-        gstride, stages = geom.shape[1], 1 | 2 | 4 | 8 | 16
+        gstride, stages = geom.shape[1], 1 | 2 | 4 | 8 | 16 | 32
     dyn0 = np.ascontiguousarray(tr["dyn"][0].transpose(1, 2, 0))
     keys0 = np.ascontiguousarray(tr["keys"][0]).astype(np.uint32)
     reset = dyn0.copy() if scenario == "robocup" else None
@@ -198,9 +201,11 @@ def test_emu_trace_actions_autoreset_vs_cport(emu_lib, EW):
         assert np.array_equal(g, w)
 
 
-def test_emu_lunar_trace_vs_cport(emu_lib):
+@pytest.mark.parametrize("bp", [0, 32], ids=["full", "broadphase"])
+def test_emu_lunar_trace_vs_cport(emu_lib, bp):
     """LunarLander (GJK/EPA contacts) collider trace of the kernel logic == the
-    C port: 24 envs with terrain per env, half of them dropped onto the ground."""
+    C port: 24 envs with terrain per env, half of them dropped onto the ground;
+    bp = 32 with the polygon broadphase (the C port has none)."""
     emu, lib = emu_lib
     sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
     from cotix_oracle import cport
@@ -221,7 +226,7 @@ def test_emu_lunar_trace_vs_cport(emu_lib):
     keys = np.ascontiguousarray(prng.split(prng.PRNGKey(1), B)).astype(np.uint32)
     got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
     want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
-    gch, gcl = emu.step_ex(lib, h, *got, rows, rows.shape[1], T, cport.STAGES_LUNAR, 4, E=4)
+    gch, gcl = emu.step_ex(lib, h, *got, rows, rows.shape[1], T, cport.STAGES_LUNAR | bp, 4, E=4)
     wch, wcl = sc.step_ex(*want, T, cport.STAGES_LUNAR, rows, trace=True)
     assert (wcl >= 0).sum() > B  # contacts were found
     assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)

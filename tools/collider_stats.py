@@ -2,7 +2,7 @@
 phase-C items, candidate-scan rounds, resolutions and phase-F items, from the
 host emulation of the kernel built with -DCOTIX_STATS.
 
-  python tools/collider_stats.py [--scenario robocup|lunar] [--envs 256] [--steps 64] [--ew 4]
+  python tools/collider_stats.py [--scenario robocup|lunar] [--envs 256] [--steps 64] [--ew 4] [--broadphase]
 """
 import argparse
 import ctypes
@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--envs", type=int, default=256)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--ew", type=int, default=4)
+    ap.add_argument("--broadphase", action="store_true", help="COTIX_STAGE_BROADPHASE (polygon scenes)")
     a = ap.parse_args()
     src = os.path.join(ROOT, "tests", "emu", "cotix_emu.cpp")
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
@@ -55,7 +56,7 @@ def main():
         geom = np.ascontiguousarray(np.stack(rows).astype(np.float32))
         gstride = geom.shape[1]
         dyn = np.ascontiguousarray(np.array(dyns, np.float32).transpose(1, 2, 0))
-        stages = 1 | 2 | 4 | 8 | 16
+        stages = 1 | 2 | 4 | 8 | 16 | (32 if a.broadphase else 0)
     keys = np.ascontiguousarray(np.array(prng.split(prng.PRNGKey(3), B), np.uint32))
     dyn_reset = dyn.copy()
     err = np.zeros(B, np.uint32)
@@ -70,7 +71,8 @@ def main():
            "b_items_per_wave_step": out[5] / ws, "valid_draw_frac": out[7] / max(out[6], 1),
            "items_left_after_round1_per_wave_step": out[8] / ws,
            "resolution_levels_per_env_step": out[9] / (B * a.steps), "resolution_levels_per_wave_step": out[10] / ws,
-           "sequential_slots_per_wave_step": out[11] / ws})
+           "sequential_slots_per_wave_step": out[11] / ws,
+           "valid_candidates_of_active_items_per_wave_step": out[12] / ws, "fit64_frac": out[13] / ws})
 
 
 if __name__ == "__main__":

@@ -541,6 +541,32 @@ def test_rollout_grad_robocup_vs_oracle(torch_cuda):
         assert ok, "env %d %s" % (e, msg)
 
 
+def test_rollout_config5_full_size_vs_vjp_oracle(torch_cuda):
+    """BASELINE config 5 at full size (4096 envs x 64 steps) checked
+    independently of the kernel's host emulation: 32 envs sampled across the
+    batch (every 128th) against the torch-f32 VJP oracle of the reference
+    step (oracle/cotix_oracle/grad.py, itself checked against finite
+    differences in tests/test_grad_cpu.py): return bit for bit, d(return)/
+    d(action) within 2e-4 (scaled), the same NaN pattern."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    B, T = 4096, 64
+    case = GC.robocup_case(B, T)
+    _, ret, ga, _, _ = _gpu_rollout(torch, case, pa.scenarios.robocup_bodies())
+    envs = list(range(0, B, 128))
+    orc = GC.oracle(case, envs)
+    finite = 0
+    for e in envs:
+        r, oga, _ = orc[e]
+        assert (np.isnan(ret[e]) and np.isnan(r)) or np.float32(ret[e]).view(np.uint32) == np.float32(r).view(
+            np.uint32), (e, ret[e], r)
+        ok, msg = GC.close(ga[:, e], oga)
+        assert ok, "env %d %s" % (e, msg)
+        finite += int(np.isfinite(oga).all())
+    assert finite > 0
+
+
 def test_rollout_config5_full_size_vs_emulation(torch_cuda):
     """BASELINE config 5 at full size (4096 envs x 64 steps): forward state,
     return and every gradient equal the host emulation of the same kernel
@@ -822,3 +848,112 @@ def test_rank_shards_concatenate_to_single_run(torch_cuda):
     assert torch.equal(torch.cat([p[4] for p in parts], 3), ftr["cells"])
     # rank 1..3 shards are not copies of rank 0's (the bug bench.py once had)
     assert not torch.equal(parts[0][0][4], parts[1][0][4])
+
+
+def test_contracts_and_check_state_vs_oracle(torch_cuda):
+    """Row f4 as a parity row: the device state check (cotix_check_state, the
+    invariant "NaN or invalid value encountered", cotix/_design_by_contract.py:
+    80-107) and the contract wrappers applied to device tensors
+    (parallax_amd.contracts: error_if / pre_condition / post_condition /
+    class_invariant, :13-107) against the oracle's scalar restatement
+    (oracle/cotix_oracle/contracts.py), env by env, on a ragged batch with
+    NaN, +-inf, -0, denormal and extreme finite words."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    from parallax_amd import contracts as C
+    from parallax_amd.envs import WorldState
+    from cotix_oracle import contracts as OC
+    rng = np.random.default_rng(5)
+    B = 4099
+    dyn = (rng.normal(size=(5, 6, B)) * 10).astype(np.float32)
+    special = np.array([np.nan, np.inf, -np.inf, -0.0, 1e-45, 3.4e38, -3.4e38, 1.2e-38], np.float32)
+    pos = rng.integers(0, dyn.size, 400)
+    dyn.reshape(-1)[pos] = special[rng.integers(0, special.size, pos.size)]
+    err0 = rng.integers(0, 4, B).astype(np.int32)
+    w = pa.World(pa.scenarios.robocup_bodies(), B, "cuda")
+    w.dyn.copy_(torch.tensor(dyn))
+    w.err.copy_(torch.tensor(err0))
+    w.check_state()
+    want = OC.check_state(dyn, err0)
+    assert 0 < int((want & OC.ERR_STATE_NONFINITE).astype(bool).sum()) < B
+    assert np.array_equal(w.err.cpu().numpy().astype(np.int64), want)
+
+    # error_if on a device WorldState
+    pred = rng.random(B) < 0.3
+    st = C.error_if(WorldState(w.dyn.clone(), w.keys.clone(), torch.tensor(err0, device="cuda")),
+                    torch.tensor(pred, device="cuda"))
+    gd, ge = st.dyn.cpu().numpy(), st.err.cpu().numpy()
+    for e in range(B):
+        wd, we = OC.env_state_error_if(dyn[:, :, e].reshape(-1).tolist(), int(err0[e]), bool(pred[e]))
+        assert same_f32(gd[:, :, e].reshape(-1), np.array(wd, np.float32)) and ge[e] == we, e
+
+    # pre / post conditions on device tensors, per env
+    x = rng.normal(size=B).astype(np.float32)
+    y = rng.normal(size=B).astype(np.float32)
+    xt, yt = torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda")
+    got = C.pre_condition(lambda a, b: a > 0)(lambda a, b: a + b)(xt, yt).cpu().numpy()
+    want = np.array([OC.pre_condition(lambda a, b: a > 0, lambda a, b: a + b, x[e], y[e]) for e in range(B)],
+                    np.float32)
+    assert same_f32(got, want)
+    got = C.post_condition(lambda r, a: r > a, provide_input=True)(lambda a: a * np.float32(1.5) - 1)(xt)
+    want = np.array([OC.post_condition(lambda r, a: r > a, lambda a: a * np.float32(1.5) - np.float32(1), x[e],
+                                       provide_input=True) for e in range(B)], np.float32)
+    assert same_f32(got.cpu().numpy(), want)
+
+    # class_invariant: the guard fires where __invariant__() is true
+    @C.class_invariant
+    class Probe:
+        def __init__(self, v):
+            self.v = v
+
+        def __invariant__(self):
+            return self.v < 0
+
+        def value(self):
+            return self.v * 2
+
+    got = Probe(xt.clone()).value().cpu().numpy()
+    want = np.array([np.float32(np.nan) if OC.class_invariant_fires(x[e] < 0) else x[e] * np.float32(2)
+                     for e in range(B)], np.float32)
+    assert same_f32(got, want)
+
+
+# ---------------------------------------------------------------------------
+# named regressions of the two hipcc 7.2 miscompiles found this far
+# (DESIGN.md section 8); both are also covered indirectly by the fixtures
+# ---------------------------------------------------------------------------
+def test_regression_hipcc_support_p4xp6(torch_cuda):
+    """A guarded, branchy unrolled argmax in the polygon support function was
+    miscompiled at -O2/-O3: 38 of the P4 x P6 fixture pairs lost their
+    contact.  The 400 P4 x P6 pairs of the poly_poly fixture: every contact
+    bit-exact and the count of contacts equal to the oracle's."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    g = np.load(os.path.join(GOLD, "contacts.npz"))
+    a, b = g["poly_poly_a"], g["poly_poly_b"]
+    sel = (a[:, 1] == 4) & (b[:, 1] == 6)
+    assert sel.sum() >= 400
+    info, _ = pa.run_contacts(int(g["poly_poly_fn"]), torch.tensor(a[sel], device="cuda"),
+                              torch.tensor(b[sel], device="cuda"))
+    got = torch.cat([info.penetration_vector, info.contact_point], 1).cpu().numpy()
+    want = g["poly_poly_out"][sel]
+    assert same_f32(got, want), diff_report(got, want)
+    assert (~np.isnan(got[:, 2])).sum() == (~np.isnan(want[:, 2])).sum() > 0
+
+
+@pytest.mark.parametrize("ew", ["1", "2", "4", "8"])
+def test_regression_hipcc_mixed_kind_transform(torch_cuda, cport_lib, monkeypatch, ew):
+    """A divergent circle / AABB tail of the part transform (phase T) faulted
+    (aperture violation: the circle lanes used an address only the AABB lanes
+    had defined).  RoboCup's parts mix a circle with AABBs; every envs-per-
+    wave tiling puts different kind mixes in one wave.  64 perturbed envs, 6
+    fused steps with restarts, against the C port."""
+    torch = torch_cuda
+    monkeypatch.setenv("COTIX_ENVS_PER_WAVE", ew)
+    import parallax_amd as pa
+    cport, lib = cport_lib
+    env = pa.BatchedEnv(pa.RoboCupEnv(batch=64, device="cuda", perturb=True), autoreset=True)
+    env.reset()
+    dyn = np.ascontiguousarray(env.world.dyn.cpu().numpy())
+    keys = np.ascontiguousarray(env.world.keys.cpu().numpy().view(np.uint32))
+    _robocup_vs_cport(torch, pa, cport, lib, env, dyn, keys, 1, 6)

@@ -73,6 +73,51 @@ struct SceneDev : SceneHdr {
   uint32_t hot[MAXHOT];
 };
 
+// Scene specializations of the step kernel.  The phases are generic over the
+// scene (body / part / contact / cell counts in the header); for the two
+// reference scenes the launcher picks an instantiation whose header copy has
+// these dimensions as compile-time constants, so every per-item loop has a
+// known trip count (no exec-mask loop control, no index division) and the
+// tile layout folds to constants.  The values are the scene compiler's output
+// for cotix/_robocup.py and cotix/_lunar_lander.py; spec_of() admits a scene
+// only when all of them match.
+struct SceneDims {
+  int nb, np, nc, nl, nt, G, W, nmw, poly, rcp_all, rcp_mask;
+};
+enum : int { SPEC_GENERIC = 0, SPEC_ROBOCUP = 1, SPEC_LUNAR = 2 };
+constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+                                    {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31},
+                                    {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14}};
+CX_HD inline bool dims_match(const SceneHdr& h, const SceneDims& d) {
+  return h.nb == d.nb && h.np == d.np && h.nc == d.nc && h.nl == d.nl && h.nt == d.nt && h.G == d.G && h.W == d.W &&
+         h.nmw == d.nmw && h.poly == d.poly && h.rcp_all == d.rcp_all && (int)h.rcp_mask == d.rcp_mask;
+}
+CX_HD inline int spec_of(const SceneHdr& h) {
+  if (dims_match(h, SPEC_DIMS[SPEC_ROBOCUP])) return SPEC_ROBOCUP;
+  if (dims_match(h, SPEC_DIMS[SPEC_LUNAR])) return SPEC_LUNAR;
+  return SPEC_GENERIC;
+}
+// the header with the specialization's dimensions as constants (SPEC > 0
+// only for a header that spec_of() mapped to SPEC)
+template <int SPEC>
+CX_HD SceneHdr spec_hdr(SceneHdr h) {
+  if constexpr (SPEC != SPEC_GENERIC) {
+    constexpr SceneDims d = SPEC_DIMS[SPEC];
+    h.nb = d.nb;
+    h.np = d.np;
+    h.nc = d.nc;
+    h.nl = d.nl;
+    h.nt = d.nt;
+    h.G = d.G;
+    h.W = d.W;
+    h.nmw = d.nmw;
+    h.poly = d.poly;
+    h.rcp_all = d.rcp_all;
+    h.rcp_mask = d.rcp_mask;
+  }
+  return h;
+}
+
 // kernel arguments (passed by value)
 struct KArgs {
   const SceneDev* sc;

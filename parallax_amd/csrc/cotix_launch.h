@@ -4,7 +4,9 @@
 // (-DCOTIX_EW=1/2/4/8, in parallel) and each object defines launch_step_ewN:
 // the step_kernel<EW, FNSET, MODE> instantiation for the scene's contact
 // function set `fs` and `mode` (0 step, 1 rollout forward, 2 backward re-play)
-// launched on `st` with `lds` bytes of dynamic LDS per workgroup.
+// launched on `st` with `lds` bytes of dynamic LDS per workgroup; `spec`
+// (cxk::spec_of of the header) selects a scene specialization where one is
+// compiled (EW = 4), else the generic kernel runs.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -12,8 +14,8 @@
 
 namespace cxl {
 constexpr int WPB = 4;  // waves per workgroup (one per SIMD of a CU)
-hipError_t launch_step_ew1(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st);
-hipError_t launch_step_ew2(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st);
-hipError_t launch_step_ew4(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st);
-hipError_t launch_step_ew8(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st);
+hipError_t launch_step_ew1(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec);
+hipError_t launch_step_ew2(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec);
+hipError_t launch_step_ew4(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec);
+hipError_t launch_step_ew8(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec);
 }  // namespace cxl

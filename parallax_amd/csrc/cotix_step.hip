@@ -262,14 +262,17 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
   ka.dbg_skip = dbg ? atoi(dbg) : 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int fs = scene->fnset;
+  // scene specialization (compile-time dimensions) unless COTIX_NO_SPEC is set
+  const char* ns = getenv("COTIX_NO_SPEC");
+  const int spec = (ns && atoi(ns)) ? cxk::SPEC_GENERIC : cxk::spec_of(scene->host);
   hipError_t e;
 #ifdef COTIX_EW4_ONLY  // tooling builds (phase profile, ISA markers): the default tiling only
-  e = cxl::launch_step_ew4(ka, fs, mode, lds, st);
+  e = cxl::launch_step_ew4(ka, fs, mode, lds, st, spec);
 #else
-  if (EW == 1) e = cxl::launch_step_ew1(ka, fs, mode, lds, st);
-  else if (EW == 2) e = cxl::launch_step_ew2(ka, fs, mode, lds, st);
-  else if (EW == 8) e = cxl::launch_step_ew8(ka, fs, mode, lds, st);
-  else e = cxl::launch_step_ew4(ka, fs, mode, lds, st);
+  if (EW == 1) e = cxl::launch_step_ew1(ka, fs, mode, lds, st, spec);
+  else if (EW == 2) e = cxl::launch_step_ew2(ka, fs, mode, lds, st, spec);
+  else if (EW == 8) e = cxl::launch_step_ew8(ka, fs, mode, lds, st, spec);
+  else e = cxl::launch_step_ew4(ka, fs, mode, lds, st, spec);
 #endif
   if (e != hipSuccess) return hip_check(e, "step_kernel launch");
   return hip_check(hipGetLastError(), "step_kernel launch");

@@ -54,15 +54,16 @@ struct WaveRun {
   }
 #endif
 };
-// MODE 0: step, 1: rollout forward (saves + return), 2: rollout backward
-template <int EW, int FNSET, int MODE>
+// MODE 0: step, 1: rollout forward (saves + return), 2: rollout backward;
+// SPEC: scene specialization (cxk::SPEC_*, compile-time dimensions)
+template <int EW, int FNSET, int MODE, int SPEC = cxk::SPEC_GENERIC>
 __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   extern __shared__ uint32_t lds[];
   const SceneDev* sc = a.sc;
   const int nhot = a.sh.nhot;
   for (int i = threadIdx.x; i < nhot; i += WPB * 64) lds[i] = sc->hot[i];
   __syncthreads();
-  const cxk::Ctx c = cxk::make_ctx<EW>(a.sh);
+  const cxk::Ctx c = cxk::make_ctx<EW>(cxk::spec_hdr<SPEC>(a.sh));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int env0 = (blockIdx.x * WPB + wave) * EW;
   if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
@@ -89,10 +90,29 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
 
 #define CXL_NAME2(n) launch_step_ew##n
 #define CXL_NAME(n) CXL_NAME2(n)
-hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st) {
+hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec) {
   constexpr int EW = COTIX_EW;
   const dim3 grid((ka.B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);
 #define COTIX_LAUNCH(FS, BW) hipLaunchKernelGGL((step_kernel<EW, FS, BW>), grid, block, lds, st, ka)
+#define COTIX_LAUNCH_SPEC(FS, BW, SP) hipLaunchKernelGGL((step_kernel<EW, FS, BW, SP>), grid, block, lds, st, ka)
+#if COTIX_EW == 4  // the default tiling carries the two reference-scene specializations
+  if (spec == cxk::SPEC_ROBOCUP && (fs & ~FNS_ANALYTIC) == 0) {
+    if (mode == 2)
+      COTIX_LAUNCH_SPEC(FNS_ANALYTIC, 2, cxk::SPEC_ROBOCUP);
+    else if (mode == 1)
+      COTIX_LAUNCH_SPEC(FNS_ANALYTIC, 1, cxk::SPEC_ROBOCUP);
+    else
+      COTIX_LAUNCH_SPEC(FNS_ANALYTIC, 0, cxk::SPEC_ROBOCUP);
+    return hipGetLastError();
+  }
+  if (spec == cxk::SPEC_LUNAR && mode == 0 && (fs & FNS_CIRCLE_POLY) == 0) {
+    COTIX_LAUNCH_SPEC(FNS_ANALYTIC | FNS_CONVEX, 0, cxk::SPEC_LUNAR);
+    return hipGetLastError();
+  }
+#else
+  (void)spec;
+#endif
+#undef COTIX_LAUNCH_SPEC
   if (mode == 2) {
     COTIX_LAUNCH(FNS_ANALYTIC, 2);  // the host admits analytic scenes only
   } else if (mode == 1) {

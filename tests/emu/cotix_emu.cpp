@@ -315,3 +315,11 @@ extern "C" int emu_check_state(const float* dyn, int nb, int B, uint32_t* err) {
   for (int g = 0; g < B; ++g) err[g] |= cxk::state_check_env(dyn, nb, B, g);
   return 0;
 }
+
+// scene header fields the step kernel specializes on (cxk::SceneDims)
+extern "C" int emu_scene_dims(void* scene, int* out) {
+  const cxk::SceneHdr& h = static_cast<EmuScene*>(scene)->s;
+  const int v[] = {h.nb, h.np, h.nc, h.nl, h.nt, h.G, h.W, h.nmw, h.poly, h.rcp_all, (int)h.rcp_mask, h.fnset};
+  for (int k = 0; k < 12; ++k) out[k] = v[k];
+  return 12;
+}

@@ -957,3 +957,32 @@ def test_regression_hipcc_mixed_kind_transform(torch_cuda, cport_lib, monkeypatc
     dyn = np.ascontiguousarray(env.world.dyn.cpu().numpy())
     keys = np.ascontiguousarray(env.world.keys.cpu().numpy().view(np.uint32))
     _robocup_vs_cport(torch, pa, cport, lib, env, dyn, keys, 1, 6)
+
+
+@pytest.mark.parametrize("scene", ["robocup", "lunar"])
+def test_specialized_kernel_equals_generic(torch_cuda, monkeypatch, scene):
+    """The scene-specialized instantiations (compile-time dimensions of the
+    two reference scenes, cxk::SPEC_*) and the generic kernel (COTIX_NO_SPEC=1)
+    give bit-identical state, keys, error bits, restarts and collider traces."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import prng
+    outs = []
+    for nospec in ("0", "1"):
+        monkeypatch.setenv("COTIX_NO_SPEC", nospec)
+        if scene == "robocup":
+            env = pa.BatchedEnv(pa.RoboCupEnv(batch=1000, device="cuda", perturb=True), autoreset=True)
+        else:
+            tk = torch.tensor(u32_to_i32(prng.split(prng.PRNGKey(0), 1000)), device="cuda")
+            env = pa.BatchedEnv(pa.LunarLander(key=tk, batch=1000, device="cuda"), autoreset=True)
+            env.scenario.dyn_reset[:3, 1, ::2] -= 6.3  # half of the landers start on the ground
+        env.reset()
+        trc = {}
+        env.step(24, trace=trc)
+        torch.cuda.synchronize()
+        outs.append([env.world.dyn.cpu().numpy(), env.world.keys.cpu().numpy(), env.world.err.cpu().numpy(),
+                     env.resets.cpu().numpy(), trc["chosen"].cpu().numpy(), trc["cells"].cpu().numpy()])
+    assert same_f32(outs[0][0], outs[1][0])
+    for g, w in zip(outs[0][1:], outs[1][1:]):
+        assert np.array_equal(g, w)
+    assert (outs[0][5] >= 0).any()

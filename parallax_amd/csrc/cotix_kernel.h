@@ -88,11 +88,11 @@ enum : int { SPEC_GENERIC = 0, SPEC_ROBOCUP = 1, SPEC_LUNAR = 2 };
 constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
                                     {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31},
                                     {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14}};
-CX_HD inline bool dims_match(const SceneHdr& h, const SceneDims& d) {
+CX_HD bool dims_match(const SceneHdr& h, const SceneDims& d) {
   return h.nb == d.nb && h.np == d.np && h.nc == d.nc && h.nl == d.nl && h.nt == d.nt && h.G == d.G && h.W == d.W &&
          h.nmw == d.nmw && h.poly == d.poly && h.rcp_all == d.rcp_all && (int)h.rcp_mask == d.rcp_mask;
 }
-CX_HD inline int spec_of(const SceneHdr& h) {
+CX_HD int spec_of(const SceneHdr& h) {
   if (dims_match(h, SPEC_DIMS[SPEC_ROBOCUP])) return SPEC_ROBOCUP;
   if (dims_match(h, SPEC_DIMS[SPEC_LUNAR])) return SPEC_LUNAR;
   return SPEC_GENERIC;

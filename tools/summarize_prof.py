@@ -46,7 +46,7 @@ summary = {
     "config": bench["config"],
     "hbm_bytes_per_launch_raw": raw,
     "hbm_bytes_per_launch_corrected": corr,
-    "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+    "alg_bytes_per_launch": bench["roofline"].get("hbm", bench["roofline"]).get("alg_bytes_per_launch"),
     "counters_per_launch": c,
     "valu_active_frac_of_wave_cycles": c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"],
     "wait_frac_of_wave_cycles": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],

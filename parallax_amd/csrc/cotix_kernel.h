@@ -60,13 +60,15 @@ struct SceneHdr {
   float d0x, d0y;                            // GJK start direction (constant)
   uint16_t o_par, o_rcp, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
   uint16_t o_ci, o_cj, o_cbeg, o_ccnt, o_tn1, o_tn2, o_cand;
-  uint16_t o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts
+  uint16_t o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts, part ids
   uint16_t o_cmask;  // per cell nmw words: bitmask of the cell's distinct contacts
   uint16_t nmw;      // contact-mask words = ceil(nc / 32)
   uint16_t poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
   uint16_t rcp_all;  // 1: every mass and inertia has an exact reciprocal (o_rcp): resolutions multiply
   uint16_t fnset;    // FNS_* bits of the contact functions the scene uses (kernel instantiation)
   uint16_t nhot;
+  uint16_t nvt;      // polygon vertices over all parts (phase T's vertex items)
+  uint16_t o_vit;    // per polygon vertex 2 words (cotix_scene.h): part, vertex, count, first item, body | offsets
   uint32_t rcp_mask; // bit b: body b's mass and inertia have exact reciprocals (bodies < 32)
 };
 struct SceneDev : SceneHdr {
@@ -82,15 +84,16 @@ struct SceneDev : SceneHdr {
 // for cotix/_robocup.py and cotix/_lunar_lander.py; spec_of() admits a scene
 // only when all of them match.
 struct SceneDims {
-  int nb, np, nc, nl, nt, G, W, nmw, poly, rcp_all, rcp_mask;
+  int nb, np, nc, nl, nt, G, W, nmw, poly, rcp_all, rcp_mask, nvt;
 };
 enum : int { SPEC_GENERIC = 0, SPEC_ROBOCUP = 1, SPEC_LUNAR = 2 };
-constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-                                    {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31},
-                                    {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14}};
+constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+                                    {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31, 0},
+                                    {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14, 42}};
 CX_HD bool dims_match(const SceneHdr& h, const SceneDims& d) {
   return h.nb == d.nb && h.np == d.np && h.nc == d.nc && h.nl == d.nl && h.nt == d.nt && h.G == d.G && h.W == d.W &&
-         h.nmw == d.nmw && h.poly == d.poly && h.rcp_all == d.rcp_all && (int)h.rcp_mask == d.rcp_mask;
+         h.nmw == d.nmw && h.poly == d.poly && h.rcp_all == d.rcp_all && (int)h.rcp_mask == d.rcp_mask &&
+         h.nvt == d.nvt;
 }
 CX_HD int spec_of(const SceneHdr& h) {
   if (dims_match(h, SPEC_DIMS[SPEC_ROBOCUP])) return SPEC_ROBOCUP;
@@ -114,6 +117,7 @@ CX_HD SceneHdr spec_hdr(SceneHdr h) {
     h.poly = d.poly;
     h.rcp_all = d.rcp_all;
     h.rcp_mask = d.rcp_mask;
+    h.nvt = d.nvt;
   }
   return h;
 }
@@ -150,7 +154,7 @@ struct KArgs {
 
 // per-wave tile layout (words, each x EW envs)
 struct Lay {
-  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, geo, rp, kw, kww, rflag, S;
+  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, geo, rp, kw, kww, rflag, pose, pcv, pbox, S;
 };
 // key window: the per-step keys of KWIN consecutive steps, precomputed
 // together (phase K) -- the collider keys depend on the key chain only, never
@@ -161,7 +165,7 @@ constexpr int REC_W = 7;  // per resolution: applied flag, v/w of body i, v/w of
 enum : int { RP_J, RP_NX, RP_NY, RP_R1X, RP_R1Y, RP_R2X, RP_R2Y, RP_PX, RP_PY, RP_DEN, RP_PT, RP_NE, RP_MU, RP_MJ, RP_IJ,
              RP_QMJ, RP_QIJ, RP_W };
 constexpr uint32_t RP_NONE = 0xFFFFFFFFu;
-CX_HD Lay layout(int nb, int W, int nc, int nt, int G) {
+CX_HD Lay layout(int nb, int np, int W, int nc, int nt, int G) {
   Lay L;
   L.dyn = 0;
   L.world = L.dyn + nb * 6;
@@ -183,10 +187,13 @@ CX_HD Lay layout(int nb, int W, int nc, int nt, int G) {
   L.kww = 2 + 2 * nt + nb;          // key window slot words
   L.kw = L.rp + nb * RP_W;
   L.rflag = L.kw + KWIN * L.kww;    // this step restarts the env (autoreset)
-  L.S = L.rflag + 1;
+  L.pose = L.rflag + 1;             // per body: the pose (px, py, angle bits) its world parts were built from
+  L.pcv = L.pose + 3 * nb;          // bit b: body b's pose entry is valid (cleared at every launch start)
+  L.pbox = L.pcv + 1;               // per part: world AABB (lo.x, lo.y, up.x, up.y), polygon scenes (broadphase)
+  L.S = L.pbox + 4 * np;
   return L;
 }
-static inline int tile_words(const SceneHdr& s) { return layout(s.nb, s.W, s.nc, s.nt, s.G).S; }
+static inline int tile_words(const SceneHdr& s) { return layout(s.nb, s.np, s.W, s.nc, s.nt, s.G).S; }
 // per-wave scratch of phase C (words, not per env): pass flags, keep flags,
 // active count, two item lists (double buffer), per-item scan positions
 enum : int { WS_FLAG = 0, WS_KEEP = 64, WS_KEEP2 = 128, WS_N = 192, WS_LIST = 193 };
@@ -196,9 +203,9 @@ constexpr int CFB = 8;                           // items per batch
 constexpr int CFS = 2 * cx::MAXV + cx::MAXV * cx::MAXV;  // max terms per item
 constexpr int EPA_NE = 20;                        // EPA edge column length (epa<20> bound)
 struct WsLay {
-  int cf_flag, cf_list, cf_n, cf_s, cf_res, epa, bl_flag, bl_list, bl_n, bl_pad, words;
+  int cf_flag, cf_list, cf_n, cf_s, cf_res, epa, bl_flag, bl_list, bl_n, bl_pad, vt, words;
 };
-CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly) {
+CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly, int nvt) {
   WsLay w;
   const int pad = ((nc * ew + 63) / 64) * 64;
   w.cf_flag = WS_LIST + 3 * nl * ew;
@@ -213,9 +220,15 @@ CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly) {
   w.bl_list = w.bl_flag + pad;
   w.bl_n = w.bl_list + pad;
   w.words = poly ? w.bl_n + 1 : w.cf_flag;
+  // phase T's polygon vertex items (x, y, sort key per vertex, [word][env]):
+  // they live only from TV1 to TV3, so they share the EPA columns, which
+  // phase B fills afresh each step; else an area of their own
+  const int nvw = 3 * nvt * ew;
+  w.vt = (poly && nvw <= 4 * EPA_NE * 64) ? w.epa : w.words;
+  if (w.vt == w.words) w.words += nvw;
   return w;
 }
-CX_HD int ws_words(const SceneHdr& s, int ew) { return ws_layout(s.nl, s.nc, ew, s.poly).words; }
+CX_HD int ws_words(const SceneHdr& s, int ew) { return ws_layout(s.nl, s.nc, ew, s.poly, s.nvt).words; }
 // LDS bytes of a workgroup of wpb waves x ew envs
 static inline size_t lds_bytes(const SceneHdr& s, int wpb, int ew) {
   return 4 * ((size_t)s.nhot + ((size_t)tile_words(s) * ew + (size_t)ws_words(s, ew)) * wpb);
@@ -370,7 +383,8 @@ struct Ctx {
 };
 template <int EW>
 CX_HD Ctx make_ctx(const SceneHdr& h) {
-  return Ctx{h.nb, h.np, h.nc, h.nl, h.nt, h, layout(h.nb, h.W, h.nc, h.nt, h.G), ws_layout(h.nl, h.nc, EW, h.poly)};
+  return Ctx{h.nb, h.np, h.nc, h.nl, h.nt, h, layout(h.nb, h.np, h.W, h.nc, h.nt, h.G),
+             ws_layout(h.nl, h.nc, EW, h.poly, h.nvt)};
 }
 
 // local part geometry of the wave's envs: read from HBM once per launch, not
@@ -404,6 +418,7 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
     t.w(c.L.key + 1, e) = (g < a.B) ? a.keys[2 * (size_t)g + 1] : 0u;
     t.w(c.L.err, e) = (g < a.B) ? a.err[g] : 0u;
     t.w(c.L.nres, e) = 0u;
+    t.w(c.L.pcv, e) = 0u;  // no world part built yet in this launch (phase T)
   }
 }
 
@@ -518,7 +533,14 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   }
 }
 
-// phase T: shape.transform(body transformer) (cotix/_colliders.py:92-94)
+// phase T: shape.transform(body transformer) (cotix/_colliders.py:92-94).
+// Circles and AABBs: one (part, env) item per lane.  Polygons
+// (:181-187 forward_vector then the re-sort of Polygon.__init__) are spread
+// over (vertex, env) items in three sub-phases TV1-TV3 (ph_TV*), and a body
+// whose pose (position and angle bits) equals the pose its world parts were
+// last built from in this launch keeps them: the transform is a function of
+// the pose and the launch-constant local geometry only, so the kept parts are
+// the bits a recomputation would give (LunarLander: the static terrain).
 template <int EW, int FNSET>
 CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
@@ -527,49 +549,208 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     int e = w % EW, p = w / EW, g = env0 + e;
     if (g >= a.B) continue;
     const int b = t.ti(sc.o_pbody + p), kind = t.ti(sc.o_pkind + p);
+    if (FNSET != FNS_ANALYTIC && kind == KIND_POLY) continue;  // ph_TV*
     const int lgo = c.L.geo + t.ti(sc.o_pgoff + p);  // this part's local geometry in the tile
     const int o = c.L.dyn + b * 6, wo = c.L.world + t.ti(sc.o_pwoff + p);
     const float px = t.f(o + 0, e), py = t.f(o + 1, e);
-    if (FNSET == FNS_ANALYTIC || kind != KIND_POLY) {
-      // Circle (r, cx, cy, pad): translate only, cotix/_convex_shapes.py:37-41
-      // AABB (lo.x, lo.y, up.x, up.y): translate only, :113-117
-      // Branch-free on purpose: all four floats are loaded unconditionally
-      // (a divergent circle/AABB tail was miscompiled by hipcc 7.2: the
-      // circle lanes read an address register only the AABB lanes defined).
-      const bool circ = kind == KIND_CIRCLE;
-      const float g0 = t.f(lgo, e), g1 = t.f(lgo + 1, e), g2 = t.f(lgo + 2, e), g3 = t.f(lgo + 3, e);
-      t.f(wo + 0, e) = circ ? g0 : g0 + px;
-      t.f(wo + 1, e) = circ ? g1 + px : g1 + py;
-      t.f(wo + 2, e) = circ ? g2 + py : g2 + px;
-      t.f(wo + 3, e) = circ ? g3 : g3 + py;
-    } else {  // :181-187 forward_vector then re-sort (Polygon.__init__)
-      const int n = t.ti(sc.o_pn + p);
-      float s, cs;
-      sincos32(t.f(o + 4, e), &s, &cs);
-      Poly q;
-#pragma unroll
-      for (int k = 0; k < MAXV; ++k) {
-        q.x[k] = 0.0f;
-        q.y[k] = 0.0f;
-        if (k < n) {
-          float x = t.f(lgo + 2 * k, e), y = t.f(lgo + 2 * k + 1, e);
-          float t0 = (cs * x + (-s) * y) + px * 1.0f;
-          float t1 = (s * x + cs * y) + py * 1.0f;
-          // w = (0*x + 0*y) + 1*1 is exactly 1 (or NaN when x or y is
-          // infinite), so t/w == (w == 1 ? t : NaN) bit for bit
-          float t2 = (0.0f * x + 0.0f * y) + 1.0f * 1.0f;
-          q.x[k] = t2 == 1.0f ? t0 : cx::qnan();
-          q.y[k] = t2 == 1.0f ? t1 : cx::qnan();
-        }
-      }
-      const Poly o = order_clockwise(q, n);
-#pragma unroll
-      for (int k = 0; k < MAXV; ++k)
-        if (k < n) {
-          t.f(wo + 2 * k, e) = o.x[k];
-          t.f(wo + 2 * k + 1, e) = o.y[k];
-        }
+    // Circle (r, cx, cy, pad): translate only, cotix/_convex_shapes.py:37-41
+    // AABB (lo.x, lo.y, up.x, up.y): translate only, :113-117
+    // Branch-free on purpose: all four floats are loaded unconditionally
+    // (a divergent circle/AABB tail was miscompiled by hipcc 7.2: the
+    // circle lanes read an address register only the AABB lanes defined).
+    const bool circ = kind == KIND_CIRCLE;
+    const float g0 = t.f(lgo, e), g1 = t.f(lgo + 1, e), g2 = t.f(lgo + 2, e), g3 = t.f(lgo + 3, e);
+    t.f(wo + 0, e) = circ ? g0 : g0 + px;
+    t.f(wo + 1, e) = circ ? g1 + px : g1 + py;
+    t.f(wo + 2, e) = circ ? g2 + py : g2 + px;
+    t.f(wo + 3, e) = circ ? g3 : g3 + py;
+    if (FNSET != FNS_ANALYTIC) {  // the part's world AABB (broadphase, ph_BP0)
+      const int bo = c.L.pbox + 4 * p;
+      const float w0 = t.f(wo, e), w1 = t.f(wo + 1, e), w2 = t.f(wo + 2, e), w3 = t.f(wo + 3, e);
+      // circle (r, cx, cy): center -+ r; AABB (lo, up)
+      t.f(bo, e) = circ ? w1 - w0 : w0;
+      t.f(bo + 1, e) = circ ? w2 - w0 : w1;
+      t.f(bo + 2, e) = circ ? w1 + w0 : w2;
+      t.f(bo + 3, e) = circ ? w2 + w0 : w3;
     }
+  }
+}
+// body b of env e still has the pose its world parts were built from
+template <int EW>
+CX_DEV bool pose_kept(const Ctx& c, Tile<EW> t, int b, int e) {
+  const Lay& L = c.L;
+  const int o = L.dyn + 6 * b, q = L.pose + 3 * b;
+  return ((t.w(L.pcv, e) >> b) & 1u) != 0u && t.w(o, e) == t.w(q, e) && t.w(o + 1, e) == t.w(q + 1, e) &&
+         t.w(o + 4, e) == t.w(q + 2, e);
+}
+// TV0 (item = (body, env)): flag the bodies whose world parts must be rebuilt
+// this step, then record the poses they will be built from
+template <int EW>
+CX_DEV void ph_TV0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  const Lay& L = c.L;
+  for (int w = lane; w < c.nb * EW; w += WAVE) {
+    const int e = w % EW, b = w / EW;
+    const bool redo = env0 + e < a.B && !pose_kept<EW>(c, t, b, e);
+    if (w < WAVE) t.ws[WS_FLAG + w] = redo ? 1u : 0u;
+    t.w(L.pose + 3 * b, e) = t.w(L.dyn + 6 * b, e);
+    t.w(L.pose + 3 * b + 1, e) = t.w(L.dyn + 6 * b + 1, e);
+    t.w(L.pose + 3 * b + 2, e) = t.w(L.dyn + 6 * b + 4, e);
+  }
+  if (lane >= c.nb * EW) t.ws[WS_FLAG + lane] = 0u;
+}
+// word q (x, y, key) of polygon vertex item v of env e (wave scratch)
+template <int EW>
+CX_DEV float& vtf(const Ctx& c, Tile<EW> t, int v, int q, int e) {
+  return reinterpret_cast<float*>(t.ws)[c.W.vt + (3 * v + q) * EW + e];
+}
+// TV1-TV3 run over the vertex items in chunks of 64 (item w = (vertex, env),
+// env fastest) and rebuild the items of the flagged (body, env) pairs only (a
+// part's vertices may straddle chunks: all of them are rebuilt or none); a
+// chunk with no flagged item is skipped (wave-uniform).
+template <int EW>
+CX_DEV uint64_t tv_redo_mask(const Ctx& c, Tile<EW> t, int lane) {
+  return c.nb * EW <= WAVE ? wave_ballot(t.ws + WS_FLAG, lane) : ~0ull;
+}
+template <int EW>
+CX_DEV bool tv_item_redo(const Ctx& c, uint64_t redo, int b, int e) {
+  return c.nb * EW > WAVE || ((redo >> (b * EW + e)) & 1ull) != 0ull;
+}
+template <int EW>
+CX_DEV bool tv_chunk_runs(const Ctx& c, Tile<EW> t, uint64_t redo, int k) {
+  if (c.nb * EW > WAVE) return true;
+  const int nw = c.sh.nvt * EW, lo = k * WAVE, hi = (lo + WAVE < nw ? lo + WAVE : nw) - 1;
+  const int blo = (int)(t.tb[c.sh.o_vit + 2 * (lo / EW)] >> 21), bhi = (int)(t.tb[c.sh.o_vit + 2 * (hi / EW)] >> 21);
+  const int n = (bhi + 1 - blo) * EW;  // item bits of bodies blo..bhi
+  const uint64_t m = (n >= 64 ? ~0ull : ((1ull << n) - 1ull)) << (blo * EW);
+  return (redo & m) != 0ull;
+}
+// bit k: chunk k runs (all chunks' table reads issued together)
+template <int EW>
+CX_DEV uint32_t tv_chunks(const Ctx& c, Tile<EW> t, uint64_t redo) {
+  uint32_t runs = 0u;
+  for (int k = 0; k * WAVE < c.sh.nvt * EW; ++k) runs |= tv_chunk_runs<EW>(c, t, redo, k) ? 1u << k : 0u;
+  return runs;
+}
+// TV1 (item = (polygon vertex v, env)): the affine map of vertex k of part p
+// (HomogenuousTransformer.forward_vector, cotix/_geometry_utils.py:105-112)
+// into the vertex item's x, y
+template <int EW>
+CX_DEV void ph_TV1(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const Lay& L = c.L;
+  const uint64_t redo = tv_redo_mask<EW>(c, t, lane);
+  const uint32_t runs = tv_chunks<EW>(c, t, redo);
+  for (int e = lane; e < EW; e += WAVE) t.w(L.pcv, e) = c.nb >= 32 ? ~0u : ((1u << c.nb) - 1u);
+  for (int k0 = 0; k0 * WAVE < sc.nvt * EW; ++k0) {
+    if (!((runs >> k0) & 1u)) continue;
+    const int w = k0 * WAVE + lane, e = w % EW, v = w / EW;
+    if (w >= sc.nvt * EW || env0 + e >= a.B) continue;
+    const uint32_t d = t.tb[sc.o_vit + 2 * v], d1 = t.tb[sc.o_vit + 2 * v + 1];
+    const int b = (int)(d >> 21), lg = L.geo + (int)(d1 & 0xFFFFu);
+    if (!tv_item_redo<EW>(c, redo, b, e)) continue;
+    const int o = L.dyn + b * 6;
+    const float px = t.f(o + 0, e), py = t.f(o + 1, e);
+    float s, cs;
+    sincos32(t.f(o + 4, e), &s, &cs);
+    const float x = t.f(lg, e), y = t.f(lg + 1, e);
+    const float t0 = (cs * x + (-s) * y) + px * 1.0f;
+    const float t1 = (s * x + cs * y) + py * 1.0f;
+    // w = (0*x + 0*y) + 1*1 is exactly 1 (or NaN when x or y is infinite), so
+    // t/w == (w == 1 ? t : NaN) bit for bit
+    const float t2 = (0.0f * x + 0.0f * y) + 1.0f * 1.0f;
+    vtf<EW>(c, t, v, 0, e) = t2 == 1.0f ? t0 : qnan();
+    vtf<EW>(c, t, v, 1, e) = t2 == 1.0f ? t1 : qnan();
+  }
+}
+// TV2: order_clockwise's sort key of the vertex (cotix/_geometry_utils.py:
+// 60-67): the sequential mean of the part's vertices, then atan2 about it;
+// NaN -> 4 (after every angle, all NaN equal: sort_lt is key order)
+template <int EW>
+CX_DEV void ph_TV2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const uint64_t redo = tv_redo_mask<EW>(c, t, lane);
+  const uint32_t runs = tv_chunks<EW>(c, t, redo);
+  for (int k0 = 0; k0 * WAVE < sc.nvt * EW; ++k0) {
+    if (!((runs >> k0) & 1u)) continue;
+    const int w = k0 * WAVE + lane, e = w % EW, v = w / EW;
+    if (w >= sc.nvt * EW || env0 + e >= a.B) continue;
+    const uint32_t d = t.tb[sc.o_vit + 2 * v];
+    const int n = (int)((d >> 8) & 15u), v0 = (int)((d >> 12) & 511u);
+    if (!tv_item_redo<EW>(c, redo, (int)(d >> 21), e)) continue;
+    // every read unconditional (clamped index, the sum selects): guarded
+    // reads compile to one LDS round trip per vertex
+    float xs[MAXV], ys[MAXV];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vk = v0 + (k < n ? k : 0);
+      xs[k] = vtf<EW>(c, t, vk, 0, e);
+      ys[k] = vtf<EW>(c, t, vk, 1, e);
+    }
+    float sx = 0.0f, sy = 0.0f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      sx = k < n ? sx + xs[k] : sx;
+      sy = k < n ? sy + ys[k] : sy;
+    }
+    const float fn = (float)n;
+    const float mx = sx / fn, my = sy / fn;
+    const float ang = atan2_32(vtf<EW>(c, t, v, 1, e) - my, vtf<EW>(c, t, v, 0, e) - mx);
+    vtf<EW>(c, t, v, 2, e) = isn(ang) ? 4.0f : ang;
+    if (v == v0) {
+      // the part's world AABB (broadphase, ph_BP0): hardware min/max (a NaN
+      // operand yields the other one), so an all-NaN part gives a NaN box
+      // and a NaN vertex is left out -- it contributes only NaN terms to
+      // _contact_from_edges; order-independent, so the unsorted vertices do
+      float lx = xs[0], ly = ys[0], ux = lx, uy = ly;
+#pragma unroll
+      for (int k = 1; k < MAXV; ++k) {
+        const bool in = k < n;
+        lx = in ? __builtin_fminf(lx, xs[k]) : lx;
+        ly = in ? __builtin_fminf(ly, ys[k]) : ly;
+        ux = in ? __builtin_fmaxf(ux, xs[k]) : ux;
+        uy = in ? __builtin_fmaxf(uy, ys[k]) : uy;
+      }
+      const int bo = c.L.pbox + 4 * (int)(d & 31u);
+      t.f(bo, e) = lx;
+      t.f(bo + 1, e) = ly;
+      t.f(bo + 2, e) = ux;
+      t.f(bo + 3, e) = uy;
+    }
+  }
+}
+// TV3: the vertex's stable rank among its part's keys -- #{j < k : !(key_k <
+// key_j)} + #{j > k : key_j < key_k}, the permutation insertion sort produces
+// -- is its slot in the world part
+template <int EW>
+CX_DEV void ph_TV3(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const Lay& L = c.L;
+  const uint64_t redo = tv_redo_mask<EW>(c, t, lane);
+  const uint32_t runs = tv_chunks<EW>(c, t, redo);
+  for (int k0 = 0; k0 * WAVE < sc.nvt * EW; ++k0) {
+    if (!((runs >> k0) & 1u)) continue;
+    const int w = k0 * WAVE + lane, e = w % EW, v = w / EW;
+    if (w >= sc.nvt * EW || env0 + e >= a.B) continue;
+    const uint32_t d = t.tb[sc.o_vit + 2 * v], d1 = t.tb[sc.o_vit + 2 * v + 1];
+    const int k = (int)((d >> 5) & 7u), n = (int)((d >> 8) & 15u), v0 = (int)((d >> 12) & 511u);
+    if (!tv_item_redo<EW>(c, redo, (int)(d >> 21), e)) continue;
+    const float kk = vtf<EW>(c, t, v, 2, e);
+    float ks[MAXV];
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) ks[j] = vtf<EW>(c, t, v0 + (j < n ? j : 0), 2, e);  // unconditional reads
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {  // flat selects (a short-circuit form compiles to branches)
+      const int before = ks[j] < kk ? 1 : 0, not_after = kk < ks[j] ? 0 : 1;
+      const int in = (j < n ? 1 : 0) & (j != k ? 1 : 0);
+      r += in & (j < k ? not_after : before);
+    }
+    const int wo = L.world + (int)(d1 >> 16) + 2 * r;
+    t.f(wo, e) = vtf<EW>(c, t, v, 0, e);
+    t.f(wo + 1, e) = vtf<EW>(c, t, v, 1, e);
   }
 }
 
@@ -688,47 +869,6 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
 // so the reference's contact point is NaN and the candidate never writes.
 // Every other item is flagged for the B list (BP1) that BP2 runs at full
 // lane width.
-// world AABB of a shape in the tile: (lo.x, lo.y, up.x, up.y), NaN-propagating
-template <int EW>
-CX_DEV void shape_box(Tile<EW> t, int wo, int e, int kind, int n, float* bx) {
-  using namespace cx;
-  if (kind != KIND_POLY) {
-    const float g0 = t.f(wo, e), g1 = t.f(wo + 1, e), g2 = t.f(wo + 2, e), g3 = t.f(wo + 3, e);
-    // circle (r, cx, cy): center -+ r; AABB (lo, up)
-    const bool circ = kind == KIND_CIRCLE;
-    bx[0] = circ ? g1 - g0 : g0;
-    bx[1] = circ ? g2 - g0 : g1;
-    bx[2] = circ ? g1 + g0 : g2;
-    bx[3] = circ ? g2 + g0 : g3;
-    return;
-  }
-  // all 2*MAXV words loaded unconditionally (the world region has 2*MAXV
-  // words of slack), so the reads issue back to back; vertices k >= n are
-  // masked by selects
-  float xs[MAXV], ys[MAXV];
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    xs[k] = t.f(wo + 2 * k, e);
-    ys[k] = t.f(wo + 2 * k + 1, e);
-  }
-  // hardware min/max (a NaN operand yields the other one): a NaN vertex
-  // contributes only NaN terms to _contact_from_edges, so the box of the
-  // other vertices is the one that matters; an all-NaN shape gives a NaN box
-  // and is never culled
-  float lx = xs[0], ly = ys[0], ux = lx, uy = ly;
-#pragma unroll
-  for (int k = 1; k < MAXV; ++k) {
-    const bool in = k < n;
-    lx = in ? __builtin_fminf(lx, xs[k]) : lx;
-    ly = in ? __builtin_fminf(ly, ys[k]) : ly;
-    ux = in ? __builtin_fmaxf(ux, xs[k]) : ux;
-    uy = in ? __builtin_fmaxf(uy, ys[k]) : uy;
-  }
-  bx[0] = lx;
-  bx[1] = ly;
-  bx[2] = ux;
-  bx[3] = uy;
-}
 template <int EW>
 CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
@@ -743,10 +883,14 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
         const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
         const int fn = (int)((d0w >> 20) & 7u);
         if (fn == FN_POLY_POLY || fn == FN_AABB_POLY) {
+          // the parts' world AABBs, built with the world parts in phase T
+          const int ba = c.L.pbox + 4 * (int)((d1w >> 16) & 255u), bb = c.L.pbox + 4 * (int)(d1w >> 24);
           float A[4], B[4];
-          shape_box<EW>(t, c.L.world + (int)(d0w & 1023u), e, (int)((d0w >> 23) & 3u), (int)(d1w & 255u), A);
-          shape_box<EW>(t, c.L.world + (int)((d0w >> 10) & 1023u), e, (int)((d0w >> 25) & 3u),
-                        (int)((d1w >> 8) & 255u), B);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            A[k] = t.f(ba + k, e);
+            B[k] = t.f(bb + k, e);
+          }
           // S and the gap with NaN-propagating max: any NaN box word keeps the full path
           float S = 0.0f;
 #pragma unroll
@@ -1666,13 +1810,28 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
              PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_TRACE, PH_BP0, PH_BP1, PH_F0, PH_F1, PH_F2, PH_F3,
-             PH_COUNT };
+             PH_TV0, PH_TV1, PH_TV2, PH_TV3, PH_COUNT };
 // ---------------------------------------------------------------------------
 // kso: tile offset of this step's sk0 (skt follows): the key window slot, or
 // L.sk0 where phase A splits the keys (backward re-play)
 template <int EW, int FNSET, bool PRE, class R>
 CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso) {
-  if (!(a.dbg_skip & 1)) run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
+  if (!(a.dbg_skip & 1)) {
+    run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
+    if (FNSET != FNS_ANALYTIC && c.sh.nvt > 0) {
+      run(PH_TV0, [&](int l) { ph_TV0<EW>(a, c, t, env0, l); });
+      run(PH_TV1, [&](int l) { ph_TV1<EW>(a, c, t, env0, l); });
+      run(PH_TV2, [&](int l) { ph_TV2<EW>(a, c, t, env0, l); });
+      run(PH_TV3, [&](int l) { ph_TV3<EW>(a, c, t, env0, l); });
+#if !defined(__HIP__)
+      // host emulation (tests): the vertex items die with phase T -- poison
+      // them so that a later step reading stale ones cannot pass by luck
+      run(PH_TV3, [&](int l) {
+        for (int q = l; q < 3 * c.sh.nvt * EW; q += WAVE) t.ws[c.W.vt + q] = 0x7FBADBADu;
+      });
+#endif
+    }
+  }
   if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !(a.dbg_skip & 2)) {
     run(PH_BP0, [&](int l) { ph_BP0<EW>(a, c, t, env0, l); });
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_BP1, [&](int l) { ph_BP1<EW>(c, t, l, ch); });
@@ -1763,6 +1922,7 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
   run(PH_ADJ, [&](int l) {
     ph_geo<EW>(a, c, t, env0, l);
     ph_adj_init<EW>(a, c, t, env0, l);
+    for (int e = l; e < EW; e += WAVE) t.w(c.L.pcv, e) = 0u;  // phase T's pose entries
   });
   for (int step = a.n_steps - 1; step >= 0; --step) {
     run(PH_RESTORE, [&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });

@@ -199,6 +199,22 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   put(s.o_pn, part_nv);
   put(s.o_pgoff, part_goffv);
   put(s.o_pwoff, part_woffv);
+  {  // phase T's polygon vertex items, part order (cxk::ph_TV*)
+    // 2 words per vertex (one 8-byte read): part | vertex << 5 | count << 8 |
+    // first item of the part << 12 | body << 21, then the vertex's local
+    // geometry offset | the part's world offset << 16
+    if (hot.size() % 2) hot.push_back(0u);
+    s.o_vit = (uint16_t)hot.size();
+    int nv = 0;
+    for (int p = 0; p < n_parts; ++p) {
+      const int first = nv;
+      for (int k = 0; k < part_nv[p]; ++k, ++nv) {
+        hot.push_back((uint32_t)(p | (k << 5) | (part_nv[p] << 8) | (first << 12) | (part_bodyv[p] << 21)));
+        hot.push_back((uint32_t)(part_goffv[p] + 2 * k) | ((uint32_t)part_woffv[p] << 16));
+      }
+    }
+    s.nvt = nv;
+  }
   std::vector<int> cpa(s.nc), cpb(s.nc), cfn(s.nc);
   for (int c = 0; c < s.nc; ++c) {
     cpa[c] = std::get<0>(clist[c]);
@@ -217,7 +233,7 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
     hot.push_back((uint32_t)part_woffv[pa] | ((uint32_t)part_woffv[pb] << 10) | ((uint32_t)cfn[c] << 20) |
                   ((uint32_t)part_kindv[pa] << 23) | ((uint32_t)part_kindv[pb] << 25) |
                   ((uint32_t)(pa == pb) << 27));  // a part paired with itself: penetration never used
-    hot.push_back((uint32_t)part_nv[pa] | ((uint32_t)part_nv[pb] << 8));
+    hot.push_back((uint32_t)part_nv[pa] | ((uint32_t)part_nv[pb] << 8) | ((uint32_t)pa << 16) | ((uint32_t)pb << 24));
   }
   s.nmw = (s.nc + 31) / 32;
   std::vector<int> ci, cj, cbeg, ccnt;

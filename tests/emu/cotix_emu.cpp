@@ -319,7 +319,13 @@ extern "C" int emu_check_state(const float* dyn, int nb, int B, uint32_t* err) {
 // scene header fields the step kernel specializes on (cxk::SceneDims)
 extern "C" int emu_scene_dims(void* scene, int* out) {
   const cxk::SceneHdr& h = static_cast<EmuScene*>(scene)->s;
-  const int v[] = {h.nb, h.np, h.nc, h.nl, h.nt, h.G, h.W, h.nmw, h.poly, h.rcp_all, (int)h.rcp_mask, h.fnset};
-  for (int k = 0; k < 12; ++k) out[k] = v[k];
-  return 12;
+  const int v[] = {h.nb, h.np, h.nc, h.nl, h.nt, h.G, h.W, h.nmw, h.poly, h.rcp_all, (int)h.rcp_mask, h.nvt, h.fnset};
+  for (int k = 0; k < 13; ++k) out[k] = v[k];
+  return 13;
+}
+// the step-kernel specialization the launcher picks for the scene (cxk::spec_of)
+extern "C" int emu_scene_spec(void* scene) { return cxk::spec_of(static_cast<EmuScene*>(scene)->s); }
+// LDS bytes of the step kernel's workgroup (cxk::lds_bytes, 4 waves) for the scene at `ew` envs per wave
+extern "C" long emu_lds_bytes(void* scene, int ew) {
+  return (long)cxk::lds_bytes(static_cast<EmuScene*>(scene)->s, 4, ew);
 }

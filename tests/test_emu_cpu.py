@@ -4,6 +4,7 @@ emulation harness (tests/emu), must reproduce the golden oracle traces bit
 for bit -- the same bar as the GPU tests -- for every envs-per-wave tiling,
 including the collider's contact choices (j* per body and the winning
 candidate of every all_contacts cell, cotix/_colliders.py:208-295)."""
+import ctypes
 import os
 import subprocess
 import sys
@@ -292,3 +293,134 @@ def test_emu_transcendentals_vs_oracle(emu_lib):
     lib.emu_atan2(yy.ctypes.data_as(emu.P_), xx.ctypes.data_as(emu.P_), yy.size, out.ctypes.data_as(emu.P_))
     want = np.array([G.atan2_32(a, b) for a, b in zip(yy, xx)], np.float32)
     assert same_f32(out, want)
+
+
+@pytest.mark.parametrize("bp", [0, 32], ids=["full", "broadphase"])
+@pytest.mark.parametrize("EW", [1, 4, 8])
+def test_emu_lunar_restarts_move_static_body_vs_cport(emu_lib, EW, bp):
+    """Phase T keeps a body's world parts while its pose bits are unchanged
+    (the static terrain): restarts into a reset state whose terrain body sits
+    elsewhere (and a NaN-posed lander in some envs) must rebuild them.  The
+    kernel logic == the C port over 2 launches of 9 fused steps; envs with an
+    error bit at launch start restart after their first step."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    if not os.path.exists(cport.LIB):
+        pytest.skip("oracle C port not built (make -C oracle)")
+    clib = cport.load()
+    B, T = 20, 9
+    tk = prng.split(prng.PRNGKey(4), B)
+    rows = np.ascontiguousarray(np.stack([emu.oracle_scene(lib, P.lunar_lander_bodies(k))[1] for k in tk]))
+    h, _ = emu.oracle_scene(lib, P.lunar_lander_bodies(tk[0]))
+    sc = cport.Scene(clib, P.lunar_lander_bodies(tk[0]))
+    base = np.array([b.dyn() for b in P.lunar_lander_bodies(tk[0])], np.float32)
+    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
+    dyn[:3, 1, :] -= np.float32(6.3)  # dropped onto the terrain
+    dyn[:3, 3, :] = np.float32(-0.3)
+    reset = dyn.copy()
+    reset[3, 0, 0::2] += np.float32(0.75)  # the terrain body restarts elsewhere
+    reset[3, 4, 1::2] = np.float32(2.0)    # ... or only rotated (vertex order changes)
+    reset[0, 4, 3::5] = np.float32(np.nan)  # a NaN-posed lander
+    keys = np.ascontiguousarray(prng.split(prng.PRNGKey(5), B)).astype(np.uint32)
+    err0 = np.zeros(B, np.uint32)
+    err0[1::3] = 1
+    got = [dyn.copy(), keys.copy(), err0.copy(), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), err0.copy(), np.zeros(B, np.uint32)]
+    for launch in range(2):
+        gch, gcl = emu.step_ex(lib, h, got[0], got[1], got[2], rows, rows.shape[1], T, cport.STAGES_LUNAR | bp, 4,
+                               E=EW, dyn_reset=reset, resets=got[3])
+        wch, wcl = sc.step_ex(want[0], want[1], want[2], T, cport.STAGES_LUNAR, rows, None, 0, reset, want[3],
+                              trace=True)
+        assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+        if launch == 0:
+            got[2][0::4] = 1
+            want[2][0::4] = 1
+    assert want[3].sum() == len(err0[1::3]) + len(err0[0::4])
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)
+
+
+def test_reference_scenes_get_their_specializations(emu_lib):
+    """The two reference scenes compile to the dimensions of their step-kernel
+    specializations (cxk::SPEC_DIMS): a scene-compiler change that moved them
+    would silently fall back to the generic kernel."""
+    emu, lib = emu_lib
+    from cotix_oracle import physics as P
+    lib.emu_scene_spec.argtypes = [ctypes.c_void_p]
+    h, _ = emu.oracle_scene(lib, P.robocup_bodies())
+    assert lib.emu_scene_spec(h) == 1
+    h, _ = emu.oracle_scene(lib, P.lunar_lander_bodies())
+    assert lib.emu_scene_spec(h) == 2
+
+
+def test_reference_scenes_fit_the_lds(emu_lib):
+    """The step kernel's workgroup LDS (hot tables + 4 wave tiles + scratch)
+    stays within the CU's 160 KiB for the tilings the library launches: every
+    envs-per-wave for RoboCup, 1/2/4 for LunarLander (the default is 4)."""
+    emu, lib = emu_lib
+    from cotix_oracle import physics as P
+    lib.emu_lds_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.emu_lds_bytes.restype = ctypes.c_long
+    h, _ = emu.oracle_scene(lib, P.robocup_bodies())
+    assert all(lib.emu_lds_bytes(h, e) <= 160 * 1024 for e in (1, 2, 4, 8))
+    h, _ = emu.oracle_scene(lib, P.lunar_lander_bodies())
+    assert all(lib.emu_lds_bytes(h, e) <= 160 * 1024 for e in (1, 2, 4))
+
+
+def _straddle_scene(theta):
+    """A falling dynamic quad (body 0, vertex items 0..3) over a static,
+    rotated body 1 of 14 far-away quads and a hexagonal floor under the quad
+    (vertex items 60..65): at one env per wave the floor straddles phase T's
+    first two 64-item chunks.  theta rotates body 1: its world
+    vertex order is a re-sort of the local order."""
+    from cotix_oracle import geometry as G
+    from cotix_oracle import physics as P
+    c, s = np.cos(-theta), np.sin(-theta)
+
+    def local(pts):  # world points of body 1 (at the origin) -> its local frame
+        return [(float(np.float32(x * c - y * s)), float(np.float32(x * s + y * c))) for x, y in pts]
+
+    dummies = [G.Polygon(local([(40 + 5 * i, 0), (42 + 5 * i, 0), (42 + 5 * i, 2), (40 + 5 * i, 2)]), kind="Polygon4")
+               for i in range(14)]
+    floor = G.Polygon(local([(-3, -1), (3, -1), (3.2, -0.5), (3, 0), (-3, 0), (-3.2, -0.5)]), kind="Polygon6")
+    box = G.Polygon([(-0.5, 0.0), (0.5, 0.0), (0.5, 0.6), (-0.5, 0.6)], kind="Polygon4")
+    return [P.Body([box], mass=1.0, inertia=1.0, position=(0.1, 0.05), velocity=(0.0, -0.5), angular_velocity=0.3,
+                   elasticity=0.5, friction_coefficient=0.2),
+            P.Body(dummies + [floor], mass=float("inf"), inertia=float("inf"), angle=theta, elasticity=0.5,
+                   friction_coefficient=0.2)]
+
+
+@pytest.mark.parametrize("bp", [0, 32], ids=["full", "broadphase"])
+@pytest.mark.parametrize("EW", [1, 2, 4])
+def test_emu_static_part_straddling_chunks_vs_cport(emu_lib, EW, bp):
+    """Phase T with a kept (static) body whose part straddles two vertex-item
+    chunks, the first of which runs for the moving body: the straddling part
+    must be kept whole (rebuilding half of it would read the other half's dead
+    vertex items).  The kernel logic == the C port over 20 steps, 6 envs."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    if not os.path.exists(cport.LIB):
+        pytest.skip("oracle C port not built (make -C oracle)")
+    clib = cport.load()
+    bodies = _straddle_scene(4.0)
+    h, geom = emu.oracle_scene(lib, bodies)
+    sc = cport.Scene(clib, bodies)
+    B, T = 6, 20
+    base = np.array([b.dyn() for b in bodies], np.float32)
+    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
+    dyn[0, 0, :] += np.linspace(-1, 1, B).astype(np.float32)
+    keys = np.ascontiguousarray(np.stack([np.arange(B), np.arange(B) * 7 + 1], 1).astype(np.uint32))
+    got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    gch, gcl = emu.step_ex(lib, h, *got, geom, 0, T, 1 | 4 | 16 | bp, 2, E=EW)
+    wch, wcl = sc.step_ex(*want, T, 1 | 4 | 16, trace=True)
+    assert (wcl[:, 0, 1] >= 0).sum() + (wcl[:, 1, 0] >= 0).sum() > T  # the triangle sits on the floor
+    assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)

@@ -446,6 +446,56 @@ def test_lunar_4096_all_envs_vs_cport(torch_cuda, cport_lib):
     assert np.array_equal(trc["cells"].cpu().numpy(), wcl)
 
 
+def test_lunar_restarts_move_static_body_vs_cport(torch_cuda, cport_lib):
+    """Phase T keeps a body's world parts while its pose bits are unchanged
+    (LunarLander's static terrain).  4096 envs dropped onto the terrain, 2
+    launches x 9 steps with restarts into a reset state whose terrain body is
+    shifted (even envs) or only rotated (odd envs), and a NaN-posed lander in
+    some: every env, restart count and contact choice vs the C port."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    cport, lib = cport_lib
+    B, T = 4096, 9
+    tkeys = prng.split(prng.PRNGKey(4), B)
+    ll = pa.LunarLander(key=torch.tensor(u32_to_i32(tkeys), device="cuda"), batch=B, device="cuda")
+    w = ll.world
+    for i in range(3):
+        w.dyn[i, 1] -= 6.3
+        w.dyn[i, 3] = -0.3
+    reset = w.dyn.clone()
+    reset[3, 0, 0::2] += 0.75
+    reset[3, 4, 1::2] = 2.0
+    reset[0, 4, 3::5] = float("nan")
+    w.err[1::3] = 1
+    dyn = np.ascontiguousarray(w.dyn.cpu().numpy())
+    keys = np.ascontiguousarray(w.keys.cpu().numpy().view(np.uint32))
+    err = np.ascontiguousarray(w.err.cpu().numpy().view(np.uint32))
+    geom = np.ascontiguousarray(w.geom.cpu().numpy())
+    rst = np.ascontiguousarray(reset.cpu().numpy())
+    resets = torch.zeros(B, dtype=torch.int32, device="cuda")
+    want_resets = np.zeros(B, np.uint32)
+    sc = cport.Scene(lib, P.lunar_lander_bodies(tkeys[0]))
+    for q in range(2):
+        trc = {}
+        w.step(T, 1e-2, ll.stages, dyn_reset=reset, resets=resets, trace=trc)
+        wch, wcl = sc.step_ex(dyn, keys, err, T, cport.STAGES_LUNAR, geom, None, 0, rst, want_resets, trace=True,
+                              nthreads=16)
+        torch.cuda.synchronize()
+        assert np.array_equal(trc["chosen"].cpu().numpy(), wch), "launch %d chosen" % q
+        assert np.array_equal(trc["cells"].cpu().numpy(), wcl), "launch %d cells" % q
+        if q == 0:
+            w.err[0::4] = 1
+            err[0::4] = 1
+    got = w.dyn.cpu().numpy()
+    assert same_f32(got, dyn), diff_report(got, dyn)
+    assert np.array_equal(w.keys.cpu().numpy().view(np.uint32), keys)
+    assert np.array_equal(w.err.cpu().numpy().view(np.uint32), err)
+    assert np.array_equal(resets.cpu().numpy().view(np.uint32), want_resets)
+    assert want_resets.sum() == len(range(1, B, 3)) + len(range(0, B, 4))
+
+
 def test_config1_lunar_single_env_10000_steps_vs_cport(torch_cuda, cport_lib):
     """BASELINE config 1 (examples/test_viz.py:24-48): one LunarLander env,
     terrain PRNGKey(0), collider key chain from PRNGKey(0), dt 1e-2, gravity

@@ -8,7 +8,8 @@ import sys
 from collections import Counter, defaultdict
 
 NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
-         "adj", "F", "K", "E1", "R", "trace", "B0", "B1", "F0", "F1", "F2", "F3"]
+         "adj", "F", "K", "E1", "R", "trace", "B0", "B1", "F0", "F1", "F2", "F3",
+         "TV0", "TV1", "TV2", "TV3"]
 src, pat = sys.argv[1], sys.argv[2]
 lines = open(src).read().split("\n")
 body, cur = [], False

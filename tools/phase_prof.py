@@ -11,7 +11,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "parallax_amd", "_lib", "libcotix_amd_prof.so")
 NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
-         "adj", "F", "K", "E1", "R", "trace", "B0", "B1", "F0", "F1", "F2", "F3"]
+         "adj", "F", "K", "E1", "R", "trace", "B0", "B1", "F0", "F1", "F2", "F3",
+         "TV0", "TV1", "TV2", "TV3"]
 
 
 def build():

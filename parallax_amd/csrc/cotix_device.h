@@ -306,7 +306,8 @@ CX_DEV v2 support(const Shape& s, v2 d) {
   auto step = [&](int k) {
     const float x = s.w[2 * k], y = s.w[2 * k + 1];
     const float t = x * d.x + y * d.y;
-    const bool take = (k < s.n) && !isn(bv) && (isn(t) || t > bv);
+    // bitwise, not short-circuit: && / || compile to exec-mask branches here
+    const bool take = (k < s.n) & !isn(bv) & (isn(t) | (t > bv));
     bv = take ? t : bv;
     bx = take ? x : bx;
     by = take ? y : by;
@@ -341,6 +342,38 @@ CX_DEV v2 support(const WrappedShape& w, v2 d) {
   const float t1 = (w.sn * l.x + w.c * l.y) + w.py * 1.0f;
   const float t2 = (0.0f * l.x + 0.0f * l.y) + 1.0f * 1.0f;
   return v2{t0 / t2, t1 / t2};
+}
+// a shape known to be a polygon (the step kernel's polygon x polygon items):
+// the support without the kind dispatch -- the same select chain, NaN
+// direction as a final select
+struct PolyRef {
+  const Shape& s;
+};
+CX_DEV v2 support(const PolyRef& p, v2 d) {
+  const Shape& s = p.s;
+  float bv = s.w[0] * d.x + s.w[1] * d.y;
+  float bx = s.w[0], by = s.w[1];
+  auto step = [&](int k) {
+    const float x = s.w[2 * k], y = s.w[2 * k + 1];
+    const float t = x * d.x + y * d.y;
+    const bool take = (k < s.n) & !isn(bv) & (isn(t) | (t > bv));
+    bv = take ? t : bv;
+    bx = take ? x : bx;
+    by = take ? y : by;
+  };
+  step(1);
+  step(2);
+  step(3);
+  if (s.n > 4) {
+    step(4);
+    step(5);
+  }
+  if (s.n > 6) {
+    step(6);
+    step(7);
+  }
+  const bool dn = vnan(d);
+  return v2{dn ? qnan() : bx, dn ? qnan() : by};
 }
 template <class SA, class SB>
 CX_DEV v2 minkowski(const SA& a, const SB& b, v2 d) { return sub(support(a, d), support(b, neg(d))); }
@@ -873,22 +906,48 @@ CX_DEV v2 contact_from_edges(const Shape& A, const Shape& B) {
 // kernel, for a part paired with itself -- such a cell is only ever chosen as
 // j == i, which resolution skips, so only the NaN-ness of the contact point
 // is observable; pen is then 0).  Returns whether the shapes collide.
-template <class MakeStore>
-CX_DEV bool gjk_epa(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen, MakeStore make) {
+#if defined(COTIX_PHASE_PROF) && (defined(__HIP__) || defined(__HIPCC__))
+static __device__ unsigned long long g_dev_sub[4];  // phase-timing build: GJK / EPA cycles (tools/phase_prof.py)
+#define CX_DSUB_T0 const unsigned long long cx_dsub_t0 = clock64()
+#define CX_DSUB_T1(k)                                                                                   \
+  do {                                                                                                  \
+    const int l_ = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));             \
+    if (l_ == __builtin_amdgcn_readfirstlane(l_)) atomicAdd(&g_dev_sub[k], clock64() - cx_dsub_t0);  \
+  } while (0)
+#else
+#define CX_DSUB_T0 ((void)0)
+#define CX_DSUB_T1(k) ((void)0)
+#endif
+template <class SA, class SB, class MakeStore>
+CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen,
+                      MakeStore make) {
   static_assert(2 * MAXV + 1 + 3 <= 20, "EPA buffer bound");
   v2 simplex[3];
   *pen = v2{0.0f, 0.0f};
-  if (!gjk(A, B, d0, simplex)) return false;
+#if defined(COTIX_ASM_MARKERS) && (defined(__HIP__) || defined(__HIPCC__))
+  asm volatile(";#GJK_BEGIN");
+#endif
+  const bool hit = gjk(a, b, d0, simplex);
+#if defined(COTIX_ASM_MARKERS) && (defined(__HIP__) || defined(__HIPCC__))
+  asm volatile(";#GJK_END");
+#endif
+  if (!hit) return false;
   const int iters = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
   if (!need_pen) return true;
   if (iters + 3 <= 14) {
     auto es = make.template get<14>();
-    *pen = epa<14, decltype(es)>(A, B, simplex, iters, es);
+    *pen = epa<14, decltype(es)>(a, b, simplex, iters, es);
   } else {
     auto es = make.template get<20>();
-    *pen = epa<20, decltype(es)>(A, B, simplex, iters, es);
+    *pen = epa<20, decltype(es)>(a, b, simplex, iters, es);
   }
   return true;
+}
+// POLY: both shapes are polygons (supports without the kind dispatch)
+template <bool POLY, class MakeStore>
+CX_DEV bool gjk_epa(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen, MakeStore make) {
+  if constexpr (POLY) return gjk_epa_t(PolyRef{A}, PolyRef{B}, A, B, d0, need_pen, pen, make);
+  else return gjk_epa_t(A, B, A, B, d0, need_pen, pen, make);
 }
 struct MakeRegs {
   template <int NE>
@@ -902,12 +961,14 @@ struct MakeCol {
 };
 // GJK, then EPA when the penetration is needed; EPA edges in registers
 CX_DEV bool convex_vs_polygon_pen(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen) {
-  return gjk_epa(A, B, d0, need_pen, pen, MakeRegs{});
+  return gjk_epa<false>(A, B, d0, need_pen, pen, MakeRegs{});
 }
 // the same with EPA edges in a per-lane memory column (the step kernel's LDS)
+// (POLY: both shapes are polygons)
+template <bool POLY>
 CX_DEV bool convex_vs_polygon_pen_col(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen, float* col,
                                       int stride) {
-  return gjk_epa(A, B, d0, need_pen, pen, MakeCol{col, stride});
+  return gjk_epa<POLY>(A, B, d0, need_pen, pen, MakeCol{col, stride});
 }
 CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, v2 d0, bool need_pen = true) {
   Contact c;

@@ -47,6 +47,21 @@ inline Stats g_stats{};
 #else
 #define CXK_STAT(f, v) ((void)0)
 #endif
+// sub-phase cycle timers of the phase-timing build (tools/phase_prof.py):
+// CXK_SUB_T0 / CXK_SUB_T1(k) add the wave's clock delta to slot k (ad-hoc
+// instrumentation; slot 4 is cotix_device.h's CX_DSUB_T0 / CX_DSUB_T1)
+#if defined(COTIX_PHASE_PROF) && (defined(__HIP__) || defined(__HIPCC__))
+static __device__ unsigned long long g_sub_cycles[8];
+#define CXK_SUB_T0 const unsigned long long cxk_sub_t0 = clock64()
+#define CXK_SUB_T1(k, lane)                                                                       \
+  do {                                                                                            \
+    const unsigned long long dt_ = clock64() - cxk_sub_t0;                                        \
+    if ((lane) == __builtin_amdgcn_readfirstlane(lane)) atomicAdd(&cxk::g_sub_cycles[k], dt_); \
+  } while (0)
+#else
+#define CXK_SUB_T0 ((void)0)
+#define CXK_SUB_T1(k, lane) ((void)0)
+#endif
 
 // Scene tables.  Everything the step reads per item is packed into hot[]
 // (word offsets below) and copied to LDS once per launch.
@@ -284,7 +299,19 @@ CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, con
 }
 
 // contact-function sets compiled into a step kernel (scene feature mask)
-enum : int { FNS_ANALYTIC = 1, FNS_CONVEX = 2, FNS_CIRCLE_POLY = 4 };
+// FNS_CONVEX: polygon x polygon GJK/EPA; FNS_AABB_POLY: AABB x polygon too
+// (without it the GJK/EPA supports are compiled for polygons only)
+enum : int { FNS_ANALYTIC = 1, FNS_CONVEX = 2, FNS_CIRCLE_POLY = 4, FNS_AABB_POLY = 8 };
+// the FNSET instantiation of the step kernel for a scene's function set
+// (launcher and host emulation): mode 2 (backward) and analytic scenes get the
+// analytic program, mode 1 (rollout) the full one
+CX_HD int launch_fnset(int fs, int mode) {
+  if (mode == 2 || (fs & ~FNS_ANALYTIC) == 0) return FNS_ANALYTIC;
+  if (mode == 1) return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
+  if ((fs & ~(FNS_ANALYTIC | FNS_CONVEX)) == 0) return FNS_ANALYTIC | FNS_CONVEX;
+  if ((fs & FNS_CIRCLE_POLY) == 0) return FNS_ANALYTIC | FNS_CONVEX | FNS_AABB_POLY;
+  return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
+}
 template <int FNSET>
 CX_DEV cx::Contact run_contact_set(int fn, const cx::Shape& a, const cx::Shape& b, cx::v2 d0, uint32_t* err,
                                    bool self_pair) {
@@ -818,8 +845,10 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
     if ((FNSET & FNS_CONVEX) != 0 && (fn == FN_POLY_POLY || fn == FN_AABB_POLY)) {
       // GJK (+EPA); the contact point is deferred to phase F (wave-cooperative)
       const bool self = ((d0w >> 27) & 1u) != 0u;
-      const bool hit = convex_vs_polygon_pen_col(A, Bs, d0, !self, &ct.pen,
-                                                 reinterpret_cast<float*>(t.ws + c.W.epa + lane), WAVE);
+      float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
+      const bool hit = (FNSET & FNS_AABB_POLY) == 0
+                           ? convex_vs_polygon_pen_col<true>(A, Bs, d0, !self, &ct.pen, col, WAVE)
+                           : convex_vs_polygon_pen_col<false>(A, Bs, d0, !self, &ct.pen, col, WAVE);
       ct.cp = v2{qnan(), qnan()};
       // a part paired with itself: only the NaN-ness of its contact point is
       // observable (such a cell is only ever chosen as j == i, which

@@ -276,7 +276,9 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   for (int c = 0; c < s.nc; ++c) {
     int fn = cfn[c];
     fnset |= (fn == cx::FN_AABB_AABB || fn == cx::FN_CIRCLE_AABB || fn == cx::FN_CIRCLE_CIRCLE) ? FNS_ANALYTIC
-             : (fn == cx::FN_CIRCLE_POLY ? FNS_CIRCLE_POLY : FNS_CONVEX);
+             : fn == cx::FN_CIRCLE_POLY                                                        ? FNS_CIRCLE_POLY
+             : fn == cx::FN_AABB_POLY                                                          ? FNS_CONVEX | FNS_AABB_POLY
+                                                                                               : FNS_CONVEX;
   }
   s.fnset = fnset;
   return 0;

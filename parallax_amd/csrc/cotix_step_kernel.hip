@@ -95,18 +95,21 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
   const dim3 grid((ka.B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);
 #define COTIX_LAUNCH(FS, BW) hipLaunchKernelGGL((step_kernel<EW, FS, BW>), grid, block, lds, st, ka)
 #define COTIX_LAUNCH_SPEC(FS, BW, SP) hipLaunchKernelGGL((step_kernel<EW, FS, BW, SP>), grid, block, lds, st, ka)
+  constexpr int F_AN = FNS_ANALYTIC, F_PP = FNS_ANALYTIC | FNS_CONVEX, F_AP = F_PP | cxk::FNS_AABB_POLY,
+                F_ALL = F_AP | FNS_CIRCLE_POLY;
+  const int F = cxk::launch_fnset(fs, mode);  // the contact-function program for this scene
 #if COTIX_EW == 4  // the default tiling carries the two reference-scene specializations
-  if (spec == cxk::SPEC_ROBOCUP && (fs & ~FNS_ANALYTIC) == 0) {
+  if (spec == cxk::SPEC_ROBOCUP && F == F_AN) {
     if (mode == 2)
-      COTIX_LAUNCH_SPEC(FNS_ANALYTIC, 2, cxk::SPEC_ROBOCUP);
+      COTIX_LAUNCH_SPEC(F_AN, 2, cxk::SPEC_ROBOCUP);
     else if (mode == 1)
-      COTIX_LAUNCH_SPEC(FNS_ANALYTIC, 1, cxk::SPEC_ROBOCUP);
+      COTIX_LAUNCH_SPEC(F_AN, 1, cxk::SPEC_ROBOCUP);
     else
-      COTIX_LAUNCH_SPEC(FNS_ANALYTIC, 0, cxk::SPEC_ROBOCUP);
+      COTIX_LAUNCH_SPEC(F_AN, 0, cxk::SPEC_ROBOCUP);
     return hipGetLastError();
   }
-  if (spec == cxk::SPEC_LUNAR && mode == 0 && (fs & FNS_CIRCLE_POLY) == 0) {
-    COTIX_LAUNCH_SPEC(FNS_ANALYTIC | FNS_CONVEX, 0, cxk::SPEC_LUNAR);
+  if (spec == cxk::SPEC_LUNAR && mode == 0 && F == F_PP) {
+    COTIX_LAUNCH_SPEC(F_PP, 0, cxk::SPEC_LUNAR);
     return hipGetLastError();
   }
 #else
@@ -114,18 +117,20 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
 #endif
 #undef COTIX_LAUNCH_SPEC
   if (mode == 2) {
-    COTIX_LAUNCH(FNS_ANALYTIC, 2);  // the host admits analytic scenes only
+    COTIX_LAUNCH(F_AN, 2);  // the host admits analytic scenes only
   } else if (mode == 1) {
-    if ((fs & ~FNS_ANALYTIC) == 0)
-      COTIX_LAUNCH(FNS_ANALYTIC, 1);
+    if (F == F_AN)
+      COTIX_LAUNCH(F_AN, 1);
     else
-      COTIX_LAUNCH(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, 1);
-  } else if ((fs & ~FNS_ANALYTIC) == 0) {
-    COTIX_LAUNCH(FNS_ANALYTIC, 0);
-  } else if ((fs & FNS_CIRCLE_POLY) == 0) {
-    COTIX_LAUNCH(FNS_ANALYTIC | FNS_CONVEX, 0);
+      COTIX_LAUNCH(F_ALL, 1);
+  } else if (F == F_AN) {
+    COTIX_LAUNCH(F_AN, 0);
+  } else if (F == F_PP) {
+    COTIX_LAUNCH(F_PP, 0);
+  } else if (F == F_AP) {
+    COTIX_LAUNCH(F_AP, 0);
   } else {
-    COTIX_LAUNCH(FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY, 0);
+    COTIX_LAUNCH(F_ALL, 0);
   }
 #undef COTIX_LAUNCH
   return hipGetLastError();
@@ -140,6 +145,16 @@ extern "C" int cotix_phase_cycles(unsigned long long* out, int n) {
   unsigned long long z[cxk::PH_COUNT] = {};
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)) != hipSuccess) return -1;
   for (int q = 0; q < n && q < cxk::PH_COUNT; ++q) out[q] = h[q];
-  return cxk::PH_COUNT;
+  // then the 8 sub-phase timers (CXK_SUB_T1)
+  unsigned long long sub[8] = {};
+  if (hipMemcpyFromSymbol(sub, HIP_SYMBOL(cxk::g_sub_cycles), sizeof(sub)) != hipSuccess) return -1;
+  unsigned long long z8[8] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(cxk::g_sub_cycles), z8, sizeof(z8)) != hipSuccess) return -1;
+  unsigned long long dsub[4] = {};  // GJK timer of cotix_device.h in slot 4
+  if (hipMemcpyFromSymbol(dsub, HIP_SYMBOL(cx::g_dev_sub), sizeof(dsub)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(cx::g_dev_sub), z8, sizeof(dsub)) != hipSuccess) return -1;
+  sub[4] = dsub[0];
+  for (int q = 0; q < 8 && cxk::PH_COUNT + q < n; ++q) out[cxk::PH_COUNT + q] = sub[q];
+  return cxk::PH_COUNT + 8 < n ? cxk::PH_COUNT + 8 : n;
 }
 #endif

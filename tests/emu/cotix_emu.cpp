@@ -42,17 +42,21 @@ void run_blocks(const cxk::KArgs& a, int mode) {
   for (int wv = 0; wv < nwaves; ++wv) {
     std::fill(lds.begin() + sc.nhot, lds.end(), 0x7FBADBADu);  // poison (a NaN pattern)
     const cxk::Tile<EW> t{lds.data() + sc.nhot, lds.data(), lds.data() + sc.nhot + (size_t)c.L.S * EW};
-    // the kernel instantiation the library launches: analytic-only scenes get
-    // the circle/AABB program (FNSET 1), others the full one
-    const bool an = (sc.fnset & ~cxk::FNS_ANALYTIC) == 0;
+    // the kernel instantiation the library launches (cxk::launch_fnset)
+    const int F = cxk::launch_fnset(sc.fnset, mode);
     if (mode == 2)
-      an ? cxk::run_wave_backward<EW, 1>(a, c, t, wv * EW, HostRun{})
-         : cxk::run_wave_backward<EW, 7>(a, c, t, wv * EW, HostRun{});
+      cxk::run_wave_backward<EW, 1>(a, c, t, wv * EW, HostRun{});
     else if (mode == 1)
-      an ? cxk::run_wave<EW, 1, true>(a, c, t, wv * EW, HostRun{}) : cxk::run_wave<EW, 7, true>(a, c, t, wv * EW, HostRun{});
+      F == 1 ? cxk::run_wave<EW, 1, true>(a, c, t, wv * EW, HostRun{})
+             : cxk::run_wave<EW, 15, true>(a, c, t, wv * EW, HostRun{});
+    else if (F == 1)
+      cxk::run_wave<EW, 1, false>(a, c, t, wv * EW, HostRun{});
+    else if (F == 3)
+      cxk::run_wave<EW, 3, false>(a, c, t, wv * EW, HostRun{});
+    else if (F == 11)
+      cxk::run_wave<EW, 11, false>(a, c, t, wv * EW, HostRun{});
     else
-      an ? cxk::run_wave<EW, 1, false>(a, c, t, wv * EW, HostRun{})
-         : cxk::run_wave<EW, 7, false>(a, c, t, wv * EW, HostRun{});
+      cxk::run_wave<EW, 15, false>(a, c, t, wv * EW, HostRun{});
   }
 }
 void run_any(const cxk::KArgs& a, int E, int mode) {

@@ -424,3 +424,47 @@ def test_emu_static_part_straddling_chunks_vs_cport(emu_lib, EW, bp):
     assert same_f32(got[0], want[0])
     for g, w in zip(got[1:], want[1:]):
         assert np.array_equal(g, w)
+
+
+@pytest.mark.parametrize("circle", [False, True], ids=["aabb_poly", "aabb_circle_poly"])
+@pytest.mark.parametrize("EW", [2, 4])
+def test_emu_mixed_kinds_step_vs_cport(emu_lib, EW, circle):
+    """The step kernel's AABB x polygon (and circle x polygon) programs
+    (cxk::launch_fnset 11 / 15): two quads falling onto a static AABB floor
+    (one in contact with the other), optionally a ball; the kernel logic == the
+    C port over 20 steps, 6 envs."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    from cotix_oracle import geometry as G
+    from cotix_oracle import physics as P
+    if not os.path.exists(cport.LIB):
+        pytest.skip("oracle C port not built (make -C oracle)")
+    clib = cport.load()
+    quad = [(-0.5, 0.0), (0.5, 0.0), (0.5, 0.6), (-0.5, 0.6)]
+    bodies = [P.Body([G.Polygon(quad, kind="Polygon4")], position=(0.1, 0.02), velocity=(0.0, -0.4),
+                     angular_velocity=0.2, elasticity=0.5, friction_coefficient=0.2),
+              P.Body([G.Polygon(quad, kind="Polygon4")], position=(0.95, 0.3), angle=0.3, velocity=(-0.2, -0.3),
+                     elasticity=0.5, friction_coefficient=0.2),
+              P.Body([G.AABB((-4.0, -1.0), (4.0, 0.0))], mass=float("inf"), inertia=float("inf"), elasticity=0.5,
+                     friction_coefficient=0.2)]
+    if circle:
+        bodies.insert(2, P.Body([G.Circle(0.3, (0.0, 0.0))], position=(-0.75, 0.25), velocity=(0.3, -0.2),
+                                elasticity=0.5, friction_coefficient=0.2))
+    h, geom = emu.oracle_scene(lib, bodies)
+    sc = cport.Scene(clib, bodies)
+    B, T = 6, 20
+    base = np.array([b.dyn() for b in bodies], np.float32)
+    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
+    dyn[0, 0, :] += np.linspace(-0.3, 0.3, B).astype(np.float32)
+    keys = np.ascontiguousarray(np.stack([np.arange(B) + 3, np.arange(B) * 5 + 1], 1).astype(np.uint32))
+    got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    nb = len(bodies)
+    gch, gcl = emu.step_ex(lib, h, *got, geom, 0, T, 1 | 4 | 16, nb, E=EW)
+    wch, wcl = sc.step_ex(*want, T, 1 | 4 | 16, trace=True)
+    assert (wcl >= 0).sum() > T  # contacts were found
+    assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)

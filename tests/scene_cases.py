@@ -1,0 +1,44 @@
+"""TEST INFRASTRUCTURE: generic scenes (oracle bodies) shared by the CPU
+emulation tests and the GPU parity tests."""
+import numpy as np
+
+
+def straddle_scene(theta):
+    """A falling dynamic quad (body 0, vertex items 0..3) over a static,
+    rotated body 1 of 14 far-away quads and a hexagonal floor under the quad
+    (vertex items 60..65): at one env per wave the floor straddles phase T's
+    first two 64-item chunks.  theta rotates body 1: its world
+    vertex order is a re-sort of the local order."""
+    from cotix_oracle import geometry as G
+    from cotix_oracle import physics as P
+    c, s = np.cos(-theta), np.sin(-theta)
+
+    def local(pts):  # world points of body 1 (at the origin) -> its local frame
+        return [(float(np.float32(x * c - y * s)), float(np.float32(x * s + y * c))) for x, y in pts]
+
+    dummies = [G.Polygon(local([(40 + 5 * i, 0), (42 + 5 * i, 0), (42 + 5 * i, 2), (40 + 5 * i, 2)]), kind="Polygon4")
+               for i in range(14)]
+    floor = G.Polygon(local([(-3, -1), (3, -1), (3.2, -0.5), (3, 0), (-3, 0), (-3.2, -0.5)]), kind="Polygon6")
+    box = G.Polygon([(-0.5, 0.0), (0.5, 0.0), (0.5, 0.6), (-0.5, 0.6)], kind="Polygon4")
+    return [P.Body([box], mass=1.0, inertia=1.0, position=(0.1, 0.05), velocity=(0.0, -0.5), angular_velocity=0.3,
+                   elasticity=0.5, friction_coefficient=0.2),
+            P.Body(dummies + [floor], mass=float("inf"), inertia=float("inf"), angle=theta, elasticity=0.5,
+                   friction_coefficient=0.2)]
+
+
+def mixed_scene(circle):
+    """Two quads falling onto a static AABB floor (one in contact with the
+    other), optionally a ball: AABB x polygon (and circle x polygon) contacts."""
+    from cotix_oracle import geometry as G
+    from cotix_oracle import physics as P
+    quad = [(-0.5, 0.0), (0.5, 0.0), (0.5, 0.6), (-0.5, 0.6)]
+    bodies = [P.Body([G.Polygon(quad, kind="Polygon4")], position=(0.1, 0.02), velocity=(0.0, -0.4),
+                     angular_velocity=0.2, elasticity=0.5, friction_coefficient=0.2),
+              P.Body([G.Polygon(quad, kind="Polygon4")], position=(0.95, 0.3), angle=0.3, velocity=(-0.2, -0.3),
+                     elasticity=0.5, friction_coefficient=0.2),
+              P.Body([G.AABB((-4.0, -1.0), (4.0, 0.0))], mass=float("inf"), inertia=float("inf"), elasticity=0.5,
+                     friction_coefficient=0.2)]
+    if circle:
+        bodies.insert(2, P.Body([G.Circle(0.3, (0.0, 0.0))], position=(-0.75, 0.25), velocity=(0.3, -0.2),
+                                elasticity=0.5, friction_coefficient=0.2))
+    return bodies

@@ -371,29 +371,6 @@ def test_reference_scenes_fit_the_lds(emu_lib):
     assert all(lib.emu_lds_bytes(h, e) <= 160 * 1024 for e in (1, 2, 4))
 
 
-def _straddle_scene(theta):
-    """A falling dynamic quad (body 0, vertex items 0..3) over a static,
-    rotated body 1 of 14 far-away quads and a hexagonal floor under the quad
-    (vertex items 60..65): at one env per wave the floor straddles phase T's
-    first two 64-item chunks.  theta rotates body 1: its world
-    vertex order is a re-sort of the local order."""
-    from cotix_oracle import geometry as G
-    from cotix_oracle import physics as P
-    c, s = np.cos(-theta), np.sin(-theta)
-
-    def local(pts):  # world points of body 1 (at the origin) -> its local frame
-        return [(float(np.float32(x * c - y * s)), float(np.float32(x * s + y * c))) for x, y in pts]
-
-    dummies = [G.Polygon(local([(40 + 5 * i, 0), (42 + 5 * i, 0), (42 + 5 * i, 2), (40 + 5 * i, 2)]), kind="Polygon4")
-               for i in range(14)]
-    floor = G.Polygon(local([(-3, -1), (3, -1), (3.2, -0.5), (3, 0), (-3, 0), (-3.2, -0.5)]), kind="Polygon6")
-    box = G.Polygon([(-0.5, 0.0), (0.5, 0.0), (0.5, 0.6), (-0.5, 0.6)], kind="Polygon4")
-    return [P.Body([box], mass=1.0, inertia=1.0, position=(0.1, 0.05), velocity=(0.0, -0.5), angular_velocity=0.3,
-                   elasticity=0.5, friction_coefficient=0.2),
-            P.Body(dummies + [floor], mass=float("inf"), inertia=float("inf"), angle=theta, elasticity=0.5,
-                   friction_coefficient=0.2)]
-
-
 @pytest.mark.parametrize("bp", [0, 32], ids=["full", "broadphase"])
 @pytest.mark.parametrize("EW", [1, 2, 4])
 def test_emu_static_part_straddling_chunks_vs_cport(emu_lib, EW, bp):
@@ -407,7 +384,43 @@ def test_emu_static_part_straddling_chunks_vs_cport(emu_lib, EW, bp):
     if not os.path.exists(cport.LIB):
         pytest.skip("oracle C port not built (make -C oracle)")
     clib = cport.load()
-    bodies = _straddle_scene(4.0)
+    import scene_cases
+    bodies = scene_cases.straddle_scene(4.0)
+    h, geom = emu.oracle_scene(lib, bodies)
+    sc = cport.Scene(clib, bodies)
+    B, T = 6, 20
+    base = np.array([b.dyn() for b in bodies], np.float32)
+    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
+    dyn[0, 0, :] += np.linspace(-1, 1, B).astype(np.float32)
+    keys = np.ascontiguousarray(np.stack([np.arange(B), np.arange(B) * 7 + 1], 1).astype(np.uint32))
+    got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    gch, gcl = emu.step_ex(lib, h, *got, geom, 0, T, 1 | 4 | 16 | bp, 2, E=EW)
+    wch, wcl = sc.step_ex(*want, T, 1 | 4 | 16, trace=True)
+    assert (wcl[:, 0, 1] >= 0).sum() + (wcl[:, 1, 0] >= 0).sum() > T  # the triangle sits on the floor
+    assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)
+
+
+@pytest.mark.parametrize("circle", [False, True], ids=["aabb_poly", "aabb_circle_poly"])
+@pytest.mark.parametrize("EW", [2, 4])
+def test_emu_mixed_kinds_step_vs_cport(emu_lib, EW, circle):
+    """The step kernel's AABB x polygon (and circle x polygon) programs
+    (cxk::launch_fnset 11 / 15): two quads falling onto a static AABB floor
+    (one in contact with the other), optionally a ball; the kernel logic == the
+    C port over 20 steps, 6 envs."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    from cotix_oracle import geometry as G
+    from cotix_oracle import physics as P
+    if not os.path.exists(cport.LIB):
+        pytest.skip("oracle C port not built (make -C oracle)")
+    clib = cport.load()
+    import scene_cases
+    bodies = scene_cases.mixed_scene(circle)
     h, geom = emu.oracle_scene(lib, bodies)
     sc = cport.Scene(clib, bodies)
     B, T = 6, 20

@@ -1036,3 +1036,62 @@ def test_specialized_kernel_equals_generic(torch_cuda, monkeypatch, scene):
     for g, w in zip(outs[0][1:], outs[1][1:]):
         assert np.array_equal(g, w)
     assert (outs[0][5] >= 0).any()
+
+
+def _world_from_oracle(pa, torch, bodies, B, keys):
+    """A World of B envs of the oracle's bodies (local geometry as the oracle
+    holds it: polygons presorted)."""
+    kinds = {"Polygon": pa.Polygon, "Polygon3": pa.Polygon3, "Polygon4": pa.Polygon4, "Polygon5": pa.Polygon5,
+             "Polygon6": pa.Polygon6}
+    out = []
+    for b in bodies:
+        parts = []
+        for p in b.parts:
+            if p.kind == "AABB":
+                parts.append(pa.AABB(list(p.lower), list(p.upper)))
+            elif p.kind == "Circle":
+                parts.append(pa.Circle(p.radius, list(p.position)))
+            else:
+                parts.append(kinds[p.kind]([list(v) for v in p.vertices_], presorted=True))
+        out.append(pa.AnyBody(shape=pa.UniversalShape(*parts), mass=b.mass, inertia=b.inertia,
+                              position=list(b.position), velocity=list(b.velocity), angle=b.angle,
+                              angular_velocity=b.angular_velocity, elasticity=b.elasticity,
+                              friction_coefficient=b.friction_coefficient))
+    return pa.World(out, B, "cuda", torch.tensor(u32_to_i32(keys), device="cuda"))
+
+
+@pytest.mark.parametrize("scene", ["aabb_poly", "aabb_circle_poly", "straddle", "straddle_ew1"])
+def test_generic_polygon_scenes_vs_cport(torch_cuda, cport_lib, monkeypatch, scene):
+    """The generic step programs on the GPU (cxk::launch_fnset: polygon-only
+    GJK/EPA for the straddling-part scene, AABB x polygon, circle x polygon)
+    against the C port: 512 envs x 24 steps, state, keys, errors and every
+    contact choice.  straddle_ew1: one env per wave, where the static floor
+    straddles phase T's first two vertex-item chunks."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    cport, lib = cport_lib
+    if scene == "straddle_ew1":
+        monkeypatch.setenv("COTIX_ENVS_PER_WAVE", "1")  # read by the library at every launch
+    import scene_cases
+    bodies = scene_cases.straddle_scene(4.0) if scene.startswith("straddle") else scene_cases.mixed_scene(
+        scene == "aabb_circle_poly")
+    B, T = 512, 24
+    keys = np.ascontiguousarray(np.stack([np.arange(B) + 3, np.arange(B) * 5 + 1], 1).astype(np.uint32))
+    w = _world_from_oracle(pa, torch, bodies, B, keys)
+    base = np.array([b.dyn() for b in bodies], np.float32)
+    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
+    dyn[0, 0, :] += np.linspace(-0.6, 0.6, B).astype(np.float32)
+    w.set_dyn(torch.tensor(dyn, device="cuda"))
+    err = np.zeros(B, np.uint32)
+    trc = {}
+    w.step(T, 1e-2, pa._ffi.STAGES_ROBOCUP, trace=trc)
+    sc = cport.Scene(lib, bodies)
+    wch, wcl = sc.step_ex(dyn, keys, err, T, cport.STAGES_ROBOCUP, trace=True, nthreads=16)
+    torch.cuda.synchronize()
+    assert (wcl >= 0).sum() > B
+    got = w.dyn.cpu().numpy()
+    assert same_f32(got, dyn), diff_report(got, dyn)
+    assert np.array_equal(w.keys.cpu().numpy().view(np.uint32), keys)
+    assert np.array_equal(w.err.cpu().numpy().view(np.uint32), err)
+    assert np.array_equal(trc["chosen"].cpu().numpy(), wch)
+    assert np.array_equal(trc["cells"].cpu().numpy(), wcl)

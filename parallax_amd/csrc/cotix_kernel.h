@@ -152,7 +152,7 @@ struct KArgs {
   int action_body;
   const float* dyn_reset;  // [nb][6][B] or null
   uint32_t* resets;        // [B] or null
-  int dbg_skip;            // timing only: skip phase T=1, B=2, C=4, D=8, A's key splits=16, E=32
+  int dbg_skip;            // timing only: skip phase T=1, B=2, C=4, D=8, A's key splits=16, E=32, GJK/EPA=64
   // collider trace (cotix_step_ex; null = off): per step, body and env the
   // chosen partner j* (cotix/_colliders.py:274-295), and per cell (i, j) the
   // reference-scan candidate whose contact all_contacts[i, j] holds (:208-268)
@@ -846,7 +846,8 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
       // GJK (+EPA); the contact point is deferred to phase F (wave-cooperative)
       const bool self = ((d0w >> 27) & 1u) != 0u;
       float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
-      const bool hit = (FNSET & FNS_AABB_POLY) == 0
+      const bool hit = (a.dbg_skip & 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
+                       : (FNSET & FNS_AABB_POLY) == 0
                            ? convex_vs_polygon_pen_col<true>(A, Bs, d0, !self, &ct.pen, col, WAVE)
                            : convex_vs_polygon_pen_col<false>(A, Bs, d0, !self, &ct.pen, col, WAVE);
       ct.cp = v2{qnan(), qnan()};

@@ -881,8 +881,79 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
     }
   }
 }
+// phase B of the analytic program (circle / AABB scenes): the items of up to
+// BQ chunks fetch their descriptors and both shapes first, then compute, so
+// the LDS latency of a chunk overlaps the others instead of adding up
+constexpr int BQ = 4;
+template <int EW>
+CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const int ni = c.nc * EW;
+  for (int base = 0; base < ni; base += BQ * WAVE) {
+    uint32_t dw[BQ];
+    float ga[BQ][4], gb[BQ][4];
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int w0 = base + q * WAVE + lane, w = w0 < ni ? w0 : ni - 1;  // clamped: every read in range
+      dw[q] = t.tb[sc.o_cdesc + 2 * (w / EW)];
+    }
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int w0 = base + q * WAVE + lane, w = w0 < ni ? w0 : ni - 1;
+      const int e = w % EW;
+      const int wa = c.L.world + (int)(dw[q] & 1023u), wb = c.L.world + (int)((dw[q] >> 10) & 1023u);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ga[q][k] = t.f(wa + k, e);
+        gb[q][k] = t.f(wb + k, e);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int w = base + q * WAVE + lane, e = w % EW, ci = w / EW;
+      if (w >= ni || env0 + e >= a.B) continue;
+      CXK_STAT(b_items, 1);
+      Shape A, Bs;
+      A.kind = (int)((dw[q] >> 23) & 3u);
+      Bs.kind = (int)((dw[q] >> 25) & 3u);
+      A.n = Bs.n = 0;
+#pragma unroll
+      for (int k = 0; k < 2 * MAXV; ++k) {
+        A.w[k] = k < 4 ? ga[q][k] : 0.0f;
+        Bs.w[k] = k < 4 ? gb[q][k] : 0.0f;
+      }
+      uint32_t er = 0u;
+      const Contact ct = run_contact_set<FNS_ANALYTIC>((int)((dw[q] >> 20) & 7u), A, Bs, v2{sc.d0x, sc.d0y}, &er,
+                                                       ((dw[q] >> 27) & 1u) != 0u);
+      const int co = c.L.con + 4 * ci;
+      t.f(co + 0, e) = ct.pen.x;
+      t.f(co + 1, e) = ct.pen.y;
+      t.f(co + 2, e) = ct.cp.x;
+      t.f(co + 3, e) = ct.cp.y;
+      if (!(isn(ct.cp.x) || isn(ct.cp.y))) {
+#if defined(__HIP__) || defined(__HIPCC__)
+        atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
+#else
+        t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
+#endif
+      }
+      if (er) {
+#if defined(__HIP__) || defined(__HIPCC__)
+        atomicOr(&t.w(c.L.err, e), er);
+#else
+        t.w(c.L.err, e) |= er;
+#endif
+      }
+    }
+  }
+}
 template <int EW, int FNSET>
 CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  if constexpr (FNSET == FNS_ANALYTIC) {
+    ph_B_analytic<EW>(a, c, t, env0, lane);
+    return;
+  }
   for (int w = lane; w < c.nc * EW; w += WAVE) {
     if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly) t.ws[c.W.cf_flag + w] = 0u;
     b_item<EW, FNSET>(a, c, t, env0, lane, w);

@@ -607,8 +607,11 @@ template <int EW>
 CX_DEV bool pose_kept(const Ctx& c, Tile<EW> t, int b, int e) {
   const Lay& L = c.L;
   const int o = L.dyn + 6 * b, q = L.pose + 3 * b;
-  return ((t.w(L.pcv, e) >> b) & 1u) != 0u && t.w(o, e) == t.w(q, e) && t.w(o + 1, e) == t.w(q + 1, e) &&
-         t.w(o + 4, e) == t.w(q + 2, e);
+  // every word read unconditionally (a short-circuit chain of LDS reads
+  // compiles to one round trip per read)
+  const uint32_t v = t.w(L.pcv, e), p0 = t.w(o, e), p1 = t.w(o + 1, e), p2 = t.w(o + 4, e);
+  const uint32_t q0 = t.w(q, e), q1 = t.w(q + 1, e), q2 = t.w(q + 2, e);
+  return (((v >> b) & 1u) != 0u) & (p0 == q0) & (p1 == q1) & (p2 == q2);
 }
 // TV0 (item = (body, env)): flag the bodies whose world parts must be rebuilt
 // this step, then record the poses they will be built from
@@ -617,7 +620,7 @@ CX_DEV void ph_TV0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
   const Lay& L = c.L;
   for (int w = lane; w < c.nb * EW; w += WAVE) {
     const int e = w % EW, b = w / EW;
-    const bool redo = env0 + e < a.B && !pose_kept<EW>(c, t, b, e);
+    const bool redo = (env0 + e < a.B) & !pose_kept<EW>(c, t, b, e);
     if (w < WAVE) t.ws[WS_FLAG + w] = redo ? 1u : 0u;
     t.w(L.pose + 3 * b, e) = t.w(L.dyn + 6 * b, e);
     t.w(L.pose + 3 * b + 1, e) = t.w(L.dyn + 6 * b + 1, e);
@@ -1159,7 +1162,7 @@ CX_DEV void ph_C0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, 
     const int e = id % EW, l = id / EW;
     if (env0 + e < a.B) {
       bool any = false;
-      for (int q = 0; q < sc.nmw; ++q) any = any || (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
+      for (int q = 0; q < sc.nmw; ++q) any |= (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
       if (any) {
         flag = 1u;
         t.ws[WS_LIST + 2 * c.nl * EW + id] = 0u;  // scan position
@@ -1270,7 +1273,7 @@ CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
     const int e = lane % EW, l = lane / EW;
     if (env0 + e < a.B) {
       bool any = false;
-      for (int q = 0; q < sc.nmw; ++q) any = any || (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
+      for (int q = 0; q < sc.nmw; ++q) any |= (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
       if (any) {
         flag = 1u;
         t.ws[WS_LIST + 2 * c.nl * EW + lane] = 0u;  // scan position

@@ -389,6 +389,22 @@ CX_DEV uint64_t wave_ballot(const uint32_t* flags, int lane) {
 #endif
 }
 CX_DEV int popc64(uint64_t m) { return __builtin_popcountll(m); }
+// the number of lanes whose flag is set, after every lane stored its flag
+// (`mine`) at flags[lane] in this phase: lane WAVE-1 gets it (the host
+// emulation runs that lane last); called convergently at the top level
+CX_DEV int wave_count_stored(const uint32_t* flags, int lane, bool mine) {
+#if defined(__HIP__) || defined(__HIPCC__)
+  (void)flags;
+  (void)lane;
+  return __builtin_popcountll((uint64_t)__ballot(mine));
+#else
+  (void)mine;
+  int n = 0;
+  if (lane == WAVE - 1)
+    for (int l = 0; l < WAVE; ++l) n += flags[l] != 0u ? 1 : 0;
+  return n;
+#endif
+}
 CX_DEV uint64_t lanes_below(int lane) { return lane == 0 ? 0ull : ((1ull << lane) - 1ull); }
 
 // LDS views: scene hot tables + this wave's [word][env] tile
@@ -1299,16 +1315,17 @@ CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
   }
 #endif
   t.ws[WS_KEEP + lane] = flag;
+  const int n = wave_count_stored(t.ws + WS_KEEP, lane, flag != 0u);  // pending items of round 1
+  if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)n;
 }
-// M1: the pending count (read after the phase: 0 ends the scan), then every
-// lane draws one candidate: G = 64 / n lanes per pending item, in mask order
+// M1 (n > 0 pending items): every lane draws one candidate: G = 64 / n lanes
+// per pending item, in mask order
 template <int EW>
 CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par, int kso) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
   const int n = popc64(pend);
-  if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)n;
   uint32_t pass = 0u;
   if (n > 0) {
     const int G = WAVE / n, slot = lane / G, q = lane % G;
@@ -1356,6 +1373,9 @@ CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
     }
   }
   t.ws[(par ? WS_KEEP : WS_KEEP2) + lane] = keep;
+  // the next round's pending count (read after the phase: 0 ends the scan)
+  const int n = wave_count_stored(t.ws + (par ? WS_KEEP : WS_KEEP2), lane, keep != 0u);
+  if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)n;
 }
 
 // phase D: choose_random_contact (cotix/_colliders.py:274-295)
@@ -1960,12 +1980,11 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
   if (!(a.dbg_skip & 4) && c.nl > 0 && c.nl * EW <= WAVE) {
     run(PH_C0, [&](int l) { ph_M0<EW>(a, c, t, env0, l); });
     CXK_STAT(wave_steps, 1);
-    for (int par = 0;; par ^= 1) {
-      run(PH_C1, [&](int l) { ph_M1<EW>(c, t, l, par, kso); });
-      if (t.ws[WS_N] == 0u) break;  // uniform: read after the phase barrier
+    for (int par = 0; t.ws[WS_N] != 0u; par ^= 1) {  // uniform: read after the phase barrier
       CXK_STAT(rounds, 1);
       if (par == 0) CXK_STAT(active_items, t.ws[WS_N]);
       if (par == 1) CXK_STAT(r1_left, t.ws[WS_N]);
+      run(PH_C1, [&](int l) { ph_M1<EW>(c, t, l, par, kso); });
       run(PH_C2, [&](int l) { ph_M2<EW>(c, t, l, par); });
     }
   } else if (!(a.dbg_skip & 4) && c.nl > 0) {

@@ -816,22 +816,22 @@ CX_DEV bool self_cp_finite(const cx::Shape& P) {
   bool ok = true, any = false;
   const float lim = 1.152921504606846976e18f;  // 2^60
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k)
-    if (k < P.n) ok = ok && __builtin_fabsf(P.w[2 * k]) < lim && __builtin_fabsf(P.w[2 * k + 1]) < lim;
+  for (int k = 0; k < MAXV; ++k)  // bitwise: no short-circuit branches
+    ok = ok & ((k >= P.n) | ((__builtin_fabsf(P.w[2 * k]) < lim) & (__builtin_fabsf(P.w[2 * k + 1]) < lim)));
   // vertex k - 1 and k - 2 (cyclic): v_{k-1} is the previous slot, or the
   // last vertex for k = 0; v_{k-2} the one before that
   v2 prev2 = vert(P, P.n - 2), prev = vert(P, P.n - 1);
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k)
-    if (k < P.n) {
-      const v2 vk = v2{P.w[2 * k], P.w[2 * k + 1]};
-      const v2 r = sub(prev, vk), sv = sub(prev2, prev);
-      prev2 = prev;
-      prev = vk;
-      const float cr = r.x * sv.y - sv.x * r.y;
-      any = any || cr != 0.0f;
-    }
-  return ok && any;
+  for (int k = 0; k < MAXV; ++k) {
+    const bool in = k < P.n;
+    const v2 vk = v2{P.w[2 * k], P.w[2 * k + 1]};
+    const v2 r = sub(prev, vk), sv = sub(prev2, prev);
+    const float cr = r.x * sv.y - sv.x * r.y;
+    any = any | (in & (cr != 0.0f));
+    prev2 = in ? prev : prev2;
+    prev = in ? vk : prev;
+  }
+  return ok & any;
 }
 
 template <int EW, int FNSET>
@@ -993,31 +993,51 @@ template <int EW>
 CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
-  for (int w = lane; w < c.W.bl_pad; w += WAVE) {
-    uint32_t keep = 0u;
-    if (w < c.nc * EW) {
-      t.ws[c.W.cf_flag + w] = 0u;
-      const int e = w % EW, ci = w / EW;
-      if (env0 + e < a.B) {
-        keep = 1u;
-        const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
-        const int fn = (int)((d0w >> 20) & 7u);
-        if (fn == FN_POLY_POLY || fn == FN_AABB_POLY) {
-          // the parts' world AABBs, built with the world parts in phase T
-          const int ba = c.L.pbox + 4 * (int)((d1w >> 16) & 255u), bb = c.L.pbox + 4 * (int)(d1w >> 24);
-          float A[4], B[4];
+  const int ni = c.nc * EW;
+  // BQ chunks at a time: every chunk's descriptors, then every box, are read
+  // before any is used (the chunks' LDS latencies overlap)
+  for (int base = 0; base < c.W.bl_pad; base += BQ * WAVE) {
+    uint32_t d1[BQ];
+    bool poly[BQ];
+    float A[BQ][4], B[BQ][4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            A[k] = t.f(ba + k, e);
-            B[k] = t.f(bb + k, e);
-          }
+    for (int q = 0; q < BQ; ++q) {
+      const int w0 = base + q * WAVE + lane, w = w0 < ni ? w0 : ni - 1;  // clamped: every read in range
+      const uint32_t d0w = t.tb[sc.o_cdesc + 2 * (w / EW)];
+      d1[q] = t.tb[sc.o_cdesc + 2 * (w / EW) + 1];
+      const int fn = (int)((d0w >> 20) & 7u);
+      poly[q] = (fn == FN_POLY_POLY) | (fn == FN_AABB_POLY);
+    }
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int w0 = base + q * WAVE + lane, w = w0 < ni ? w0 : ni - 1;
+      const int e = w % EW;
+      // the parts' world AABBs, built with the world parts in phase T
+      const int ba = c.L.pbox + 4 * (int)((d1[q] >> 16) & 255u), bb = c.L.pbox + 4 * (int)(d1[q] >> 24);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        A[q][k] = t.f(ba + k, e);
+        B[q][k] = t.f(bb + k, e);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int w = base + q * WAVE + lane;
+      if (w >= c.W.bl_pad) continue;
+      uint32_t keep = 0u;
+      if (w < ni) {
+        t.ws[c.W.cf_flag + w] = 0u;
+        const int e = w % EW, ci = w / EW;
+        if (env0 + e < a.B) {
+          keep = 1u;
           // S and the gap with NaN-propagating max: any NaN box word keeps the full path
           float S = 0.0f;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) S = cx::fmax_(S, cx::fmax_(__builtin_fabsf(A[k]), __builtin_fabsf(B[k])));
+          for (int k = 0; k < 4; ++k) S = cx::fmax_(S, cx::fmax_(__builtin_fabsf(A[q][k]), __builtin_fabsf(B[q][k])));
           const float margin = S * 0.00390625f + 1.52587890625e-05f;  // 2^-8 S + 2^-16
-          const float gap = cx::fmax_(cx::fmax_(B[0] - A[2], A[0] - B[2]), cx::fmax_(B[1] - A[3], A[1] - B[3]));
-          if (gap > margin) {  // false for NaN
+          const float gap = cx::fmax_(cx::fmax_(B[q][0] - A[q][2], A[q][0] - B[q][2]),
+                                      cx::fmax_(B[q][1] - A[q][3], A[q][1] - B[q][3]));
+          if (poly[q] && gap > margin) {  // false for NaN
             keep = 0u;
             const int co = c.L.con + 4 * ci;
             t.f(co + 0, e) = 0.0f;
@@ -1027,8 +1047,8 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
           }
         }
       }
+      t.ws[c.W.bl_flag + w] = keep;
     }
-    t.ws[c.W.bl_flag + w] = keep;
   }
 }
 // BP1: append chunk `chunk`'s flagged items to the B list

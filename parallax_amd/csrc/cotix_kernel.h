@@ -1553,6 +1553,14 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
+  uint32_t jv[NB];
+  bool any = false;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    jv[i] = t.w(L.rp + RP_W * i + RP_J, e);
+    any = any | (jv[i] != RP_NONE);
+  }
+  if (!REC && !any) return;  // no resolution this step: the velocities stay as they are
   float vx[NB], vy[NB], vw[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -1561,14 +1569,12 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
     vw[b] = t.f(L.dyn + 6 * b + 5, e);
   }
   // every resolution's operands up front: one LDS latency for the pass
-  uint32_t jv[NB];
   ResPre pr[NB];
   Params pj[NB], pi[NB];
   Rcp qj[NB], qi[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int ro = L.rp + RP_W * i;
-    jv[i] = t.w(ro + RP_J, e);
     pr[i] = load_rp<EW>(t, ro, e);
     pj[i] = Params{t.f(ro + RP_MJ, e), t.f(ro + RP_IJ, e), 0.0f, 0.0f};
     qj[i] = Rcp{t.f(ro + RP_QMJ, e), t.f(ro + RP_QIJ, e)};

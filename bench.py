@@ -250,6 +250,11 @@ def sub_step(pa, dev, name, B, substeps, steps, warmup):
     out = {"workload": WORKLOAD[name] % B, "substeps_per_launch": substeps, "launches": steps,
            "value": B * substeps * steps / wall, "unit": "env-steps/s", "launch_ms": ev_ms,
            "hbm_GBs": bytes_per_env(name, len(scen.bodies)) * B / (ev_ms * 1e-3) / 1e9}
+    v = valu_roofline(name, B, substeps, ev_ms)
+    if v is not None:  # the committed PMC pass of this workload (profiles/latest_pmc_<name>.json)
+        out["valu"] = {"achieved": v["valu_instr_per_launch"] / (ev_ms * 1e-3) / 1e9,
+                       "frac": v["valu_instr_per_launch"] / (ev_ms * 1e-3) / VALU_PEAK_WAVE_INSTR_S,
+                       "unit": "G wave-instr/s", "traffic": v["traffic"], "source": v["source"]}
     out.update(finite_stats(pa, make_scenario(pa, name, dev, B), 1, 64))
     return out
 

@@ -96,6 +96,18 @@ WORKLOAD = {"robocup": "RoboCup (cotix/_robocup.py) %d envs/GPU",
             "box": "BoxWorld (balls in a box, finite dynamics; not a reference scenario) %d envs/GPU"}
 
 
+def obs_checksum(obs):
+    """Position-weighted checksum of an observation tensor's bit patterns,
+    exact in int64 (each product < 2^63, sums < 2^53): two weightings mod
+    2^31 - 1, packed into one int64."""
+    M = 2147483647
+    v = (obs.contiguous().view(torch.int32).reshape(-1).to(torch.int64) & 0xFFFFFFFF) % M
+    i = torch.arange(1, v.numel() + 1, dtype=torch.int64, device=v.device)
+    a = ((v * (i * 48271 % M)) % M).sum() % M
+    b = ((v * (i * 69621 % M)) % M).sum() % M
+    return a * M + b
+
+
 def timed_launches(fn, steps, warmup):
     """`warmup` untimed calls, then `steps` calls bracketed by synchronize;
     HIP events around each call on the current stream.  Returns (wall s,
@@ -149,6 +161,8 @@ def valu_roofline(scenario, B, substeps, launch_ms):
         c = pmc["config"]
         if not (c.get("envs_per_gpu") == B and c.get("substeps_per_launch") == substeps):
             return None
+        if c.get("library") != library_build():  # counters of other kernel code: no frac
+            return None
         return {"valu_instr_per_launch": pmc["counters_per_launch"]["SQ_INSTS_VALU"],
                 "traffic": pmc["hbm_bytes_per_launch_corrected"],
                 "source": "profiles/%s_%s_summary.json" % (pmc["tag"], scenario),
@@ -156,6 +170,13 @@ def valu_roofline(scenario, B, substeps, launch_ms):
                 "pmc_avg_launch_ms": pmc["avg_launch_ns"] * 1e-6}
     except (OSError, KeyError, ValueError):
         return None
+
+
+def library_build():
+    """cotix_version() of the loaded libcotix_amd.so: it carries the build id
+    (hash of the kernel sources and flags, __graft_entry__.build_id)."""
+    from parallax_amd import _ffi
+    return _ffi.lib.cotix_version().decode()
 
 
 def roofline(scenario, B, substeps, launch_ms, nb):
@@ -170,7 +191,10 @@ def roofline(scenario, B, substeps, launch_ms, nb):
                    "2 cycles per wave64 instruction (one wave per SIMD issues at most half of it); "
                    "hbm = algorithmic bytes / launch time, reported because north_star asks"}
     v = valu_roofline(scenario, B, substeps, launch_ms)
-    if v is not None:
+    if v is None:
+        out["frac_note"] = ("no committed PMC pass (profiles/latest_pmc_%s.json) of this library build and "
+                            "workload: frac left null rather than mixing counters of other code" % scenario)
+    else:
         ach = v["valu_instr_per_launch"] / (launch_ms * 1e-3)
         out.update(achieved=ach / 1e9, frac=ach / VALU_PEAK_WAVE_INSTR_S, traffic=v["traffic"],
                    traffic_source=v["source"], valu_active_frac_of_wave_cycles=v["valu_active_frac_of_wave_cycles"],
@@ -365,11 +389,18 @@ def main():
     wall = float(tmax.item())
     resets = int(env.resets.sum().item())
     gather = None
-    if dist is not None:  # the gathered tensor holds this rank's local observation in its slice
+    if dist is not None:
+        # every slice of the gathered tensor must be its owner's local observation:
+        # each rank publishes a checksum of its own obs bits, every rank checks all slices
         last = (launches[0] - 1) % 2
         local = env.observation()
-        mine = obs_all[last][rank * B:(rank + 1) * B]
-        gather = "ok" if torch.equal(mine.view(torch.int32), local.view(torch.int32)) else "MISMATCH"
+        sums = torch.zeros(world_size, dtype=torch.int64, device=dev)
+        sums[rank] = obs_checksum(local)
+        dist.all_reduce(sums)
+        got = torch.stack([obs_checksum(obs_all[last][r * B:(r + 1) * B]) for r in range(world_size)])
+        bad = torch.tensor([int((got != sums).sum().item())], dtype=torch.int64, device=dev)
+        dist.all_reduce(bad)
+        gather = "ok (%d slices checked on every rank)" % world_size if int(bad.item()) == 0 else "MISMATCH"
         if a.dump_gather and rank == 0:
             np.savez(a.dump_gather, gathered=obs_all[last].cpu().numpy(), local=local.cpu().numpy(),
                      dyn=env.world.dyn.cpu().numpy())
@@ -396,6 +427,7 @@ def main():
             "envs_per_gpu": B,
             "substeps_per_launch": a.substeps,
             "autoreset_on_error": True,
+            "library": library_build(),
             "episode_restarts": resets,
             "restarts_per_env_step": resets / (B * a.substeps * (a.steps + a.warmup)),
             "parallelism": "dp%d (independent env shards by global env id, RCCL obs all-gather)" % world_size,

@@ -186,7 +186,13 @@ __global__ void lunar_kernel(float* dyn, int B, cx::Params p0, cx::Params p1, cx
 extern "C" {
 
 const char* cotix_last_error(void) { return g_err.c_str(); }
-const char* cotix_version(void) { return "cotix_amd 0.1 (gfx950)"; }
+#ifndef COTIX_BUILD_ID
+#define COTIX_BUILD_ID "unknown"
+#endif
+// the build id is a hash of the kernel sources + compile flags (__graft_entry__.build_id):
+// profiles/latest_pmc_*.json are keyed to it, so a counter pass of older code is never
+// divided by a newer kernel's time (bench.py)
+const char* cotix_version(void) { return "cotix_amd 0.2 (gfx950) build " COTIX_BUILD_ID; }
 
 
 int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,

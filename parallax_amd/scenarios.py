@@ -25,6 +25,18 @@ F = np.float32
 INF = float("inf")
 
 
+def env_range(batch, env_offset, total_envs):
+    """Validated global env range of a (shard) batch: returns total_envs.
+    Every slice of a global key split goes through here, so a shard outside
+    the global batch is an error, not a short key tensor."""
+    batch, env_offset = int(batch), int(env_offset)
+    total = batch if total_envs is None else int(total_envs)
+    if batch < 0 or env_offset < 0 or env_offset + batch > total:
+        raise ValueError("env range [%d, %d) outside the global batch of %d envs"
+                         % (env_offset, env_offset + batch, total))
+    return total
+
+
 # ---------------------------------------------------------------------------
 # RoboCup
 # ---------------------------------------------------------------------------
@@ -67,9 +79,7 @@ def robocup_perturbation(B, seed=2, device="cuda", offset=0, total=None):
     split(PRNGKey(seed), total)[g] -> (kp, kv, kw) = split(., 3): ball position
     U([-4.4,4.4] x [-2.9,2.9]), velocity U([-2,2]^2), angular velocity
     U(-10,10).  Returns the ball's [6, B] dynamic columns."""
-    total = B if total is None else int(total)
-    if offset < 0 or offset + B > total:
-        raise ValueError("env range [offset, offset+B) outside the global batch")
+    total = env_range(B, offset, total)
     k = jr.split(jr.PRNGKey(seed, device), total)[offset:offset + B].contiguous()
     kk = jr.split(k, 3)
     u = jr.uniform(kk[:, 0], 2)
@@ -96,7 +106,7 @@ class RoboCupEnv:
     def __init__(self, batch=1, device="cuda", keys=None, perturb=False, perturb_seed=2, env_offset=0,
                  total_envs=None):
         self.bodies = robocup_bodies()
-        total = batch if total_envs is None else int(total_envs)
+        total = env_range(batch, env_offset, total_envs)
         if keys is None:
             keys = jr.split(jr.PRNGKey(3, device), total)[env_offset:env_offset + batch].contiguous()
         self.world = World(self.bodies, batch, device, keys)
@@ -152,7 +162,7 @@ class BoxWorld:
 
     def __init__(self, batch=1, device="cuda", seed=9, env_offset=0, total_envs=None):
         self.bodies = box_world_bodies()
-        total = batch if total_envs is None else int(total_envs)
+        total = env_range(batch, env_offset, total_envs)
         sl = slice(env_offset, env_offset + batch)
         keys = jr.split(jr.PRNGKey(seed + 1, device), total)[sl].contiguous()
         self.world = World(self.bodies, batch, device, keys)

@@ -61,6 +61,8 @@ class World:
         self.geom = self._upload_geometry()
         self.geom_stride = 0 if self.geom.dim() == 1 else self.geom.shape[1]
         self.dyn = torch.stack([b.dyn_columns(self.B) for b in self.bodies], 0).to(self.device).contiguous()
+        if keys is not None and tuple(keys.shape) != (self.B, 2):
+            raise ValueError("keys must be [B, 2] = [%d, 2], got %s" % (self.B, tuple(keys.shape)))
         self.keys = (keys if keys is not None else torch.zeros(self.B, 2, dtype=torch.int32)).to(
             self.device, torch.int32).contiguous()
         self.err = torch.zeros(self.B, dtype=torch.int32, device=self.device)
@@ -92,24 +94,38 @@ class World:
     def polygon_min_angle(self):
         """Smallest interior angle (degrees) of any polygon part of the uploaded
         geometry, over every env (180 when the scene has no polygon; NaN
-        geometry gives NaN)."""
-        g = self.geom.detach().to("cpu", torch.float64)
+        geometry gives NaN).  Computed on the geometry's device in float64;
+        only the scalar comes back."""
+        g = self.geom.detach()
         amin, off = 180.0, 0
         for p in self.scene.parts:
             n = p.geom_floats()
             if isinstance(p, AbstractPolygon):
-                v = g[..., off:off + n].reshape(*g.shape[:-1], n // 2, 2)
+                v = g[..., off:off + n].to(torch.float64).reshape(*g.shape[:-1], n // 2, 2)
                 a, b = v.roll(1, -2) - v, v.roll(-1, -2) - v
                 cr = (a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]).abs()
-                m = float(torch.rad2deg(torch.atan2(cr, (a * b).sum(-1))).min())
+                m = float(torch.rad2deg(torch.atan2(cr, (a * b).sum(-1))).min())  # torch's min propagates NaN
                 amin = m if not (m >= amin) else amin  # NaN sticks
             off += n
         return amin
 
     def broadphase_ok(self):
         """The condition COTIX_STAGE_BROADPHASE asks its caller to certify:
-        every polygon interior angle >= 0.5 degrees (include/cotix_amd.h)."""
-        return self.polygon_min_angle() >= 0.5
+        every polygon interior angle >= 0.5 degrees (include/cotix_amd.h).
+        Cached per geometry tensor and its in-place version counter, so an
+        edit of world.geom (in place or by replacement) is re-checked."""
+        key = (id(self.geom), self.geom._version)
+        if getattr(self, "_bp_key", None) != key:
+            self._bp_ok = self.polygon_min_angle() >= 0.5
+            self._bp_key = key
+        return self._bp_ok
+
+    def _stages(self, stages):
+        """The broadphase bit survives only while the geometry still meets
+        its condition (the bit never changes results, only skips work)."""
+        if stages & _ffi.STAGE_BROADPHASE and not self.broadphase_ok():
+            return stages & ~_ffi.STAGE_BROADPHASE
+        return stages
 
     # -- state access -----------------------------------------------------
     def body(self, i):
@@ -145,13 +161,14 @@ class World:
         if dyn_reset is None and trace is None:
             _ffi.check(_ffi.lib.cotix_step(
                 self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.keys), _ffi.ptr(self.err),
-                _ffi.ptr(self.geom), self.geom_stride, self.B, int(n_steps), float(dt), int(stages),
+                _ffi.ptr(self.geom), self.geom_stride, self.B, int(n_steps), float(dt), int(self._stages(stages)),
                 _ffi.ptr(action), int(action_body), s), "cotix_step")
             return self
         _ffi.check(_ffi.lib.cotix_step_ex(
             self.scene.handle, _ffi.ptr(self.dyn), _ffi.ptr(self.keys), _ffi.ptr(self.err), _ffi.ptr(self.geom),
-            self.geom_stride, self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(action), int(action_body),
-            _ffi.ptr(dyn_reset), _ffi.ptr(resets), _ffi.ptr(chosen), _ffi.ptr(cells), s), "cotix_step_ex")
+            self.geom_stride, self.B, int(n_steps), float(dt), int(self._stages(stages)), _ffi.ptr(action),
+            int(action_body), _ffi.ptr(dyn_reset), _ffi.ptr(resets), _ffi.ptr(chosen), _ffi.ptr(cells), s),
+            "cotix_step_ex")
         return self
 
     def step_state(self, dyn, keys, err, n_steps=1, dt=1e-2, stages=_ffi.STAGES_ROBOCUP, action=None,
@@ -167,7 +184,7 @@ class World:
                 raise ValueError("action must be [n_steps, B, 2]")
         _ffi.check(_ffi.lib.cotix_step(
             self.scene.handle, _ffi.ptr(dyn), _ffi.ptr(keys), _ffi.ptr(err), _ffi.ptr(self.geom), self.geom_stride,
-            self.B, int(n_steps), float(dt), int(stages), _ffi.ptr(action), int(action_body),
+            self.B, int(n_steps), float(dt), int(self._stages(stages)), _ffi.ptr(action), int(action_body),
             _ffi.stream_ptr(self.device)), "cotix_step")
 
     # -- body-level operators (UniversalShape, cotix/_universal_shape.py:87-132) --

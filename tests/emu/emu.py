@@ -10,7 +10,11 @@ P_ = ctypes.c_void_p
 
 
 def load(asan=False):
+    """The host build (tests/emu/Makefile; __graft_entry__.build() builds the
+    plain one).  Missing is an error, not a skip."""
     path = os.path.join(HERE, "build", "libcotix_emu_asan.so" if asan else "libcotix_emu.so")
+    if not os.path.exists(path):
+        raise FileNotFoundError("%s missing: run `make -C tests/emu` (or python __graft_entry__.py)" % path)
     lib = ctypes.CDLL(path)
     lib.emu_scene_create.argtypes = [ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.POINTER(P_)]
     lib.emu_step.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,

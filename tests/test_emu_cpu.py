@@ -25,6 +25,12 @@ def emu_lib():
     return emu, emu.load()
 
 
+def _build_cport():
+    """The oracle's C port (make -C oracle): built here when missing -- a
+    missing checker is never a skip."""
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "..", "oracle")], check=True)
+
+
 def same_f32(a, b):
     a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
     na, nb = np.isnan(a), np.isnan(b)
@@ -148,8 +154,7 @@ def test_emu_robocup_autoreset_vs_cport(emu_lib):
     sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
     from cotix_oracle import cport
     from cotix_oracle import physics as P
-    if not os.path.exists(cport.LIB):
-        pytest.skip("oracle C port not built (make -C oracle)")
+    _build_cport()
     clib = cport.load()
     dyn, keys = cport.robocup_batch(64)
     dyn, keys = np.ascontiguousarray(dyn, np.float32), np.ascontiguousarray(keys, np.uint32)
@@ -176,8 +181,7 @@ def test_emu_trace_actions_autoreset_vs_cport(emu_lib, EW):
     sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
     from cotix_oracle import cport
     from cotix_oracle import physics as P
-    if not os.path.exists(cport.LIB):
-        pytest.skip("oracle C port not built (make -C oracle)")
+    _build_cport()
     clib = cport.load()
     B, T = 96, 18
     dyn, keys = cport.robocup_batch(B)
@@ -212,8 +216,7 @@ def test_emu_lunar_trace_vs_cport(emu_lib, bp):
     from cotix_oracle import cport
     from cotix_oracle import physics as P
     from cotix_oracle import prng
-    if not os.path.exists(cport.LIB):
-        pytest.skip("oracle C port not built (make -C oracle)")
+    _build_cport()
     clib = cport.load()
     B, T = 24, 10
     tk = prng.split(prng.PRNGKey(0), B)
@@ -308,8 +311,7 @@ def test_emu_lunar_restarts_move_static_body_vs_cport(emu_lib, EW, bp):
     from cotix_oracle import cport
     from cotix_oracle import physics as P
     from cotix_oracle import prng
-    if not os.path.exists(cport.LIB):
-        pytest.skip("oracle C port not built (make -C oracle)")
+    _build_cport()
     clib = cport.load()
     B, T = 20, 9
     tk = prng.split(prng.PRNGKey(4), B)
@@ -381,8 +383,7 @@ def test_emu_static_part_straddling_chunks_vs_cport(emu_lib, EW, bp):
     emu, lib = emu_lib
     sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
     from cotix_oracle import cport
-    if not os.path.exists(cport.LIB):
-        pytest.skip("oracle C port not built (make -C oracle)")
+    _build_cport()
     clib = cport.load()
     import scene_cases
     bodies = scene_cases.straddle_scene(4.0)
@@ -416,8 +417,7 @@ def test_emu_mixed_kinds_step_vs_cport(emu_lib, EW, circle):
     from cotix_oracle import cport
     from cotix_oracle import geometry as G
     from cotix_oracle import physics as P
-    if not os.path.exists(cport.LIB):
-        pytest.skip("oracle C port not built (make -C oracle)")
+    _build_cport()
     clib = cport.load()
     import scene_cases
     bodies = scene_cases.mixed_scene(circle)
@@ -451,8 +451,7 @@ def test_emu_mixed_kinds_step_vs_cport(emu_lib, EW, circle):
     from cotix_oracle import cport
     from cotix_oracle import geometry as G
     from cotix_oracle import physics as P
-    if not os.path.exists(cport.LIB):
-        pytest.skip("oracle C port not built (make -C oracle)")
+    _build_cport()
     clib = cport.load()
     quad = [(-0.5, 0.0), (0.5, 0.0), (0.5, 0.6), (-0.5, 0.6)]
     bodies = [P.Body([G.Polygon(quad, kind="Polygon4")], position=(0.1, 0.02), velocity=(0.0, -0.4),

@@ -41,7 +41,7 @@ def counts(n_ratio):
 def ci():
     import torch
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        pytest.fail("-m gpu test without a visible GPU (torch.cuda.is_available() is False)")
     import contact_invariants
     return contact_invariants
 

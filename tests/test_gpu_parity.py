@@ -39,7 +39,7 @@ def diff_report(a, b):
 def torch_cuda():
     import torch
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        pytest.fail("-m gpu test without a visible GPU (torch.cuda.is_available() is False)")
     return torch
 
 
@@ -331,9 +331,11 @@ def test_lunar_4096_sampled_oracle(torch_cuda):
 # ---------------------------------------------------------------------------
 @pytest.fixture(scope="module")
 def cport_lib():
+    """The C port of the oracle.  A missing build is a FAILURE under -m gpu,
+    never a skip: these tests are the north star's index-parity evidence."""
     from cotix_oracle import cport
-    if not os.path.exists(cport.LIB):
-        pytest.skip("oracle C port not built (make -C oracle)")
+    assert os.path.exists(cport.LIB), ("oracle C port %s missing: build it before the GPU run "
+                                       "(python __graft_entry__.py, or make -C oracle)" % cport.LIB)
     return cport, cport.load()
 
 

@@ -33,6 +33,10 @@
  *   cotix_render          env.draw(painter) via Painter callbacks  cotix/_viz.py:55-75,
  *                         cotix/_robocup.py:140-150, cotix/_lunar_lander.py:220-225
  *   cotix_check_state     class_invariant  cotix/_design_by_contract.py:80-107
+ *   cotix_eval            AbstractEnvironment.eval     cotix/_envs.py:37-132 with a
+ *                         device AbstractJudge (:9-28) / AbstractControl
+ *                         (cotix/_controls.py:16-27); also env.step() -> (obs,
+ *                         reward, done) of the north star
  */
 #ifndef COTIX_AMD_H
 #define COTIX_AMD_H
@@ -148,6 +152,69 @@ int cotix_step_autoreset(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_
 int cotix_step_ex(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
                   int B, int n_steps, float dt, int stages, const float* action, int action_body,
                   const float* dyn_reset, uint32_t* resets, int32_t* chosen, int32_t* cells, cotix_stream_t stream);
+
+/* Device judge: AbstractJudge (cotix/_envs.py:9-28) in the form the step
+ * kernel evaluates after every env-step.  s = the env's state words
+ * [n_bodies*6] (body-major: px, py, vx, vy, angle, angular_velocity):
+ *   judge(s)      = sum_k rate_w[k] * s[k]                       (reward rate)
+ *   end_reward(s) = sum_k end_w[k] * s[k]  (+ region_reward[r] for the first
+ *                   region r that holds s)
+ *   is_done(s)    = some region holds s, or (done_on_error and the env's
+ *                   error bits are set -- the reference raises there)
+ * Sums run in k order over the NONZERO weights (at most 16 each), starting
+ * from the first term (none: 0).  Region r holds s when region_lo[r][q] <
+ * s[6*region_body[r] + q] < region_hi[r][q] for every q (NaN is never inside;
+ * +-inf leaves a word free). */
+#define COTIX_JUDGE_REGIONS 4
+#define COTIX_MAX_STATE_WORDS 96
+typedef struct cotix_judge {
+  float rate_w[COTIX_MAX_STATE_WORDS];
+  float end_w[COTIX_MAX_STATE_WORDS];
+  int n_regions;
+  int region_body[COTIX_JUDGE_REGIONS];
+  float region_lo[COTIX_JUDGE_REGIONS][6];
+  float region_hi[COTIX_JUDGE_REGIONS][6];
+  float region_reward[COTIX_JUDGE_REGIONS];
+  int done_on_error;
+} cotix_judge;
+
+/* Device control: AbstractControl (cotix/_controls.py:16-27) whose dense
+ * signal is a velocity impulse on `body`, re-evaluated before every env-step
+ * from that body's state s[6] and added after Euler (world.forward(state,
+ * signal), cotix/_envs.py:72-75):
+ *   dv[i] = sum_q gain[i][q] * (target[i][q] - s[q])  (nonzero gains, q order,
+ *           from the first term)  + bias[i] (if nonzero) */
+typedef struct cotix_control {
+  int body;
+  float gain[2][6];
+  float target[2][6];
+  float bias[2];
+} cotix_control;
+
+/* AbstractEnvironment.eval (cotix/_envs.py:37-132) fused into ONE launch:
+ * num_NFEs x WFE_scale env-steps (n_steps = n_nfe * wfe, dt per env-step),
+ * per env with the reference's carry -- at each NFE start end_reward is taken
+ * (unless finished) and is_done checked; after every env-step the first done
+ * state becomes the premature out with reward + end_reward; reward +=
+ * judge(s) * dt; at the NFE end a done env takes its premature out (state,
+ * key, err, reward) and `finished` is set.
+ *   judge      nullable host struct (NULL: no reward / done bookkeeping)
+ *   control    nullable host struct (NULL: no device control)
+ *   action     nullable device f32 [B][2]: a held impulse added to action_body
+ *              every env-step after Euler (env.step(action))
+ *   reward     device f32 [B] in/out (the carry's reward; zero it for a fresh eval)
+ *   finished   device u32 [B] in/out (the carry's flag)
+ *   reset_mode 0: none; 2: envs finished at entry restart from dyn_reset
+ *              (err, finished cleared, resets[env]++, key chain continues) --
+ *              next-step autoreset for env.step(); 1: restart on error bits
+ *              after each env-step (cotix_step_autoreset; judge must be NULL)
+ *   obs        nullable device f32 [B][n_bodies][6]: the final observation,
+ *              written by the same launch */
+int cotix_eval(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
+               int B, int n_nfe, int wfe, float dt, int stages, const cotix_judge* judge,
+               const cotix_control* control, const float* action, int action_body, float* reward,
+               uint32_t* finished, int reset_mode, const float* dyn_reset, uint32_t* resets, float* obs,
+               cotix_stream_t stream);
 
 /* Differentiable rollout (BASELINE config 5: grad(return)/d(action) through a
  * fused n_steps RoboCup rollout).  The reference has no return or action

@@ -7,7 +7,9 @@ from . import _ffi  # noqa: F401  (raises ImportError when the HIP library is mi
 from . import random  # noqa: F401
 from . import contracts, render  # noqa: F401
 from .bodies import AnyBody, BodyView  # noqa: F401
-from .env import BatchedEnv  # noqa: F401
+from .env import BatchedEnv, StepResult  # noqa: F401
+from .envs import (AbstractEnvironment, AffineControl, LinearJudge, PhysicsWorld, VelocityImpulse,  # noqa: F401
+                   WorldState)
 from .physics import (ContactInfo, ExplicitEulerPhysics, RandomizedCollider, SimpleConstraintSolver,  # noqa: F401
                       contact_funcs, resolve_collision, run_contacts)
 from .rollout import rollout as differentiable_rollout  # noqa: F401
@@ -16,4 +18,4 @@ from .scenarios import BoxWorld, LunarLander, RoboCupEnv  # noqa: F401
 from .shapes import AABB, Circle, Polygon, Polygon3, Polygon4, Polygon5, Polygon6, UniversalShape  # noqa: F401
 from .world import Scene, World  # noqa: F401
 
-__version__ = "0.1.0"
+__version__ = "0.2.0"

@@ -23,6 +23,22 @@ ERR_STATE_NONFINITE = 4
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
+JUDGE_REGIONS = 4
+MAX_STATE_WORDS = 96
+
+
+class CotixJudge(ctypes.Structure):
+    """struct cotix_judge (include/cotix_amd.h)."""
+    _fields_ = [("rate_w", _F * MAX_STATE_WORDS), ("end_w", _F * MAX_STATE_WORDS), ("n_regions", _I),
+                ("region_body", _I * JUDGE_REGIONS), ("region_lo", (_F * 6) * JUDGE_REGIONS),
+                ("region_hi", (_F * 6) * JUDGE_REGIONS), ("region_reward", _F * JUDGE_REGIONS),
+                ("done_on_error", _I)]
+
+
+class CotixControl(ctypes.Structure):
+    """struct cotix_control (include/cotix_amd.h)."""
+    _fields_ = [("body", _I), ("gain", (_F * 6) * 2), ("target", (_F * 6) * 2), ("bias", _F * 2)]
+
 
 SIGNATURES = {
     "cotix_scene_create": (_I, [_I, _P, _I, _P, _P, _P, ctypes.POINTER(_P)]),
@@ -32,6 +48,8 @@ SIGNATURES = {
     "cotix_step": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P]),
     "cotix_step_autoreset": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
     "cotix_step_ex": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P, _P]),
+    "cotix_eval": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, ctypes.POINTER(CotixJudge),
+                        ctypes.POINTER(CotixControl), _P, _I, _P, _P, _I, _P, _P, _P, _P]),
     "cotix_rollout": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P, _P]),
     "cotix_rollout_backward": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P]),
     "cotix_body_penetration": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),

@@ -137,6 +137,23 @@ CX_HD SceneHdr spec_hdr(SceneHdr h) {
   return h;
 }
 
+// device judge and control of cotix_eval (include/cotix_amd.h: cotix_judge,
+// cotix_control), compacted by the host: the nonzero weights as (word, w)
+// terms in word order -- the sums run over them in that order, starting from
+// the first term
+constexpr int JT = 16, JR = 4;
+struct JudgeArgs {
+  int on, nrate, nend, nreg, doe;
+  uint8_t rate_k[JT], end_k[JT];
+  float rate_w[JT], end_w[JT];
+  int rbody[JR];
+  float lo[JR][6], hi[JR][6], rrew[JR];
+};
+struct CtlArgs {
+  int on, body;
+  float gain[2][6], target[2][6], bias[2];
+};
+
 // kernel arguments (passed by value)
 struct KArgs {
   const SceneDev* sc;
@@ -165,11 +182,21 @@ struct KArgs {
   float* grad_action;      // backward: [n_steps][B][2] d ret / d action
   float* grad_dyn;         // backward: [nb*6][B] d ret / d initial state, or null
   float ret_w[MAXB * 6];
+  // cotix_eval (AbstractEnvironment.eval, cotix/_envs.py:37-132, fused):
+  int reset_mode;          // 1: restart on error bits after a step (dyn_reset); 2: restart envs finished at entry
+  int action_held;         // 1: action is [B][2], the same impulse every step (a held control signal)
+  float* obs;              // [B][nb][6] final observation, or null
+  float* reward;           // [B] in/out: the eval carry's reward (judge on)
+  uint32_t* finished;      // [B] in/out: the eval carry's `finished` flag (judge on)
+  int nfe_len;             // env-steps per NFE (WFE_scale); n_steps is a multiple of it (judge on)
+  JudgeArgs judge;         // device AbstractJudge (judge.on == 0: off)
+  CtlArgs ctl;             // device AbstractControl (ctl.on == 0: off)
 };
 
 // per-wave tile layout (words, each x EW envs)
 struct Lay {
-  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, geo, rp, kw, kww, rflag, pose, pcv, pbox, S;
+  int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, geo, rp, kw, kww, rflag, pose, pcv, pbox,
+      jfin, jal, jr, jpr, jk, je, jsn, S;
 };
 // key window: the per-step keys of KWIN consecutive steps, precomputed
 // together (phase K) -- the collider keys depend on the key chain only, never
@@ -205,7 +232,17 @@ CX_HD Lay layout(int nb, int np, int W, int nc, int nt, int G) {
   L.pose = L.rflag + 1;             // per body: the pose (px, py, angle bits) its world parts were built from
   L.pcv = L.pose + 3 * nb;          // bit b: body b's pose entry is valid (cleared at every launch start)
   L.pbox = L.pcv + 1;               // per part: world AABB (lo.x, lo.y, up.x, up.y), polygon scenes (broadphase)
-  L.S = L.pbox + 4 * np;
+  // cotix_eval's carry (judge on): finished, already_premature_outted, reward,
+  // the premature-out reward, key and err; the premature-out state itself is
+  // kept in rst (free in eval: its restarts are taken at entry, reset_mode 2)
+  L.jfin = L.pbox + 4 * np;
+  L.jal = L.jfin + 1;
+  L.jr = L.jal + 1;
+  L.jpr = L.jr + 1;
+  L.jk = L.jpr + 1;
+  L.je = L.jk + 2;
+  L.jsn = L.je + 1;                 // this step's state becomes the premature out
+  L.S = L.jsn + 1;
   return L;
 }
 static inline int tile_words(const SceneHdr& s) { return layout(s.nb, s.np, s.W, s.nc, s.nt, s.G).S; }
@@ -445,23 +482,32 @@ template <int EW>
 CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   if (c.sh.poly)  // phase F's flag array incl. its padding to a multiple of 64
     for (int w = lane; w < c.W.cf_list - c.W.cf_flag; w += WAVE) t.ws[c.W.cf_flag + w] = 0u;
+  // reset_mode 2 (cotix_eval's next-step autoreset): an env finished at entry
+  // starts from its reset state (key chain continues, err and finished cleared)
+  const bool r2 = a.reset_mode == 2 && a.dyn_reset != nullptr && a.finished != nullptr;
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
-    t.f(c.L.dyn + off, e) = (g < a.B) ? a.dyn[(size_t)off * a.B + g] : 0.0f;
+    const bool rs = r2 && g < a.B && a.finished[g] != 0u;
+    t.f(c.L.dyn + off, e) = (g < a.B) ? (rs ? a.dyn_reset : a.dyn)[(size_t)off * a.B + g] : 0.0f;
   }
   ph_geo<EW>(a, c, t, env0, lane);
-  if (a.dyn_reset != nullptr)
+  if (a.dyn_reset != nullptr && a.reset_mode == 1)
     for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
       int e = w % EW, off = w / EW, g = env0 + e;
       t.f(c.L.rst + off, e) = (g < a.B) ? a.dyn_reset[(size_t)off * a.B + g] : 0.0f;
     }
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
+    const bool rs = r2 && g < a.B && a.finished[g] != 0u;
     t.w(c.L.key, e) = (g < a.B) ? a.keys[2 * (size_t)g] : 0u;
     t.w(c.L.key + 1, e) = (g < a.B) ? a.keys[2 * (size_t)g + 1] : 0u;
-    t.w(c.L.err, e) = (g < a.B) ? a.err[g] : 0u;
-    t.w(c.L.nres, e) = 0u;
+    t.w(c.L.err, e) = (g < a.B && !rs) ? a.err[g] : 0u;
+    t.w(c.L.nres, e) = rs ? 1u : 0u;
     t.w(c.L.pcv, e) = 0u;  // no world part built yet in this launch (phase T)
+    if (a.judge.on) {
+      t.w(c.L.jfin, e) = (g < a.B && !rs && a.finished != nullptr) ? (a.finished[g] != 0u ? 1u : 0u) : 0u;
+      t.f(c.L.jr, e) = (g < a.B && a.reward != nullptr) ? a.reward[g] : 0.0f;
+    }
   }
 }
 
@@ -518,10 +564,35 @@ CX_DEV void ph_K2(const Ctx& c, Tile<EW> t, int lane, int n) {
 // (backward re-play from saved keys) they are split here.
 // Euler (cotix/_physics_solvers.py:16-33) + the driver's velocity terms for
 // body b of env e (examples/test_viz.py:27-31; the config-5 action hook)
+// the device control's velocity impulse from the body's state before the
+// step (cotix_control): dv[i] = sum_q gain[i][q] * (target[i][q] - s[q]) over
+// the nonzero gains in q order (from the first term), then + bias[i] if nonzero
+template <int EW>
+CX_DEV cx::v2 control_dv(const KArgs& a, Tile<EW> t, int o, int e) {
+  float dv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float acc = 0.0f;
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      if (a.ctl.gain[i][q] != 0.0f) {  // kernel-argument constant: uniform branch
+        const float term = a.ctl.gain[i][q] * (a.ctl.target[i][q] - t.f(o + q, e));
+        acc = any ? acc + term : term;
+        any = true;
+      }
+    if (a.ctl.bias[i] != 0.0f) acc = any ? acc + a.ctl.bias[i] : a.ctl.bias[i];
+    dv[i] = acc;
+  }
+  return cx::v2{dv[0], dv[1]};
+}
+
 template <int EW>
 CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int b, int step) {
   const int o = c.L.dyn + b * 6;
-  if (!(a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))) return;
+  const bool ctl = a.ctl.on && b == a.ctl.body;
+  const cx::v2 dv = ctl ? control_dv<EW>(a, t, o, e) : cx::v2{0.0f, 0.0f};
+  if (!(a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))) return;  // (ph_A calls only with either)
   if (a.stages & COTIX_STAGE_EULER) {
     t.f(o + 0, e) = t.f(o + 0, e) + t.f(o + 2, e) * a.dt;
     t.f(o + 1, e) = t.f(o + 1, e) + t.f(o + 3, e) * a.dt;
@@ -532,9 +603,13 @@ CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e
     t.f(o + 3, e) = t.f(o + 3, e) + -0.002f;
   }
   if (a.action != nullptr && b == a.action_body) {
-    const float* ac = a.action + ((size_t)step * a.B + env0 + e) * 2;
+    const float* ac = a.action + ((size_t)(a.action_held ? 0 : step) * a.B + env0 + e) * 2;
     t.f(o + 2, e) = t.f(o + 2, e) + ac[0];
     t.f(o + 3, e) = t.f(o + 3, e) + ac[1];
+  }
+  if (ctl) {  // world.forward(state, signal): the impulse after Euler (cotix/_envs.py:72-75)
+    t.f(o + 2, e) = t.f(o + 2, e) + dv.x;
+    t.f(o + 3, e) = t.f(o + 3, e) + dv.y;
   }
 }
 // per-step collider scratch: all_contacts cells empty (:137-140), choice =
@@ -1735,7 +1810,7 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
       t.w(L.key, e) = t.w(kso, e);
       t.w(L.key + 1, e) = t.w(kso + 1, e);
     }
-    if (a.dyn_reset != nullptr) {
+    if (a.dyn_reset != nullptr && a.reset_mode == 1) {
       // episode end on an error_if trip (the reference raises here): the env
       // restarts from its reset state (phase R, spread over the lanes); the
       // key chain continues.
@@ -1780,6 +1855,113 @@ CX_DEV void ph_R(const Ctx& c, Tile<EW> t, int lane) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// cotix_eval: the reference's NFE loop (cotix/_envs.py:37-117) per env, with
+// the device judge.  The carry (finished, reward) lives in the tile; the
+// premature-out state in rst, its key / err / reward in jk, je, jpr.
+// ---------------------------------------------------------------------------
+template <int EW>
+CX_DEV float judge_lin(Tile<EW> t, int o, int e, int n, const uint8_t* k, const float* w) {
+  float acc = 0.0f;
+  for (int q = 0; q < n; ++q) {
+    const float term = w[q] * t.f(o + k[q], e);
+    acc = q == 0 ? term : acc + term;
+  }
+  return acc;
+}
+// the first region holding the env's state (strictly inside every bound), or -1
+template <int EW>
+CX_DEV int judge_region(const JudgeArgs& j, Tile<EW> t, int o, int e) {
+  for (int r = 0; r < j.nreg; ++r) {
+    bool in = true;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const float v = t.f(o + 6 * j.rbody[r] + q, e);
+      in = in & (j.lo[r][q] < v) & (v < j.hi[r][q]);
+    }
+    if (in) return r;
+  }
+  return -1;
+}
+template <int EW>
+CX_DEV float judge_end(const JudgeArgs& j, Tile<EW> t, int o, int e, int r) {
+  float acc = judge_lin<EW>(t, o, e, j.nend, j.end_k, j.end_w);
+  if (r >= 0) acc = j.nend > 0 ? acc + j.rrew[r] : j.rrew[r];
+  return acc;
+}
+template <int EW>
+CX_DEV bool judge_done(const JudgeArgs& j, Tile<EW> t, int e, int r, int err_off) {
+  return r >= 0 || (j.doe && t.w(err_off, e) != 0u);
+}
+// NFE start (:43-65), one lane per env: end_reward = finished ? reward :
+// reward + end_reward(s); premature_out = (s, end_reward);
+// already = is_done(s).  The state words are snapshot by ph_JS.
+template <int EW>
+CX_DEV void ph_JB(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  const Lay& L = c.L;
+  for (int e = lane; e < EW; e += WAVE) {
+    if (env0 + e >= a.B) continue;
+    const int r = judge_region<EW>(a.judge, t, L.dyn, e);
+    const float R = t.f(L.jr, e);
+    t.f(L.jpr, e) = t.w(L.jfin, e) != 0u ? R : R + judge_end<EW>(a.judge, t, L.dyn, e, r);
+    t.w(L.jal, e) = judge_done<EW>(a.judge, t, e, r, L.err) ? 1u : 0u;
+    t.w(L.jk, e) = t.w(L.key, e);
+    t.w(L.jk + 1, e) = t.w(L.key + 1, e);
+    t.w(L.je, e) = t.w(L.err, e);
+    t.w(L.jsn, e) = 1u;
+  }
+}
+// after each env-step (:77-108): ending = reward + end_reward(s); the first
+// step that is done becomes the premature out; reward += rate(s) * dt
+template <int EW>
+CX_DEV void ph_J(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  const Lay& L = c.L;
+  for (int e = lane; e < EW; e += WAVE) {
+    if (env0 + e >= a.B) continue;
+    const int r = judge_region<EW>(a.judge, t, L.dyn, e);
+    const float R = t.f(L.jr, e);
+    const bool now = judge_done<EW>(a.judge, t, e, r, L.err) && t.w(L.jal, e) == 0u;
+    if (now) {
+      t.f(L.jpr, e) = R + judge_end<EW>(a.judge, t, L.dyn, e, r);
+      t.w(L.jal, e) = 1u;
+      t.w(L.jk, e) = t.w(L.key, e);
+      t.w(L.jk + 1, e) = t.w(L.key + 1, e);
+      t.w(L.je, e) = t.w(L.err, e);
+    }
+    t.w(L.jsn, e) = now ? 1u : 0u;
+    t.f(L.jr, e) = R + judge_lin<EW>(t, L.dyn, e, a.judge.nrate, a.judge.rate_k, a.judge.rate_w) * a.dt;
+  }
+}
+// the premature-out state words of the envs flagged by ph_JB / ph_J, item = (word, env)
+template <int EW>
+CX_DEV void ph_JS(const Ctx& c, Tile<EW> t, int lane) {
+  const Lay& L = c.L;
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    const int e = w % EW, off = w / EW;
+    if (t.w(L.jsn, e) != 0u) t.f(L.rst + off, e) = t.f(L.dyn + off, e);
+  }
+}
+// NFE end (:110-117): an env that is done takes its premature out; finished = already
+template <int EW>
+CX_DEV void ph_JE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  const Lay& L = c.L;
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
+    const int e = w % EW, off = w / EW;
+    if (t.w(L.jal, e) != 0u) t.f(L.dyn + off, e) = t.f(L.rst + off, e);
+  }
+  for (int e = lane; e < EW; e += WAVE) {
+    if (env0 + e >= a.B) continue;
+    const bool al = t.w(L.jal, e) != 0u;
+    if (al) {
+      t.w(L.key, e) = t.w(L.jk, e);
+      t.w(L.key + 1, e) = t.w(L.jk + 1, e);
+      t.w(L.err, e) = t.w(L.je, e);
+      t.f(L.jr, e) = t.f(L.jpr, e);
+    }
+    t.w(L.jfin, e) = al ? 1u : 0u;
+  }
+}
+
 template <int EW, bool ROLL = false>
 CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
@@ -1794,6 +1976,19 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
       a.err[g] = t.w(c.L.err, e);
       if (a.resets) a.resets[g] += t.w(c.L.nres, e);
       if (ROLL) a.ret[g] += t.f(c.L.ret, e);
+      if (!ROLL && a.judge.on) {
+        if (a.reward) a.reward[g] = t.f(c.L.jr, e);
+        if (a.finished) a.finished[g] = t.w(c.L.jfin, e);
+      }
+    }
+  }
+  // the observation [B][nb][6]: the wave's EW envs are one contiguous block,
+  // item = (env, word) with the word fastest -> coalesced stores
+  if (!ROLL && a.obs != nullptr) {
+    const int nw = c.nb * 6;
+    for (int w = lane; w < nw * EW; w += WAVE) {
+      const int e = w / nw, off = w % nw, g = env0 + e;
+      if (g < a.B) a.obs[(size_t)g * nw + off] = t.f(c.L.dyn + off, e);
     }
   }
 }
@@ -1960,7 +2155,7 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
              PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_TRACE, PH_BP0, PH_BP1, PH_F0, PH_F1, PH_F2, PH_F3,
-             PH_TV0, PH_TV1, PH_TV2, PH_TV3, PH_COUNT };
+             PH_TV0, PH_TV1, PH_TV2, PH_TV3, PH_J, PH_COUNT };
 // ---------------------------------------------------------------------------
 // kso: tile offset of this step's sk0 (skt follows): the key window slot, or
 // L.sk0 where phase A splits the keys (backward re-play)
@@ -2040,6 +2235,10 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
   });
   const bool keys = (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !(a.dbg_skip & 16);
+  if (!ROLL && a.judge.on) {  // the first NFE's start
+    run(PH_J, [&](int l) { ph_JB<EW>(a, c, t, env0, l); });
+    run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });
+  }
 
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
@@ -2057,9 +2256,20 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!(a.dbg_skip & 32)) {
       run(PH_E1, [&](int l) { ph_E<EW>(a, c, t, env0, l, kso); });
-      if (a.dyn_reset != nullptr) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
+      if (a.dyn_reset != nullptr && a.reset_mode == 1) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     }
     if (ROLL) run(PH_RET, [&](int l) { ph_ret<EW>(a, c, t, env0, l); });
+    if (!ROLL && a.judge.on) {  // cotix_eval: NFE bookkeeping (cotix/_envs.py:77-117)
+      run(PH_J, [&](int l) { ph_J<EW>(a, c, t, env0, l); });
+      run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });
+      if ((step + 1) % a.nfe_len == 0) {
+        run(PH_J, [&](int l) { ph_JE<EW>(a, c, t, env0, l); });
+        if (step + 1 < a.n_steps) {
+          run(PH_J, [&](int l) { ph_JB<EW>(a, c, t, env0, l); });
+          run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });
+        }
+      }
+    }
   }
   run(PH_STORE, [&](int l) { ph_store<EW, ROLL>(a, c, t, env0, l); });
 }

@@ -284,4 +284,57 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   return 0;
 }
 
+// cotix_eval's judge / control (include/cotix_amd.h) -> the kernel's compact
+// arguments: the nonzero weights as (word, w) terms in word order.  nw = the
+// scene's state words (n_bodies * 6).
+inline int pack_judge(const cotix_judge* j, int nw, int nb, JudgeArgs& out, std::string& err) {
+  out = JudgeArgs{};
+  if (j == nullptr) return 0;
+  out.on = 1;
+  for (int k = 0; k < COTIX_MAX_STATE_WORDS; ++k) {
+    if (j->rate_w[k] != 0.0f || j->end_w[k] != 0.0f) {
+      if (k >= nw) return scene_fail(err, "judge weight on a state word beyond the scene's bodies");
+      if (std::isnan(j->rate_w[k]) || std::isnan(j->end_w[k])) return scene_fail(err, "NaN judge weight");
+    }
+    if (j->rate_w[k] != 0.0f) {
+      if (out.nrate == JT) return scene_fail(err, "more than 16 nonzero judge rate weights");
+      out.rate_k[out.nrate] = (uint8_t)k;
+      out.rate_w[out.nrate++] = j->rate_w[k];
+    }
+    if (j->end_w[k] != 0.0f) {
+      if (out.nend == JT) return scene_fail(err, "more than 16 nonzero judge end-reward weights");
+      out.end_k[out.nend] = (uint8_t)k;
+      out.end_w[out.nend++] = j->end_w[k];
+    }
+  }
+  if (j->n_regions < 0 || j->n_regions > JR) return scene_fail(err, "judge n_regions outside [0, 4]");
+  out.nreg = j->n_regions;
+  for (int r = 0; r < out.nreg; ++r) {
+    if (j->region_body[r] < 0 || j->region_body[r] >= nb) return scene_fail(err, "judge region body out of range");
+    out.rbody[r] = j->region_body[r];
+    for (int q = 0; q < 6; ++q) {
+      out.lo[r][q] = j->region_lo[r][q];
+      out.hi[r][q] = j->region_hi[r][q];
+    }
+    out.rrew[r] = j->region_reward[r];
+  }
+  out.doe = j->done_on_error ? 1 : 0;
+  return 0;
+}
+inline int pack_control(const cotix_control* ct, int nb, CtlArgs& out, std::string& err) {
+  out = CtlArgs{};
+  if (ct == nullptr) return 0;
+  if (ct->body < 0 || ct->body >= nb) return scene_fail(err, "control body out of range");
+  out.on = 1;
+  out.body = ct->body;
+  for (int i = 0; i < 2; ++i) {
+    for (int q = 0; q < 6; ++q) {
+      out.gain[i][q] = ct->gain[i][q];
+      out.target[i][q] = ct->target[i][q];
+    }
+    out.bias[i] = ct->bias[i];
+  }
+  return 0;
+}
+
 }  // namespace cxk

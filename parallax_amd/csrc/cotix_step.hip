@@ -304,9 +304,49 @@ static int step_impl(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* e
   ka.action = action;
   ka.action_body = action_body;
   ka.dyn_reset = dyn_reset;
+  ka.reset_mode = dyn_reset ? 1 : 0;
   ka.resets = resets;
   ka.trace_chosen = chosen;
   ka.trace_cells = cells;
+  return launch(scene, ka, 0, stream);
+}
+
+int cotix_eval(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
+               int B, int n_nfe, int wfe, float dt, int stages, const cotix_judge* judge,
+               const cotix_control* control, const float* action, int action_body, float* reward,
+               uint32_t* finished, int reset_mode, const float* dyn_reset, uint32_t* resets, float* obs,
+               cotix_stream_t stream) {
+  if (n_nfe < 0 || wfe < 0) return fail("negative size");
+  if (check_step_args(scene, dyn, keys, geom, geom_stride, B, n_nfe * wfe, stages, action, action_body)) return -1;
+  if (!err) return fail("null argument");
+  if (reset_mode < 0 || reset_mode > 2) return fail("reset_mode must be 0, 1 or 2");
+  if (reset_mode != 0 && !dyn_reset) return fail("reset_mode needs dyn_reset");
+  if (reset_mode == 1 && judge) return fail("reset_mode 1 (restart on error) cannot be combined with a judge");
+  if (reset_mode == 2 && !finished) return fail("reset_mode 2 needs finished");
+  if (judge && (!reward || !finished)) return fail("a judge needs reward and finished");
+  if (B == 0 || n_nfe == 0 || wfe == 0) return 0;
+  cxk::KArgs ka{};
+  const int nb = scene->host.nb;
+  if (cxk::pack_judge(judge, nb * 6, nb, ka.judge, g_err) || cxk::pack_control(control, nb, ka.ctl, g_err)) return -1;
+  ka.dyn = dyn;
+  ka.keys = keys;
+  ka.err = err;
+  ka.geom = geom;
+  ka.gstride = geom_stride;
+  ka.B = B;
+  ka.n_steps = n_nfe * wfe;
+  ka.nfe_len = wfe;
+  ka.dt = dt;
+  ka.stages = stages;
+  ka.action = action;
+  ka.action_held = 1;
+  ka.action_body = action_body;
+  ka.reward = reward;
+  ka.finished = finished;
+  ka.reset_mode = reset_mode;
+  ka.dyn_reset = dyn_reset;
+  ka.resets = resets;
+  ka.obs = obs;
   return launch(scene, ka, 0, stream);
 }
 

@@ -2,43 +2,90 @@
 the reference's intended env API is the non-functional
 AbstractEnvironment.eval, cotix/_envs.py:37-132).
 
-  env = BatchedEnv(RoboCupEnv(batch=4096, perturb=True))
+  env = BatchedEnv(RoboCupEnv(batch=4096, perturb=True), autoreset=True)
   env.reset()
-  env.step(n_steps=64)          # 64 driver steps fused in one launch
-  obs = env.observation()       # f32 [B, n_bodies, 6]
+  obs = env.step(n_steps=64)          # 64 driver steps fused in one launch
+
+With a device judge (parallax_amd.envs.LinearJudge) the step is an RL step:
+
+  env = BatchedEnv(scen, judge=LinearJudge(...), autoreset=True)
+  obs, reward, done = env.step(action)    # action f32 [B, 2], held over n_steps
+
+One launch (cotix_eval) advances every env, integrates the judge's reward
+rate, applies is_done / end_reward exactly as one NFE of the reference's eval
+(a done env is frozen at its first done state and receives its end reward),
+and writes the observation.  autoreset=True restarts an env that was done at
+the previous call at the start of this one (next-step autoreset: the terminal
+observation is returned once, then the env restarts from its reset state with
+its key chain continuing).
 """
+from collections import namedtuple
+
 import torch
+
+StepResult = namedtuple("StepResult", ["obs", "reward", "done"])
 
 
 class BatchedEnv:
-    def __init__(self, scenario, dt=1e-2, autoreset=False):
+    def __init__(self, scenario, dt=1e-2, autoreset=False, judge=None, control=None):
         self.scenario = scenario
         self.world = scenario.world
         self.dt = dt
         self.autoreset = autoreset
-        self.resets = torch.zeros(self.world.B, dtype=torch.int32, device=self.world.device)
-        self._keys0 = self.world.keys.clone()
+        w = self.world
+        self.resets = torch.zeros(w.B, dtype=torch.int32, device=w.device)
+        self._keys0 = w.keys.clone()
+        self.judge, self.control = judge, control
+        self._judge_c = judge.c_struct() if judge is not None else None
+        self._control_c = control.c_struct() if control is not None else None
+        nb = len(w.bodies)
+        self._obs = torch.empty(w.B, nb, 6, dtype=torch.float32, device=w.device)
+        self.reward = torch.zeros(w.B, dtype=torch.float32, device=w.device)
+        self.done = torch.zeros(w.B, dtype=torch.int32, device=w.device)
 
     def reset(self):
         self.world.dyn.copy_(self.scenario.dyn_reset)
         self.world.keys.copy_(self._keys0)
         self.world.err.zero_()
         self.resets.zero_()
+        self.done.zero_()
+        self.reward.zero_()
         return self.observation()
 
     def step(self, n_steps=1, action=None, action_body=None, trace=None):
-        """n_steps fused driver steps; action f32 [n_steps, B, 2] is added to the
-        velocity of `action_body` (default: the last body, the RoboCup ball)
-        after Euler.  With autoreset an env whose error bits trip restarts from
-        its reset state and keeps receiving actions.  trace: see World.step."""
+        """n_steps fused driver steps in ONE launch; returns the observation
+        f32 [B, n_bodies, 6] (written by the step kernel itself), or with a
+        judge StepResult(obs, reward, done).  obs / reward / done are buffers
+        of this env that the next step overwrites (clone what you keep).
+
+        action: f32 [B, 2] held over the n_steps, or [n_steps, B, 2] per step
+        (no judge), added to the velocity of `action_body` (default: the last
+        body, the RoboCup ball) after Euler.  Without a judge, autoreset
+        restarts an env from its reset state after any step that sets its
+        error bits (cotix_step_autoreset).  trace: see World.step."""
         w = self.world
         body = len(w.bodies) - 1 if action_body is None else action_body
-        if self.autoreset:
-            w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body,
-                   dyn_reset=self.scenario.dyn_reset, resets=self.resets, trace=trace)
-        else:
-            w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body, trace=trace)
-        return self.observation()
+        if self.judge is None and (trace is not None or (action is not None and action.dim() == 3)):
+            if action is not None and action.dim() == 2:
+                action = action[None].expand(n_steps, -1, -1)
+            kw = dict(dyn_reset=self.scenario.dyn_reset, resets=self.resets) if self.autoreset else {}
+            w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body, trace=trace, **kw)
+            return self.observation()
+        if action is not None:
+            action = action.to(w.device, torch.float32).contiguous()
+        if self.judge is None:
+            w.eval_state(w.dyn, w.keys, w.err, 1, n_steps, self.dt, self.scenario.stages, action=action,
+                         action_body=body, control=self._control_c, reset_mode=1 if self.autoreset else 0,
+                         dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
+                         resets=self.resets if self.autoreset else None, obs=self._obs)
+            return self._obs
+        self.reward.zero_()
+        w.eval_state(w.dyn, w.keys, w.err, 1, n_steps, self.dt, self.scenario.stages, judge=self._judge_c,
+                     control=self._control_c, reward=self.reward, finished=self.done, action=action,
+                     action_body=body, reset_mode=2 if self.autoreset else 0,
+                     dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
+                     resets=self.resets if self.autoreset else None, obs=self._obs)
+        return StepResult(self._obs, self.reward, self.done)
 
     def observation(self, out=None):
         """f32 [B, n_bodies, 6] (px, py, vx, vy, angle, angular_velocity),

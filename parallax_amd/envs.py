@@ -81,6 +81,139 @@ class AbstractJudge:
         raise NotImplementedError
 
 
+def _f32(x):
+    return float(np.float32(x))
+
+
+class LinearJudge(AbstractJudge):
+    """A device AbstractJudge (include/cotix_amd.h cotix_judge): over the env's
+    state words s[k] (k = 6 * body + {px, py, vx, vy, angle, angular_velocity})
+
+      judge(s)      = sum_k rate_w[k] * s[k]
+      end_reward(s) = sum_k end_w[k] * s[k] (+ the reward of the first region holding s)
+      is_done(s)    = some region holds s, or (done_on_error and err bits set)
+
+    sums over the nonzero weights in k order, from the first term.
+    regions: [(body, lo[6], hi[6], reward)], strictly inside every bound
+    (NaN never inside, +-inf leaves a word free); at most 4, and at most 16
+    nonzero weights per sum.  The torch methods evaluate the same f32
+    expressions in the same order as the kernel, so the host loop and the
+    fused cotix_eval agree bit for bit."""
+
+    def __init__(self, rate_w=None, end_w=None, regions=(), done_on_error=False):
+        self.rate = sorted((int(k), _f32(w)) for k, w in dict(rate_w or {}).items() if _f32(w) != 0.0)
+        self.end = sorted((int(k), _f32(w)) for k, w in dict(end_w or {}).items() if _f32(w) != 0.0)
+        self.regions = [(int(b), [_f32(v) for v in lo], [_f32(v) for v in hi], _f32(r)) for b, lo, hi, r in regions]
+        self.done_on_error = bool(done_on_error)
+        if len(self.rate) > 16 or len(self.end) > 16 or len(self.regions) > _ffi.JUDGE_REGIONS:
+            raise ValueError("LinearJudge: at most 16 nonzero weights per sum and 4 regions")
+        if any(len(lo) != 6 or len(hi) != 6 for _, lo, hi, _ in self.regions):
+            raise ValueError("LinearJudge: region bounds are 6 words (one body's state)")
+
+    def c_struct(self):
+        j = _ffi.CotixJudge()
+        for k, w in self.rate:
+            j.rate_w[k] = w
+        for k, w in self.end:
+            j.end_w[k] = w
+        j.n_regions = len(self.regions)
+        for r, (b, lo, hi, rew) in enumerate(self.regions):
+            j.region_body[r] = b
+            for q in range(6):
+                j.region_lo[r][q] = lo[q]
+                j.region_hi[r][q] = hi[q]
+            j.region_reward[r] = rew
+        j.done_on_error = int(self.done_on_error)
+        return j
+
+    @staticmethod
+    def _word(state, k):
+        return state.dyn[k // 6, k % 6, :]
+
+    def _lin(self, state, terms):
+        acc = None
+        for k, w in terms:
+            t = self._word(state, k) * torch.tensor(w, dtype=torch.float32, device=state.dyn.device)
+            acc = t if acc is None else acc + t
+        return torch.zeros_like(state.dyn[0, 0, :]) if acc is None else acc
+
+    def _region(self, state):
+        """index of the first region holding the state, -1 for none ([B] int)."""
+        B = state.dyn.shape[2]
+        r_of = torch.full((B,), -1, dtype=torch.int64, device=state.dyn.device)
+        for r in reversed(range(len(self.regions))):
+            b, lo, hi, _ = self.regions[r]
+            inside = torch.ones(B, dtype=torch.bool, device=state.dyn.device)
+            for q in range(6):
+                v = state.dyn[b, q, :]
+                inside = inside & (torch.tensor(lo[q], dtype=torch.float32, device=v.device) < v) & \
+                    (v < torch.tensor(hi[q], dtype=torch.float32, device=v.device))
+            r_of = torch.where(inside, torch.full_like(r_of, r), r_of)
+        return r_of
+
+    def __call__(self, state, control_signal):
+        return self._lin(state, self.rate)
+
+    def is_done(self, state, control_signal):
+        d = self._region(state) >= 0
+        if self.done_on_error:
+            d = d | (state.err != 0)
+        return d
+
+    def end_reward(self, state, control_signal):
+        acc = self._lin(state, self.end)
+        r_of = self._region(state)
+        for r, (_, _, _, rew) in enumerate(self.regions):
+            rt = torch.tensor(rew, dtype=torch.float32, device=acc.device)
+            acc = torch.where(r_of == r, acc + rt if self.end else rt.expand_as(acc), acc)
+        return acc
+
+
+class AffineControl(AbstractControl):
+    """A device AbstractControl (include/cotix_amd.h cotix_control): the dense
+    signal is the velocity impulse dv[i] = sum_q gain[i][q] * (target[i][q] -
+    s[q]) (+ bias[i]) on `body`, from that body's state s before each
+    env-step (nonzero gains in q order from the first term, bias last when
+    nonzero).  Stateless."""
+
+    def __init__(self, body, gain=None, target=None, bias=(0.0, 0.0)):
+        self.body = int(body)
+        z = [[0.0] * 6, [0.0] * 6]
+        self.gain = [[_f32(v) for v in row] for row in (gain or z)]
+        self.target = [[_f32(v) for v in row] for row in (target or z)]
+        self.bias = [_f32(v) for v in bias]
+
+    def c_struct(self):
+        c = _ffi.CotixControl()
+        c.body = self.body
+        for i in range(2):
+            for q in range(6):
+                c.gain[i][q] = self.gain[i][q]
+                c.target[i][q] = self.target[i][q]
+            c.bias[i] = self.bias[i]
+        return c
+
+    def dv(self, state):
+        out = []
+        for i in range(2):
+            acc = None
+            for q in range(6):
+                g = self.gain[i][q]
+                if g != 0.0:
+                    v = state.dyn[self.body, q, :]
+                    tg = torch.tensor(self.target[i][q], dtype=torch.float32, device=v.device)
+                    t = torch.tensor(g, dtype=torch.float32, device=v.device) * (tg - v)
+                    acc = t if acc is None else acc + t
+            if self.bias[i] != 0.0:
+                bt = torch.tensor(self.bias[i], dtype=torch.float32, device=state.dyn.device)
+                acc = bt.expand(state.dyn.shape[2]).clone() if acc is None else acc + bt
+            out.append(torch.zeros_like(state.dyn[0, 0, :]) if acc is None else acc)
+        return torch.stack(out, 1).contiguous()
+
+    def __call__(self, state):
+        return (lambda s: VelocityImpulse(self.dv(s), self.body)), self
+
+
 class AbstractWorld:
     def forward(self, state, control_signal, dt):
         raise NotImplementedError
@@ -109,13 +242,23 @@ class AbstractEnvironment:
     def __init__(self, world, state, control, judge):
         self.world, self.state, self.control, self.judge = world, state, control, judge
 
-    def eval(self, eval_period, num_NFEs, WFE_scale=10):
+    def fused(self):
+        """True when eval runs as ONE cotix_eval launch: a PhysicsWorld with a
+        device judge (LinearJudge) and a device control (AffineControl or None)."""
+        return (isinstance(self.world, PhysicsWorld) and isinstance(self.judge, LinearJudge)
+                and (self.control is None or isinstance(self.control, AffineControl)))
+
+    def eval(self, eval_period, num_NFEs, WFE_scale=10, fused=None):
         """-> (new environment with the end state, reward [B]); the reference's
-        cotix/_envs.py:37-132, per env."""
+        cotix/_envs.py:37-132, per env.  With a device judge and control
+        (fused(), or fused=True) the whole NFE x WFE loop is one kernel launch
+        (cotix_eval); otherwise the loop runs here, one launch per env-step."""
         B = self.state.err.shape[0]
         dev = self.state.err.device
         tpn = float(np.float32(eval_period / num_NFEs))  # the carry's f32 time_per_NFE
         dt = float(np.float32(np.float32(tpn) / np.float32(float(WFE_scale))))
+        if self.fused() if fused is None else fused:
+            return self._eval_fused(num_NFEs, WFE_scale, dt)
         state, control = self.state, self.control
         reward = torch.zeros(B, dtype=torch.float32, device=dev)
         finished = torch.zeros(B, dtype=torch.bool, device=dev)
@@ -142,3 +285,14 @@ class AbstractEnvironment:
             finished = already
         out = AbstractEnvironment(self.world, state, self.control, self.judge)
         return out, reward
+
+    def _eval_fused(self, num_NFEs, WFE_scale, dt):
+        w = self.world.world
+        st = self.state.clone()
+        B = st.err.shape[0]
+        reward = torch.zeros(B, dtype=torch.float32, device=st.dyn.device)
+        finished = torch.zeros(B, dtype=torch.int32, device=st.dyn.device)
+        j = self.judge.c_struct()
+        c = self.control.c_struct() if self.control is not None else None
+        w.eval_state(st.dyn, st.keys, st.err, num_NFEs, WFE_scale, dt, self.world.stages, j, c, reward, finished)
+        return AbstractEnvironment(self.world, st, self.control, self.judge), reward

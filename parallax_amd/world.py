@@ -187,6 +187,29 @@ class World:
             self.B, int(n_steps), float(dt), int(self._stages(stages)), _ffi.ptr(action), int(action_body),
             _ffi.stream_ptr(self.device)), "cotix_step")
 
+    def eval_state(self, dyn, keys, err, n_nfe, wfe, dt, stages, judge=None, control=None, reward=None,
+                   finished=None, action=None, action_body=0, reset_mode=0, dyn_reset=None, resets=None, obs=None):
+        """cotix_eval on caller-owned state tensors (same layouts as self.dyn /
+        self.keys / self.err): AbstractEnvironment.eval's NFE x WFE loop in one
+        launch.  judge / control: ctypes cotix_judge / cotix_control (or None);
+        action f32 [B, 2] held over the env-steps; reward f32 [B] and finished
+        i32 [B] in/out; obs f32 [B, n_bodies, 6] out (nullable)."""
+        for t, shape in ((dyn, tuple(self.dyn.shape)), (keys, (self.B, 2)), (err, (self.B,))):
+            if tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.dyn.device:
+                raise ValueError("state tensor shape/device/layout mismatch")
+        for t, shape in ((reward, (self.B,)), (finished, (self.B,)), (action, (self.B, 2)),
+                         (dyn_reset, tuple(self.dyn.shape)), (resets, (self.B,)),
+                         (obs, (self.B, len(self.bodies), 6))):
+            if t is not None and (tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.dyn.device):
+                raise ValueError("eval tensor shape/device/layout mismatch")
+        import ctypes
+        _ffi.check(_ffi.lib.cotix_eval(
+            self.scene.handle, _ffi.ptr(dyn), _ffi.ptr(keys), _ffi.ptr(err), _ffi.ptr(self.geom), self.geom_stride,
+            self.B, int(n_nfe), int(wfe), float(dt), int(self._stages(stages)),
+            None if judge is None else ctypes.byref(judge), None if control is None else ctypes.byref(control),
+            _ffi.ptr(action), int(action_body), _ffi.ptr(reward), _ffi.ptr(finished), int(reset_mode),
+            _ffi.ptr(dyn_reset), _ffi.ptr(resets), _ffi.ptr(obs), _ffi.stream_ptr(self.device)), "cotix_eval")
+
     # -- body-level operators (UniversalShape, cotix/_universal_shape.py:87-132) --
     def penetrates_with(self, i, j):
         """(collides bool [B], penetration f32 [B, 2]) of body i against body j:

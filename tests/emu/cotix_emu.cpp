@@ -105,6 +105,7 @@ int emu_step(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float
   a.action = action;
   a.action_body = action_body;
   a.dyn_reset = dyn_reset;
+  a.reset_mode = dyn_reset ? 1 : 0;
   a.resets = resets;
   run_any(a, E, 0);
   return 0;
@@ -128,9 +129,47 @@ int emu_step_ex(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const fl
   a.action = action;
   a.action_body = action_body;
   a.dyn_reset = dyn_reset;
+  a.reset_mode = dyn_reset ? 1 : 0;
   a.resets = resets;
   a.trace_chosen = chosen;
   a.trace_cells = cells;
+  run_any(a, E, 0);
+  return 0;
+}
+
+// cotix_eval on the host (same argument checks as the library's entry point)
+int emu_eval(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B, int n_nfe,
+             int wfe, float dt, int stages, const cotix_judge* judge, const cotix_control* control,
+             const float* action, int action_body, float* reward, uint32_t* finished, int reset_mode,
+             const float* dyn_reset, uint32_t* resets, float* obs, int E) {
+  EmuScene* s = static_cast<EmuScene*>(scene);
+  if (reset_mode == 1 && judge) return g_err = "reset_mode 1 with a judge", -1;
+  if (reset_mode != 0 && !dyn_reset) return g_err = "reset_mode needs dyn_reset", -1;
+  if (judge && (!reward || !finished)) return g_err = "a judge needs reward and finished", -1;
+  if (B == 0 || n_nfe == 0 || wfe == 0) return 0;
+  cxk::KArgs a{};
+  const int nb = s->s.nb;
+  if (cxk::pack_judge(judge, nb * 6, nb, a.judge, g_err) || cxk::pack_control(control, nb, a.ctl, g_err)) return -1;
+  a.sc = &s->s;
+  a.dyn = dyn;
+  a.keys = keys;
+  a.err = err;
+  a.geom = geom;
+  a.gstride = gstride;
+  a.B = B;
+  a.n_steps = n_nfe * wfe;
+  a.nfe_len = wfe;
+  a.dt = dt;
+  a.stages = stages;
+  a.action = action;
+  a.action_held = 1;
+  a.action_body = action_body;
+  a.reward = reward;
+  a.finished = finished;
+  a.reset_mode = reset_mode;
+  a.dyn_reset = dyn_reset;
+  a.resets = resets;
+  a.obs = obs;
   run_any(a, E, 0);
   return 0;
 }

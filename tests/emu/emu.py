@@ -29,6 +29,9 @@ def load(asan=False):
                                 ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, ctypes.c_int]
     lib.emu_rollout_backward.argtypes = [P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                          ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.c_int]
+    lib.emu_eval.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                             ctypes.c_float, ctypes.c_int, P_, P_, P_, ctypes.c_int, P_, P_, ctypes.c_int, P_, P_, P_,
+                             ctypes.c_int]
     lib.emu_last_error.restype = ctypes.c_char_p
     return lib
 
@@ -113,3 +116,15 @@ def rollout_backward(lib, h, sd, sk, geom, gstride, stages, actions, action_body
     if rc:
         raise RuntimeError(lib.emu_last_error().decode())
     return ga, gd
+
+
+def eval_(lib, h, dyn, keys, err, geom, gstride, n_nfe, wfe, dt, stages, judge=None, control=None, action=None,
+          action_body=0, reward=None, finished=None, reset_mode=0, dyn_reset=None, resets=None, obs=None, E=4):
+    """cotix_eval on the host (numpy arrays updated in place; judge / control
+    are ctypes cotix_judge / cotix_control structs or None)."""
+    ref = lambda s: None if s is None else ctypes.cast(ctypes.pointer(s), P_)  # noqa: E731
+    rc = lib.emu_eval(h, _p(dyn), _p(keys), _p(err), _p(geom), gstride, dyn.shape[2], n_nfe, wfe, dt, stages,
+                      ref(judge), ref(control), _p(action), action_body, _p(reward), _p(finished), reset_mode,
+                      _p(dyn_reset), _p(resets), _p(obs), E)
+    if rc:
+        raise RuntimeError(lib.emu_last_error().decode())

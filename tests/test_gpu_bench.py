@@ -33,7 +33,7 @@ def test_bench_rccl_path_single_rank(tmp_path):
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
-    assert line["config"]["obs_all_gather_check"] == "ok"
+    assert line["config"]["obs_all_gather_check"].startswith("ok")
     assert line["n_gpus"] == 1 and line["value"] > 0
     d = np.load(dump)
     # the gathered tensor == cotix_observe of the local state == the SoA state transposed

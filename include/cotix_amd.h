@@ -79,11 +79,13 @@ enum {
   COTIX_STAGE_ADVANCE_KEY = 16, /* key = split(key)[0]                        */
   /* broadphase of the collider's polygon contacts (opt-in, results unchanged):
    * a polygon x polygon / AABB x polygon pair whose world AABBs are separated
-   * by more than 2^-8 * S + 2^-16 (S = the pair's largest |coordinate|)
-   * skips GJK, EPA and the contact points -- such a pair's reference contact
-   * point is NaN.  The caller certifies that every polygon's interior angles
-   * are >= 0.5 degrees (the condition of the argument);
-   * parallax_amd.World checks its geometry and sets the bit itself. */
+   * by more than 2^-8 * S + 2^-16 (S = the pair's largest |coordinate|) and
+   * whose world shapes pass the argument's shape conditions (strictly convex,
+   * no sharp vertex with sin(angle) < 2^-7, no edge of one within 2^-9 of
+   * parallel to an edge of the other; checked by the kernel per pair) skips
+   * GJK, EPA and the contact points: every term of _contact_from_edges is
+   * then provably NaN / false, so the reference's contact is NaN
+   * ("Broadphase exactness"). */
   COTIX_STAGE_BROADPHASE = 32,
   COTIX_STAGES_ROBOCUP = 1 | 4 | 16,
   COTIX_STAGES_LUNAR = 1 | 2 | 4 | 8 | 16

@@ -41,6 +41,7 @@ constexpr int WAVE = 64;
 struct Stats {
   unsigned long long wave_steps, active_items, rounds, resolutions, f_items, b_items, draws, valid_draws, r1_left, lvl_env, lvl_wave, e1_slots;
   unsigned long long valid_cands, fit64;  // valid candidates of the active items; wave-steps where they fit 64 lanes
+  unsigned long long bp_cand, bp_guard_fail;  // broadphase: pairs past the gap test; of them, not certified by bp_guard
 };
 inline Stats g_stats{};
 #define CXK_STAT(f, v) (cxk::g_stats.f += (unsigned long long)(v))
@@ -1058,12 +1059,92 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
 // exactness argument is in DESIGN.md section 3).  BP0: a polygon pair
 // (polygon x polygon, AABB x polygon) whose world AABBs are separated by
 // more than the margin 2^-8 * S + 2^-16 (S = the largest coordinate
-// magnitude of the two shapes) gets the no-contact result without GJK, EPA
-// or contact points -- _contact_from_edges (cotix/_contacts.py:205-267)
-// cannot find a contained vertex or an edge intersection across that gap,
-// so the reference's contact point is NaN and the candidate never writes.
-// Every other item is flagged for the B list (BP1) that BP2 runs at full
-// lane width.
+// magnitude of the two shapes) and whose world shapes pass bp_guard gets the
+// no-contact result without GJK, EPA or contact points -- then no vertex is
+// contained and no edge pair intersects in _contact_from_edges
+// (cotix/_contacts.py:205-267), with the rounding of f32 included, so the
+// reference's contact point is NaN and the candidate never writes.  Every
+// other item is flagged for the B list (BP1) that BP2 runs at full lane width.
+// The conditions of the broadphase exactness argument (DESIGN.md section 3,
+// "Broadphase exactness") that the gap test alone does not give, checked on
+// the pair's WORLD shapes (the f32 vertices the reference works on):
+//  (P) every polygon is strictly convex in its stored order, and no sharp
+//      vertex (dot(d_k, d_k+1) < 0, interior angle < 90 deg) has
+//      |cross(d_k, d_k+1)| < 2^-7 |d_k|_1 |d_k+1|_1  (sin(angle) >= 2^-7);
+//  (E) no edge of A is within |cross| <= 2^-9 |.|_1 |.|_1 of parallel to an
+//      edge of B (AABB edges: the axes).
+// Edge 1-norms lie in [2^-40, 2^40] (no under/overflow in the products).
+// With the gap > 2^-8 S + 2^-16 of BP0 these make every term of
+// _contact_from_edges (cotix/_contacts.py:205-267) NaN / false -- the contact
+// is NaN whatever GJK returns.  False when it cannot certify (full path).
+CX_DEV bool bp_edges(const cx::Shape& P, float* dx, float* dy, float* l1, int* n) {
+  using namespace cx;
+  if (P.kind != KIND_POLY) {  // AABB: the axes, exactly (get_edges, cotix/_convex_shapes.py:82-93)
+    dx[0] = 1.0f; dy[0] = 0.0f; l1[0] = 1.0f;
+    dx[1] = 0.0f; dy[1] = 1.0f; l1[1] = 1.0f;
+    *n = 2;
+    return true;
+  }
+  bool ok = P.n >= 3;
+  int m = 0;
+  float px = P.w[2 * (P.n - 1)], py = P.w[2 * (P.n - 1) + 1];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    if (k < P.n) {
+      const float x = P.w[2 * k], y = P.w[2 * k + 1];
+      dx[k] = x - px;
+      dy[k] = y - py;
+      l1[k] = __builtin_fabsf(dx[k]) + __builtin_fabsf(dy[k]);
+      ok = ok & (l1[k] >= 9.094947017729282e-13f) & (l1[k] <= 1.099511627776e12f);  // [2^-40, 2^40], false for NaN
+      px = x;
+      py = y;
+      m = k + 1;
+    }
+  }
+  *n = m;
+  if (!ok) return false;
+  // (P): consecutive edges d_k = v_k - v_k-1, d_k+1; one turning sign, sharp vertices not too sharp
+  bool pos = true, neg = true;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    if (k < m) {
+      const int j = k + 1 < m ? k + 1 : 0;
+      const float cr = dx[k] * dy[j] - dy[k] * dx[j];
+      const float dt = dx[k] * dx[j] + dy[k] * dy[j];
+      pos = pos & (cr > 0.0f);
+      neg = neg & (cr < 0.0f);
+      ok = ok & ((dt >= 0.0f) | (__builtin_fabsf(cr) >= 0.0078125f * (l1[k] * l1[j])));
+    }
+  }
+  return ok & (pos | neg);
+}
+CX_DEV bool bp_guard(const cx::Shape& A, const cx::Shape& B) {
+  using namespace cx;
+  float ax[MAXV], ay[MAXV], al[MAXV], bx[MAXV], by[MAXV], bl[MAXV];
+  int na = 0, nb = 0;
+  bool ok = bp_edges(A, ax, ay, al, &na);
+  ok = ok & bp_edges(B, bx, by, bl, &nb);
+  if (!ok) return false;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    if (i >= na) break;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      if (j >= nb) break;
+      ok = ok & (__builtin_fabsf(ax[i] * by[j] - ay[i] * bx[j]) > 0.001953125f * (al[i] * bl[j]));
+    }
+  }
+  return ok;
+}
+
+// mutation knobs for the tests only (tests/test_broadphase_cpu.py builds the
+// host emulation with them); the library is always built with the defaults
+#ifndef COTIX_BP_MARGIN_MUL
+#define COTIX_BP_MARGIN_MUL 1.0f
+#endif
+#ifndef COTIX_BP_GUARD
+#define COTIX_BP_GUARD 1
+#endif
 template <int EW>
 CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
@@ -1109,10 +1190,28 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
           float S = 0.0f;
 #pragma unroll
           for (int k = 0; k < 4; ++k) S = cx::fmax_(S, cx::fmax_(__builtin_fabsf(A[q][k]), __builtin_fabsf(B[q][k])));
-          const float margin = S * 0.00390625f + 1.52587890625e-05f;  // 2^-8 S + 2^-16
+          const float margin = (S * 0.00390625f + 1.52587890625e-05f) * COTIX_BP_MARGIN_MUL;  // 2^-8 S + 2^-16
           const float gap = cx::fmax_(cx::fmax_(B[q][0] - A[q][2], A[q][0] - B[q][2]),
                                       cx::fmax_(B[q][1] - A[q][3], A[q][1] - B[q][3]));
-          if (poly[q] && gap > margin) {  // false for NaN
+          bool skip = poly[q] && gap > margin;  // false for NaN
+          if (skip) {  // the argument's shape conditions, on the world shapes
+            const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci];
+            const int wa = c.L.world + (int)(d0w & 1023u), wb = c.L.world + (int)((d0w >> 10) & 1023u);
+            Shape SA, SB;
+            SA.kind = (int)((d0w >> 23) & 3u);
+            SB.kind = (int)((d0w >> 25) & 3u);
+            SA.n = (int)(d1[q] & 255u);
+            SB.n = (int)((d1[q] >> 8) & 255u);
+#pragma unroll
+            for (int k = 0; k < 2 * MAXV; ++k) {
+              SA.w[k] = t.f(wa + k, e);
+              SB.w[k] = t.f(wb + k, e);
+            }
+            skip = COTIX_BP_GUARD ? bp_guard(SA, SB) : true;
+            CXK_STAT(bp_cand, 1);
+            CXK_STAT(bp_guard_fail, skip ? 0 : 1);
+          }
+          if (skip) {
             keep = 0u;
             const int co = c.L.con + 4 * ci;
             t.f(co + 0, e) = 0.0f;

@@ -262,8 +262,8 @@ class LunarLander:
                              else jr.split(jr.PRNGKey(1, device), batch))
         self.world = World(self.bodies, batch, device, collider_keys)
         self.dyn_reset = self.world.dyn.clone()
-        # the polygon broadphase (results unchanged) when the terrain meets its condition
-        self.stages = _ffi.STAGES_LUNAR | (_ffi.STAGE_BROADPHASE if self.world.broadphase_ok() else 0)
+        # the polygon broadphase (results unchanged: the kernel certifies every pair it skips)
+        self.stages = _ffi.STAGES_LUNAR | _ffi.STAGE_BROADPHASE
 
     def step(self):
         """LunarLander.step(): the joint constraints (cotix/_lunar_lander.py:145-218)."""

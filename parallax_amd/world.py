@@ -110,10 +110,10 @@ class World:
         return amin
 
     def broadphase_ok(self):
-        """The condition COTIX_STAGE_BROADPHASE asks its caller to certify:
-        every polygon interior angle >= 0.5 degrees (include/cotix_amd.h).
-        Cached per geometry tensor and its in-place version counter, so an
-        edit of world.geom (in place or by replacement) is re-checked."""
+        """Informational: every polygon interior angle of the uploaded local
+        geometry >= 0.5 degrees.  COTIX_STAGE_BROADPHASE no longer depends on
+        it: the kernel checks the conditions of its exactness argument on the
+        world shapes of every pair it skips."""
         key = (id(self.geom), self.geom._version)
         if getattr(self, "_bp_key", None) != key:
             self._bp_ok = self.polygon_min_angle() >= 0.5
@@ -121,10 +121,6 @@ class World:
         return self._bp_ok
 
     def _stages(self, stages):
-        """The broadphase bit survives only while the geometry still meets
-        its condition (the bit never changes results, only skips work)."""
-        if stages & _ffi.STAGE_BROADPHASE and not self.broadphase_ok():
-            return stages & ~_ffi.STAGE_BROADPHASE
         return stages
 
     # -- state access -----------------------------------------------------

@@ -319,8 +319,10 @@ extern "C" int emu_stats(unsigned long long* out) {
   out[11] = cxk::g_stats.e1_slots;
   out[12] = cxk::g_stats.valid_cands;
   out[13] = cxk::g_stats.fit64;
+  out[14] = cxk::g_stats.bp_cand;
+  out[15] = cxk::g_stats.bp_guard_fail;
   cxk::g_stats = cxk::Stats{};
-  return 12;
+  return 16;
 }
 #endif
 

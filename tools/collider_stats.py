@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--ew", type=int, default=4)
     ap.add_argument("--broadphase", action="store_true", help="COTIX_STAGE_BROADPHASE (polygon scenes)")
+    ap.add_argument("--drop", type=float, default=0.0, help="lunar: lower the lander and legs by this much (contact)")
     a = ap.parse_args()
     src = os.path.join(ROOT, "tests", "emu", "cotix_emu.cpp")
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
@@ -52,7 +53,10 @@ def main():
             bodies = P.lunar_lander_bodies(tk[e])
             h, g = emu.oracle_scene(lib, bodies)
             rows.append(g)
-            dyns.append([b.dyn() for b in bodies])
+            d = [b.dyn() for b in bodies]
+            for b in range(3):
+                d[b][1] -= a.drop
+            dyns.append(d)
         geom = np.ascontiguousarray(np.stack(rows).astype(np.float32))
         gstride = geom.shape[1]
         dyn = np.ascontiguousarray(np.array(dyns, np.float32).transpose(1, 2, 0))
@@ -72,7 +76,8 @@ def main():
            "items_left_after_round1_per_wave_step": out[8] / ws,
            "resolution_levels_per_env_step": out[9] / (B * a.steps), "resolution_levels_per_wave_step": out[10] / ws,
            "sequential_slots_per_wave_step": out[11] / ws,
-           "valid_candidates_of_active_items_per_wave_step": out[12] / ws, "fit64_frac": out[13] / ws})
+           "valid_candidates_of_active_items_per_wave_step": out[12] / ws, "fit64_frac": out[13] / ws,
+           "bp_candidates_per_wave_step": out[14] / ws, "bp_guard_fail_frac": out[15] / max(out[14], 1)})
 
 
 if __name__ == "__main__":

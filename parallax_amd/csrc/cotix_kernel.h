@@ -1068,7 +1068,8 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
 // The conditions of the broadphase exactness argument (DESIGN.md section 3,
 // "Broadphase exactness") that the gap test alone does not give, checked on
 // the pair's WORLD shapes (the f32 vertices the reference works on):
-//  (P) every polygon is strictly convex in its stored order, and no sharp
+//  (P) every polygon is strictly convex in its stored order (every turn's
+//      |cross| > 2^-21 |d_k|_1 |d_k+1|_1, so the computed signs are exact), no sharp
 //      vertex (dot(d_k, d_k+1) < 0, interior angle < 90 deg) has
 //      |cross(d_k, d_k+1)| < 2^-7 |d_k|_1 |d_k+1|_1  (sin(angle) >= 2^-7);
 //  (E) no edge of A is within |cross| <= 2^-9 |.|_1 |.|_1 of parallel to an
@@ -1111,9 +1112,11 @@ CX_DEV bool bp_edges(const cx::Shape& P, float* dx, float* dy, float* l1, int* n
       const int j = k + 1 < m ? k + 1 : 0;
       const float cr = dx[k] * dy[j] - dy[k] * dx[j];
       const float dt = dx[k] * dx[j] + dy[k] * dy[j];
-      pos = pos & (cr > 0.0f);
-      neg = neg & (cr < 0.0f);
-      ok = ok & ((dt >= 0.0f) | (__builtin_fabsf(cr) >= 0.0078125f * (l1[k] * l1[j])));
+      const float ll = l1[k] * l1[j];
+      // the turn's sign beyond the cross product's rounding (2^-21 > 4u): strictly convex exactly
+      pos = pos & (cr > 4.76837158203125e-07f * ll);
+      neg = neg & (cr < -4.76837158203125e-07f * ll);
+      ok = ok & ((dt >= 0.0f) | (__builtin_fabsf(cr) >= 0.0078125f * ll));
     }
   }
   return ok & (pos | neg);

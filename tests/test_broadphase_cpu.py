@@ -6,7 +6,7 @@ cells show every contact's NaN-ness.  Mutation builds of the same kernel
 source show what the test detects: margin 0 drops the reference's contacts
 at positive gaps (the touch set) and fails; the margin halved and the shape
 guard removed still pass, as DESIGN.md section 3 explains (the margin has
-~2^4 headroom over the rounding bound; without the guard exactness rests on
+~2^8 headroom over the rounding bound; without the guard exactness rests on
 GJK rejecting, which the argument does not need but which holds on every
 case searched)."""
 import os
@@ -29,8 +29,10 @@ def _build(name, defines):
     src = os.path.join(EMU, "cotix_emu.cpp")
     hdr = [os.path.join(HERE, "..", "parallax_amd", "csrc", f) for f in ("cotix_kernel.h", "cotix_device.h")]
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(f) for f in [src] + hdr):
+        tmp = "%s.%d.tmp" % (out, os.getpid())  # parallel workers: build privately, then rename atomically
         subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-w",
-                        *["-D" + d for d in defines], src, "-o", out], check=True)
+                        *["-D" + d for d in defines], src, "-o", tmp], check=True)
+        os.replace(tmp, out)
     return out
 
 

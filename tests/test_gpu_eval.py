@@ -113,7 +113,7 @@ def test_fused_eval_4096_envs_vs_emulation(torch_cuda):
     assert same(out.state.dyn.cpu().numpy(), dyn)
     assert np.array_equal(out.state.keys.cpu().numpy().view(np.uint32), keys)
     assert same(reward.cpu().numpy(), rw)
-    assert 100 < fin.sum() < 4096
+    assert fin.sum() > 100  # RoboCup's error trip ends most episodes (done_on_error)
 
 
 def test_batched_env_rl_loop_vs_emulation(torch_cuda):

@@ -86,6 +86,7 @@ struct SceneHdr {
   uint16_t nvt;      // polygon vertices over all parts (phase T's vertex items)
   uint16_t o_vit;    // per polygon vertex 2 words (cotix_scene.h): part, vertex, count, first item, body | offsets
   uint32_t rcp_mask; // bit b: body b's mass and inertia have exact reciprocals (bodies < 32)
+  uint16_t maxv;     // the most vertices of any polygon part (0: none) -- bounds the broadphase guard's loops
 };
 struct SceneDev : SceneHdr {
   uint32_t hot[MAXHOT];
@@ -100,16 +101,16 @@ struct SceneDev : SceneHdr {
 // for cotix/_robocup.py and cotix/_lunar_lander.py; spec_of() admits a scene
 // only when all of them match.
 struct SceneDims {
-  int nb, np, nc, nl, nt, G, W, nmw, poly, rcp_all, rcp_mask, nvt;
+  int nb, np, nc, nl, nt, G, W, nmw, poly, rcp_all, rcp_mask, nvt, maxv;
 };
 enum : int { SPEC_GENERIC = 0, SPEC_ROBOCUP = 1, SPEC_LUNAR = 2 };
-constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-                                    {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31, 0},
-                                    {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14, 42}};
+constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+                                    {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31, 0, 0},
+                                    {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14, 42, 6}};
 CX_HD bool dims_match(const SceneHdr& h, const SceneDims& d) {
   return h.nb == d.nb && h.np == d.np && h.nc == d.nc && h.nl == d.nl && h.nt == d.nt && h.G == d.G && h.W == d.W &&
          h.nmw == d.nmw && h.poly == d.poly && h.rcp_all == d.rcp_all && (int)h.rcp_mask == d.rcp_mask &&
-         h.nvt == d.nvt;
+         h.nvt == d.nvt && h.maxv == d.maxv;
 }
 CX_HD int spec_of(const SceneHdr& h) {
   if (dims_match(h, SPEC_DIMS[SPEC_ROBOCUP])) return SPEC_ROBOCUP;
@@ -134,6 +135,7 @@ CX_HD SceneHdr spec_hdr(SceneHdr h) {
     h.rcp_all = d.rcp_all;
     h.rcp_mask = d.rcp_mask;
     h.nvt = d.nvt;
+    h.maxv = d.maxv;
   }
   return h;
 }
@@ -197,7 +199,7 @@ struct KArgs {
 // per-wave tile layout (words, each x EW envs)
 struct Lay {
   int dyn, world, con, m, ch, key, sk0, skt, err, nres, ret, adj, rec, vm, rst, geo, rp, kw, kww, rflag, pose, pcv, pbox,
-      jfin, jal, jr, jpr, jk, je, jsn, S;
+      pedge, jfin, jal, jr, jpr, jk, je, jsn, S;
 };
 // key window: the per-step keys of KWIN consecutive steps, precomputed
 // together (phase K) -- the collider keys depend on the key chain only, never
@@ -208,7 +210,8 @@ constexpr int REC_W = 7;  // per resolution: applied flag, v/w of body i, v/w of
 enum : int { RP_J, RP_NX, RP_NY, RP_R1X, RP_R1Y, RP_R2X, RP_R2Y, RP_PX, RP_PY, RP_DEN, RP_PT, RP_NE, RP_MU, RP_MJ, RP_IJ,
              RP_QMJ, RP_QIJ, RP_W };
 constexpr uint32_t RP_NONE = 0xFFFFFFFFu;
-CX_HD Lay layout(int nb, int np, int W, int nc, int nt, int G) {
+// PE: words of the broadphase guard's per-edge pseudo-angles (polygon scenes: W / 2, else 0)
+CX_HD Lay layout(int nb, int np, int W, int nc, int nt, int G, int PE) {
   Lay L;
   L.dyn = 0;
   L.world = L.dyn + nb * 6;
@@ -236,7 +239,15 @@ CX_HD Lay layout(int nb, int np, int W, int nc, int nt, int G) {
   // cotix_eval's carry (judge on): finished, already_premature_outted, reward,
   // the premature-out reward, key and err; the premature-out state itself is
   // kept in rst (free in eval: its restarts are taken at entry, reset_mode 2)
-  L.jfin = L.pbox + 4 * np;
+  // per world vertex (word offset / 2 of the world parts): the broadphase
+  // guard's edge pseudo-angle (ph_TV4).  It overlays adj and rec, which only
+  // the backward re-play uses, and the backward program is admitted for
+  // analytic (polygon-free) scenes only (cotix_rollout_backward): the
+  // LunarLander tile stays within the LDS
+  // (a scene with more polygon vertices gets words of its own)
+  const bool own = PE > nb * (6 + REC_W);
+  L.pedge = own ? L.pbox + 4 * np : L.adj;
+  L.jfin = L.pbox + 4 * np + (own ? PE : 0);
   L.jal = L.jfin + 1;
   L.jr = L.jal + 1;
   L.jpr = L.jr + 1;
@@ -246,7 +257,9 @@ CX_HD Lay layout(int nb, int np, int W, int nc, int nt, int G) {
   L.S = L.jsn + 1;
   return L;
 }
-static inline int tile_words(const SceneHdr& s) { return layout(s.nb, s.np, s.W, s.nc, s.nt, s.G).S; }
+static inline int tile_words(const SceneHdr& s) {
+  return layout(s.nb, s.np, s.W, s.nc, s.nt, s.G, s.poly ? s.W / 2 : 0).S;
+}
 // per-wave scratch of phase C (words, not per env): pass flags, keep flags,
 // active count, two item lists (double buffer), per-item scan positions
 enum : int { WS_FLAG = 0, WS_KEEP = 64, WS_KEEP2 = 128, WS_N = 192, WS_LIST = 193 };
@@ -342,10 +355,11 @@ CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, con
 enum : int { FNS_ANALYTIC = 1, FNS_CONVEX = 2, FNS_CIRCLE_POLY = 4, FNS_AABB_POLY = 8 };
 // the FNSET instantiation of the step kernel for a scene's function set
 // (launcher and host emulation): mode 2 (backward) and analytic scenes get the
-// analytic program, mode 1 (rollout) the full one
+// analytic program, modes 1 (rollout) and 3 (eval with a judge or control) the
+// full one
 CX_HD int launch_fnset(int fs, int mode) {
   if (mode == 2 || (fs & ~FNS_ANALYTIC) == 0) return FNS_ANALYTIC;
-  if (mode == 1) return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
+  if (mode == 1 || mode == 3) return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
   if ((fs & ~(FNS_ANALYTIC | FNS_CONVEX)) == 0) return FNS_ANALYTIC | FNS_CONVEX;
   if ((fs & FNS_CIRCLE_POLY) == 0) return FNS_ANALYTIC | FNS_CONVEX | FNS_AABB_POLY;
   return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
@@ -464,7 +478,7 @@ struct Ctx {
 };
 template <int EW>
 CX_HD Ctx make_ctx(const SceneHdr& h) {
-  return Ctx{h.nb, h.np, h.nc, h.nl, h.nt, h, layout(h.nb, h.np, h.W, h.nc, h.nt, h.G),
+  return Ctx{h.nb, h.np, h.nc, h.nl, h.nt, h, layout(h.nb, h.np, h.W, h.nc, h.nt, h.G, h.poly ? h.W / 2 : 0),
              ws_layout(h.nl, h.nc, EW, h.poly, h.nvt)};
 }
 
@@ -479,7 +493,7 @@ CX_DEV void ph_geo(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
   }
 }
 
-template <int EW>
+template <int EW, bool EVAL = false>
 CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   if (c.sh.poly)  // phase F's flag array incl. its padding to a multiple of 64
     for (int w = lane; w < c.W.cf_list - c.W.cf_flag; w += WAVE) t.ws[c.W.cf_flag + w] = 0u;
@@ -505,7 +519,7 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
     t.w(c.L.err, e) = (g < a.B && !rs) ? a.err[g] : 0u;
     t.w(c.L.nres, e) = rs ? 1u : 0u;
     t.w(c.L.pcv, e) = 0u;  // no world part built yet in this launch (phase T)
-    if (a.judge.on) {
+    if (EVAL && a.judge.on) {
       t.w(c.L.jfin, e) = (g < a.B && !rs && a.finished != nullptr) ? (a.finished[g] != 0u ? 1u : 0u) : 0u;
       t.f(c.L.jr, e) = (g < a.B && a.reward != nullptr) ? a.reward[g] : 0.0f;
     }
@@ -588,10 +602,12 @@ CX_DEV cx::v2 control_dv(const KArgs& a, Tile<EW> t, int o, int e) {
   return cx::v2{dv[0], dv[1]};
 }
 
-template <int EW>
+// EVAL: the cotix_eval program (device judge / control); the step programs
+// are compiled without them
+template <int EW, bool EVAL = false>
 CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int b, int step) {
   const int o = c.L.dyn + b * 6;
-  const bool ctl = a.ctl.on && b == a.ctl.body;
+  const bool ctl = EVAL && a.ctl.on && b == a.ctl.body;
   const cx::v2 dv = ctl ? control_dv<EW>(a, t, o, e) : cx::v2{0.0f, 0.0f};
   if (!(a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))) return;  // (ph_A calls only with either)
   if (a.stages & COTIX_STAGE_EULER) {
@@ -624,7 +640,7 @@ CX_DEV void reset_scratch(const Ctx& c, Tile<EW> t, int lane) {
   for (int w = lane; w < c.sh.nmw * EW; w += WAVE) t.u[c.L.vm * EW + w] = 0u;
 }
 
-template <int EW, bool PRE = false>
+template <int EW, bool PRE = false, bool EVAL = false>
 CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step, int slot = 0) {
   using namespace cx;
   const int nb = c.nb;
@@ -632,7 +648,7 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
     for (int w = lane; w < nb * EW; w += WAVE) {
       const int e = w % EW, b = w / EW;
-      if (env0 + e < a.B) euler_item<EW>(a, c, t, env0, e, b, step);
+      if (env0 + e < a.B) euler_item<EW, EVAL>(a, c, t, env0, e, b, step);
     }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
     for (int e = lane; e < EW; e += WAVE) {
@@ -691,6 +707,14 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       t.f(bo + 1, e) = circ ? w2 - w0 : w1;
       t.f(bo + 2, e) = circ ? w1 + w0 : w2;
       t.f(bo + 3, e) = circ ? w2 + w0 : w3;
+      if (sc.poly) {
+        // the broadphase guard's edge pseudo-angles of an AABB: the axes
+        // (get_edges, cotix/_convex_shapes.py:82-93), exactly 0 and 1 (ph_TV4);
+        // unused for a circle
+        const int po = c.L.pedge + t.ti(sc.o_pwoff + p) / 2;
+        t.f(po, e) = 0.0f;
+        t.f(po + 1, e) = 1.0f;
+      }
     }
   }
 }
@@ -873,6 +897,53 @@ CX_DEV void ph_TV3(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
     const int wo = L.world + (int)(d1 >> 16) + 2 * r;
     t.f(wo, e) = vtf<EW>(c, t, v, 0, e);
     t.f(wo + 1, e) = vtf<EW>(c, t, v, 1, e);
+  }
+}
+// TV4 (broadphase scenes; item = (world vertex slot k of a rebuilt polygon,
+// env)): the shape half of the broadphase guard (DESIGN.md section 3,
+// "Broadphase exactness"), once per rebuilt world part instead of per pair.
+// Edge k is d_k = v_k - v_k-1 (get_edges, cotix/_convex_shapes.py:160-163);
+// the slot stores the pseudo-angle of its line, q = 1 - x in [0, 2) for the
+// l1-normalized direction (x, y) = +-d_k / |d_k|_1 with the sign taken so
+// that y > 0 or (y == 0, x > 0), when
+//  * |d_k|_1 lies in [2^-40, 2^40] (no under/overflow in the products below;
+//    false for NaN),
+//  * the turn at v_k is strictly counter-clockwise beyond the rounding of the
+//    cross product: cross(d_k, d_k+1) > 2^-21 |d_k|_1 |d_k+1|_1 (the world
+//    vertices are in order_clockwise's ascending-angle order, so a strictly
+//    convex part turns left at every vertex),
+//  * a sharp vertex (dot(d_k, d_k+1) < 0: interior angle below 90 degrees) is
+//    not too sharp: |cross| >= 2^-7 |d_k|_1 |d_k+1|_1,
+// and NaN otherwise -- a NaN pseudo-angle fails every edge-pair test of
+// ph_BP0, so a part with any failing vertex is never certified.
+template <int EW>
+CX_DEV void ph_TV4(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const Lay& L = c.L;
+  const uint64_t redo = tv_redo_mask<EW>(c, t, lane);
+  const uint32_t runs = tv_chunks<EW>(c, t, redo);
+  for (int k0 = 0; k0 * WAVE < sc.nvt * EW; ++k0) {
+    if (!((runs >> k0) & 1u)) continue;
+    const int w = k0 * WAVE + lane, e = w % EW, v = w / EW;
+    if (w >= sc.nvt * EW || env0 + e >= a.B) continue;
+    const uint32_t d = t.tb[sc.o_vit + 2 * v], d1 = t.tb[sc.o_vit + 2 * v + 1];
+    const int k = (int)((d >> 5) & 7u), n = (int)((d >> 8) & 15u);
+    if (!tv_item_redo<EW>(c, redo, (int)(d >> 21), e)) continue;
+    const int wo = L.world + (int)(d1 >> 16);
+    const int km = k == 0 ? n - 1 : k - 1, kp = k + 1 == n ? 0 : k + 1;
+    const float xm = t.f(wo + 2 * km, e), ym = t.f(wo + 2 * km + 1, e);
+    const float x0 = t.f(wo + 2 * k, e), y0 = t.f(wo + 2 * k + 1, e);
+    const float xp = t.f(wo + 2 * kp, e), yp = t.f(wo + 2 * kp + 1, e);
+    const float dx0 = x0 - xm, dy0 = y0 - ym, dx1 = xp - x0, dy1 = yp - y0;
+    const float l0 = __builtin_fabsf(dx0) + __builtin_fabsf(dy0), l1 = __builtin_fabsf(dx1) + __builtin_fabsf(dy1);
+    const float cr = dx0 * dy1 - dy0 * dx1, dt = dx0 * dx1 + dy0 * dy1, ll = l0 * l1;
+    const bool ok = (n >= 3) & (l0 >= 9.094947017729282e-13f) & (l0 <= 1.099511627776e12f) &  // [2^-40, 2^40]
+                    (cr > 4.76837158203125e-07f * ll) &                                      // 2^-21
+                    ((dt >= 0.0f) | (__builtin_fabsf(cr) >= 0.0078125f * ll));               // 2^-7
+    const bool flip = (dy0 < 0.0f) | ((dy0 == 0.0f) & (dx0 < 0.0f));
+    const float q = 1.0f - (flip ? -dx0 : dx0) / l0;
+    t.f(L.pedge + (int)(d1 >> 16) / 2 + k, e) = ok ? q : qnan();
   }
 }
 
@@ -1065,78 +1136,44 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
 // (cotix/_contacts.py:205-267), with the rounding of f32 included, so the
 // reference's contact point is NaN and the candidate never writes.  Every
 // other item is flagged for the B list (BP1) that BP2 runs at full lane width.
-// The conditions of the broadphase exactness argument (DESIGN.md section 3,
-// "Broadphase exactness") that the gap test alone does not give, checked on
-// the pair's WORLD shapes (the f32 vertices the reference works on):
-//  (P) every polygon is strictly convex in its stored order (every turn's
-//      |cross| > 2^-21 |d_k|_1 |d_k+1|_1, so the computed signs are exact), no sharp
-//      vertex (dot(d_k, d_k+1) < 0, interior angle < 90 deg) has
-//      |cross(d_k, d_k+1)| < 2^-7 |d_k|_1 |d_k+1|_1  (sin(angle) >= 2^-7);
-//  (E) no edge of A is within |cross| <= 2^-9 |.|_1 |.|_1 of parallel to an
-//      edge of B (AABB edges: the axes).
-// Edge 1-norms lie in [2^-40, 2^40] (no under/overflow in the products).
-// With the gap > 2^-8 S + 2^-16 of BP0 these make every term of
-// _contact_from_edges (cotix/_contacts.py:205-267) NaN / false -- the contact
-// is NaN whatever GJK returns.  False when it cannot certify (full path).
-CX_DEV bool bp_edges(const cx::Shape& P, float* dx, float* dy, float* l1, int* n) {
+// The broadphase exactness argument ("Broadphase
+// exactness") needs, besides the gap, conditions on the pair's WORLD shapes
+// (the f32 vertices the reference works on):
+//  (P) every polygon strictly convex with no too-sharp vertex -- checked once
+//      per rebuilt part by ph_TV4, which leaves a NaN edge direction when not;
+//  (E) no edge of A within |cross(d_a, d_b)| <= 2^-9 |d_a|_1 |d_b|_1 of
+//      parallel to an edge of B (AABB edges: the axes).
+// (E) on the pseudo-angles q of ph_TV4: for l1-unit vectors a, b in the
+// upper half plane and the line distance delta = min(|qa - qb|, 2 - |qa - qb|)
+// (<= 1), |cross(a, b)| >= delta - delta^2 / 2 (equality-checked case split in
+// DESIGN.md), so delta > 2^-9 + 2^-16 -- with q rounded by at most 2^-22 --
+// certifies |cross(d_a, d_b)| > 2^-9 |d_a|_1 |d_b|_1 exactly.  A NaN
+// pseudo-angle fails the test.  False when it cannot certify (the pair takes
+// the full path).
+template <int EW>
+CX_DEV bool bp_guard(const Ctx& c, Tile<EW> t, int e, int pa, int na, int pb, int nb) {
   using namespace cx;
-  if (P.kind != KIND_POLY) {  // AABB: the axes, exactly (get_edges, cotix/_convex_shapes.py:82-93)
-    dx[0] = 1.0f; dy[0] = 0.0f; l1[0] = 1.0f;
-    dx[1] = 0.0f; dy[1] = 1.0f; l1[1] = 1.0f;
-    *n = 2;
-    return true;
-  }
-  bool ok = P.n >= 3;
-  int m = 0;
-  float px = P.w[2 * (P.n - 1)], py = P.w[2 * (P.n - 1) + 1];
+  const int mv = c.sh.maxv > 2 ? c.sh.maxv : 2;  // scene constant (LunarLander: 6)
+  // every read issued before any test (clamped indices): one LDS round trip
+  float qa[MAXV], qb[MAXV];
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    if (k < P.n) {
-      const float x = P.w[2 * k], y = P.w[2 * k + 1];
-      dx[k] = x - px;
-      dy[k] = y - py;
-      l1[k] = __builtin_fabsf(dx[k]) + __builtin_fabsf(dy[k]);
-      ok = ok & (l1[k] >= 9.094947017729282e-13f) & (l1[k] <= 1.099511627776e12f);  // [2^-40, 2^40], false for NaN
-      px = x;
-      py = y;
-      m = k + 1;
+  for (int j = 0; j < MAXV; ++j)
+    if (j < mv) {
+      qa[j] = t.f(pa + (j < na ? j : 0), e);
+      qb[j] = t.f(pb + (j < nb ? j : 0), e);
     }
-  }
-  *n = m;
-  if (!ok) return false;
-  // (P): consecutive edges d_k = v_k - v_k-1, d_k+1; one turning sign, sharp vertices not too sharp
-  bool pos = true, neg = true;
+  constexpr float T = 0.0019683837890625f, T2 = 2.0f - T;  // 2^-9 + 2^-16
+  bool ok = true;
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    if (k < m) {
-      const int j = k + 1 < m ? k + 1 : 0;
-      const float cr = dx[k] * dy[j] - dy[k] * dx[j];
-      const float dt = dx[k] * dx[j] + dy[k] * dy[j];
-      const float ll = l1[k] * l1[j];
-      // the turn's sign beyond the cross product's rounding (2^-21 > 4u): strictly convex exactly
-      pos = pos & (cr > 4.76837158203125e-07f * ll);
-      neg = neg & (cr < -4.76837158203125e-07f * ll);
-      ok = ok & ((dt >= 0.0f) | (__builtin_fabsf(cr) >= 0.0078125f * ll));
+  for (int i = 0; i < MAXV; ++i)
+    if (i < mv) {
+#pragma unroll
+      for (int j = 0; j < MAXV; ++j)
+        if (j < mv) {
+          const float dq = __builtin_fabsf(qa[i] - qb[j]);
+          ok = ok & ((i >= na) | (j >= nb) | ((dq > T) & (dq < T2)));
+        }
     }
-  }
-  return ok & (pos | neg);
-}
-CX_DEV bool bp_guard(const cx::Shape& A, const cx::Shape& B) {
-  using namespace cx;
-  float ax[MAXV], ay[MAXV], al[MAXV], bx[MAXV], by[MAXV], bl[MAXV];
-  int na = 0, nb = 0;
-  bool ok = bp_edges(A, ax, ay, al, &na);
-  ok = ok & bp_edges(B, bx, by, bl, &nb);
-  if (!ok) return false;
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    if (i >= na) break;
-#pragma unroll
-    for (int j = 0; j < MAXV; ++j) {
-      if (j >= nb) break;
-      ok = ok & (__builtin_fabsf(ax[i] * by[j] - ay[i] * bx[j]) > 0.001953125f * (al[i] * bl[j]));
-    }
-  }
   return ok;
 }
 
@@ -1197,20 +1234,12 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
           const float gap = cx::fmax_(cx::fmax_(B[q][0] - A[q][2], A[q][0] - B[q][2]),
                                       cx::fmax_(B[q][1] - A[q][3], A[q][1] - B[q][3]));
           bool skip = poly[q] && gap > margin;  // false for NaN
-          if (skip) {  // the argument's shape conditions, on the world shapes
+          if (skip) {  // the argument's shape conditions, on the world shapes' edge directions (ph_TV4)
             const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci];
-            const int wa = c.L.world + (int)(d0w & 1023u), wb = c.L.world + (int)((d0w >> 10) & 1023u);
-            Shape SA, SB;
-            SA.kind = (int)((d0w >> 23) & 3u);
-            SB.kind = (int)((d0w >> 25) & 3u);
-            SA.n = (int)(d1[q] & 255u);
-            SB.n = (int)((d1[q] >> 8) & 255u);
-#pragma unroll
-            for (int k = 0; k < 2 * MAXV; ++k) {
-              SA.w[k] = t.f(wa + k, e);
-              SB.w[k] = t.f(wb + k, e);
-            }
-            skip = COTIX_BP_GUARD ? bp_guard(SA, SB) : true;
+            const int pa = c.L.pedge + (int)(d0w & 1023u) / 2, pb = c.L.pedge + (int)((d0w >> 10) & 1023u) / 2;
+            const int na = ((d0w >> 23) & 3u) == (uint32_t)KIND_POLY ? (int)(d1[q] & 255u) : 2;
+            const int nb = ((d0w >> 25) & 3u) == (uint32_t)KIND_POLY ? (int)((d1[q] >> 8) & 255u) : 2;
+            skip = COTIX_BP_GUARD ? bp_guard<EW>(c, t, e, pa, na, pb, nb) : true;
             CXK_STAT(bp_cand, 1);
             CXK_STAT(bp_guard_fail, skip ? 0 : 1);
           }
@@ -2064,7 +2093,7 @@ CX_DEV void ph_JE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
   }
 }
 
-template <int EW, bool ROLL = false>
+template <int EW, bool ROLL = false, bool EVAL = false>
 CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
@@ -2078,7 +2107,7 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
       a.err[g] = t.w(c.L.err, e);
       if (a.resets) a.resets[g] += t.w(c.L.nres, e);
       if (ROLL) a.ret[g] += t.f(c.L.ret, e);
-      if (!ROLL && a.judge.on) {
+      if (EVAL && a.judge.on) {
         if (a.reward) a.reward[g] = t.f(c.L.jr, e);
         if (a.finished) a.finished[g] = t.w(c.L.jfin, e);
       }
@@ -2270,6 +2299,8 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_TV1, [&](int l) { ph_TV1<EW>(a, c, t, env0, l); });
       run(PH_TV2, [&](int l) { ph_TV2<EW>(a, c, t, env0, l); });
       run(PH_TV3, [&](int l) { ph_TV3<EW>(a, c, t, env0, l); });
+      if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !(a.dbg_skip & 2))
+        run(PH_TV3, [&](int l) { ph_TV4<EW>(a, c, t, env0, l); });
 #if !defined(__HIP__)
       // host emulation (tests): the vertex items die with phase T -- poison
       // them so that a later step reading stale ones cannot pass by luck
@@ -2328,16 +2359,18 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
 }
 
 // forward: n_steps fused steps; ROLL adds the trajectory save and the return
-// (cotix_rollout), compiled out of the plain step kernel
-template <int EW, int FNSET, bool ROLL, class R>
+// (cotix_rollout), EVAL the device judge and control (cotix_eval with either
+// on), both compiled out of the plain step kernel
+template <int EW, int FNSET, bool ROLL, bool EVAL = false, class R = void>
 CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
+  static_assert(!(ROLL && EVAL), "the rollout has no judge");
   run(PH_LOAD, [&](int l) {
-    ph_load<EW>(a, c, t, env0, l);
+    ph_load<EW, EVAL>(a, c, t, env0, l);
     if (ROLL)
       for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
   });
   const bool keys = (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !(a.dbg_skip & 16);
-  if (!ROLL && a.judge.on) {  // the first NFE's start
+  if (EVAL && a.judge.on) {  // the first NFE's start
     run(PH_J, [&](int l) { ph_JB<EW>(a, c, t, env0, l); });
     run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });
   }
@@ -2352,7 +2385,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       if (a.stages & COTIX_STAGE_COLLIDER) run(PH_K, [&](int l) { ph_K2<EW>(c, t, l, n); });
     }
     const int kso = c.L.kw + slot * c.L.kww;  // this step's sk0, skt in the key window
-    run(PH_A, [&](int l) { ph_A<EW, true>(a, c, t, env0, l, step, slot); });
+    run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso);
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
@@ -2361,7 +2394,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       if (a.dyn_reset != nullptr && a.reset_mode == 1) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     }
     if (ROLL) run(PH_RET, [&](int l) { ph_ret<EW>(a, c, t, env0, l); });
-    if (!ROLL && a.judge.on) {  // cotix_eval: NFE bookkeeping (cotix/_envs.py:77-117)
+    if (EVAL && a.judge.on) {  // cotix_eval: NFE bookkeeping (cotix/_envs.py:77-117)
       run(PH_J, [&](int l) { ph_J<EW>(a, c, t, env0, l); });
       run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });
       if ((step + 1) % a.nfe_len == 0) {
@@ -2373,7 +2406,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       }
     }
   }
-  run(PH_STORE, [&](int l) { ph_store<EW, ROLL>(a, c, t, env0, l); });
+  run(PH_STORE, [&](int l) { ph_store<EW, ROLL, EVAL>(a, c, t, env0, l); });
 }
 
 // backward: steps n_steps-1 .. 0, each re-played from the saved state (so

@@ -214,6 +214,9 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
       }
     }
     s.nvt = nv;
+    int mv = 0;
+    for (int p = 0; p < n_parts; ++p) mv = part_nv[p] > mv ? part_nv[p] : mv;
+    s.maxv = (uint16_t)mv;
   }
   std::vector<int> cpa(s.nc), cpb(s.nc), cfn(s.nc);
   for (int c = 0; c < s.nc; ++c) {

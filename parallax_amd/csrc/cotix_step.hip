@@ -251,7 +251,7 @@ static int check_step_args(const cotix_scene* scene, const float* dyn, const uin
   return 0;
 }
 
-// launch the fused step kernel (mode 0 step, 1 rollout forward, 2 backward re-play)
+// launch the fused step kernel (mode 0 step, 1 rollout forward, 2 backward re-play, 3 eval with a judge/control)
 static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_stream_t stream) {
   if (scene_upload(scene)) return -1;
 #ifdef COTIX_EW4_ONLY
@@ -347,7 +347,9 @@ int cotix_eval(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, co
   ka.dyn_reset = dyn_reset;
   ka.resets = resets;
   ka.obs = obs;
-  return launch(scene, ka, 0, stream);
+  // the judge / control program only when one is on: the plain step program
+  // (specialized, fewer registers) serves the rest (obs, held action, resets)
+  return launch(scene, ka, (ka.judge.on || ka.ctl.on) ? 3 : 0, stream);
 }
 
 int cotix_step(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,

@@ -54,7 +54,8 @@ struct WaveRun {
   }
 #endif
 };
-// MODE 0: step, 1: rollout forward (saves + return), 2: rollout backward;
+// MODE 0: step, 1: rollout forward (saves + return), 2: rollout backward,
+// 3: eval with the device judge / control (cotix_eval);
 // SPEC: scene specialization (cxk::SPEC_*, compile-time dimensions)
 template <int EW, int FNSET, int MODE, int SPEC = cxk::SPEC_GENERIC>
 __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
@@ -78,6 +79,8 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
 #endif
   if (MODE == 2)
     cxk::run_wave_backward<EW, FNSET>(a, c, t, env0, run);
+  else if (MODE == 3)
+    cxk::run_wave<EW, FNSET, false, true>(a, c, t, env0, run);
   else
     cxk::run_wave<EW, FNSET, MODE == 1>(a, c, t, env0, run);
 #ifdef COTIX_PHASE_PROF
@@ -100,7 +103,9 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
   const int F = cxk::launch_fnset(fs, mode);  // the contact-function program for this scene
 #if COTIX_EW == 4  // the default tiling carries the two reference-scene specializations
   if (spec == cxk::SPEC_ROBOCUP && F == F_AN) {
-    if (mode == 2)
+    if (mode == 3)
+      COTIX_LAUNCH_SPEC(F_AN, 3, cxk::SPEC_ROBOCUP);
+    else if (mode == 2)
       COTIX_LAUNCH_SPEC(F_AN, 2, cxk::SPEC_ROBOCUP);
     else if (mode == 1)
       COTIX_LAUNCH_SPEC(F_AN, 1, cxk::SPEC_ROBOCUP);
@@ -118,6 +123,11 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
 #undef COTIX_LAUNCH_SPEC
   if (mode == 2) {
     COTIX_LAUNCH(F_AN, 2);  // the host admits analytic scenes only
+  } else if (mode == 3) {
+    if (F == F_AN)
+      COTIX_LAUNCH(F_AN, 3);
+    else
+      COTIX_LAUNCH(F_ALL, 3);
   } else if (mode == 1) {
     if (F == F_AN)
       COTIX_LAUNCH(F_AN, 1);

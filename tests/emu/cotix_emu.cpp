@@ -49,6 +49,9 @@ void run_blocks(const cxk::KArgs& a, int mode) {
     else if (mode == 1)
       F == 1 ? cxk::run_wave<EW, 1, true>(a, c, t, wv * EW, HostRun{})
              : cxk::run_wave<EW, 15, true>(a, c, t, wv * EW, HostRun{});
+    else if (mode == 3)
+      F == 1 ? cxk::run_wave<EW, 1, false, true>(a, c, t, wv * EW, HostRun{})
+             : cxk::run_wave<EW, 15, false, true>(a, c, t, wv * EW, HostRun{});
     else if (F == 1)
       cxk::run_wave<EW, 1, false>(a, c, t, wv * EW, HostRun{});
     else if (F == 3)
@@ -170,7 +173,7 @@ int emu_eval(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float
   a.dyn_reset = dyn_reset;
   a.resets = resets;
   a.obs = obs;
-  run_any(a, E, 0);
+  run_any(a, E, (a.judge.on || a.ctl.on) ? 3 : 0);
   return 0;
 }
 

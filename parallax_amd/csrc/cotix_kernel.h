@@ -87,6 +87,7 @@ struct SceneHdr {
   uint16_t o_vit;    // per polygon vertex 2 words (cotix_scene.h): part, vertex, count, first item, body | offsets
   uint32_t rcp_mask; // bit b: body b's mass and inertia have exact reciprocals (bodies < 32)
   uint16_t maxv;     // the most vertices of any polygon part (0: none) -- bounds the broadphase guard's loops
+  uint16_t pminv;    // max over polygon pairs of the smaller edge count (AABB: 2) -- the guard's outer loop
 };
 struct SceneDev : SceneHdr {
   uint32_t hot[MAXHOT];
@@ -101,16 +102,16 @@ struct SceneDev : SceneHdr {
 // for cotix/_robocup.py and cotix/_lunar_lander.py; spec_of() admits a scene
 // only when all of them match.
 struct SceneDims {
-  int nb, np, nc, nl, nt, G, W, nmw, poly, rcp_all, rcp_mask, nvt, maxv;
+  int nb, np, nc, nl, nt, G, W, nmw, poly, rcp_all, rcp_mask, nvt, maxv, pminv;
 };
 enum : int { SPEC_GENERIC = 0, SPEC_ROBOCUP = 1, SPEC_LUNAR = 2 };
-constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-                                    {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31, 0, 0},
-                                    {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14, 42, 6}};
+constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+                                    {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31, 0, 0, 0},
+                                    {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14, 42, 6, 4}};
 CX_HD bool dims_match(const SceneHdr& h, const SceneDims& d) {
   return h.nb == d.nb && h.np == d.np && h.nc == d.nc && h.nl == d.nl && h.nt == d.nt && h.G == d.G && h.W == d.W &&
          h.nmw == d.nmw && h.poly == d.poly && h.rcp_all == d.rcp_all && (int)h.rcp_mask == d.rcp_mask &&
-         h.nvt == d.nvt && h.maxv == d.maxv;
+         h.nvt == d.nvt && h.maxv == d.maxv && h.pminv == d.pminv;
 }
 CX_HD int spec_of(const SceneHdr& h) {
   if (dims_match(h, SPEC_DIMS[SPEC_ROBOCUP])) return SPEC_ROBOCUP;
@@ -136,6 +137,7 @@ CX_HD SceneHdr spec_hdr(SceneHdr h) {
     h.rcp_mask = d.rcp_mask;
     h.nvt = d.nvt;
     h.maxv = d.maxv;
+    h.pminv = d.pminv;
   }
   return h;
 }
@@ -781,12 +783,10 @@ CX_DEV uint32_t tv_chunks(const Ctx& c, Tile<EW> t, uint64_t redo) {
 // (HomogenuousTransformer.forward_vector, cotix/_geometry_utils.py:105-112)
 // into the vertex item's x, y
 template <int EW>
-CX_DEV void ph_TV1(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void ph_TV1(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, uint64_t redo, uint32_t runs) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
-  const uint64_t redo = tv_redo_mask<EW>(c, t, lane);
-  const uint32_t runs = tv_chunks<EW>(c, t, redo);
   for (int e = lane; e < EW; e += WAVE) t.w(L.pcv, e) = c.nb >= 32 ? ~0u : ((1u << c.nb) - 1u);
   for (int k0 = 0; k0 * WAVE < sc.nvt * EW; ++k0) {
     if (!((runs >> k0) & 1u)) continue;
@@ -813,11 +813,9 @@ CX_DEV void ph_TV1(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
 // 60-67): the sequential mean of the part's vertices, then atan2 about it;
 // NaN -> 4 (after every angle, all NaN equal: sort_lt is key order)
 template <int EW>
-CX_DEV void ph_TV2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void ph_TV2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, uint64_t redo, uint32_t runs) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
-  const uint64_t redo = tv_redo_mask<EW>(c, t, lane);
-  const uint32_t runs = tv_chunks<EW>(c, t, redo);
   for (int k0 = 0; k0 * WAVE < sc.nvt * EW; ++k0) {
     if (!((runs >> k0) & 1u)) continue;
     const int w = k0 * WAVE + lane, e = w % EW, v = w / EW;
@@ -870,12 +868,10 @@ CX_DEV void ph_TV2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
 // key_j)} + #{j > k : key_j < key_k}, the permutation insertion sort produces
 // -- is its slot in the world part
 template <int EW>
-CX_DEV void ph_TV3(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void ph_TV3(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, uint64_t redo, uint32_t runs) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
-  const uint64_t redo = tv_redo_mask<EW>(c, t, lane);
-  const uint32_t runs = tv_chunks<EW>(c, t, redo);
   for (int k0 = 0; k0 * WAVE < sc.nvt * EW; ++k0) {
     if (!((runs >> k0) & 1u)) continue;
     const int w = k0 * WAVE + lane, e = w % EW, v = w / EW;
@@ -914,15 +910,13 @@ CX_DEV void ph_TV3(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
 //    convex part turns left at every vertex),
 //  * a sharp vertex (dot(d_k, d_k+1) < 0: interior angle below 90 degrees) is
 //    not too sharp: |cross| >= 2^-7 |d_k|_1 |d_k+1|_1,
-// and NaN otherwise -- a NaN pseudo-angle fails every edge-pair test of
-// ph_BP0, so a part with any failing vertex is never certified.
+// and 2^100 otherwise -- it fails every edge-pair test of ph_BP0, so a part
+// with any failing vertex is never certified.
 template <int EW>
-CX_DEV void ph_TV4(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void ph_TV4(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, uint64_t redo, uint32_t runs) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
-  const uint64_t redo = tv_redo_mask<EW>(c, t, lane);
-  const uint32_t runs = tv_chunks<EW>(c, t, redo);
   for (int k0 = 0; k0 * WAVE < sc.nvt * EW; ++k0) {
     if (!((runs >> k0) & 1u)) continue;
     const int w = k0 * WAVE + lane, e = w % EW, v = w / EW;
@@ -943,7 +937,7 @@ CX_DEV void ph_TV4(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
                     ((dt >= 0.0f) | (__builtin_fabsf(cr) >= 0.0078125f * ll));               // 2^-7
     const bool flip = (dy0 < 0.0f) | ((dy0 == 0.0f) & (dx0 < 0.0f));
     const float q = 1.0f - (flip ? -dx0 : dx0) / l0;
-    t.f(L.pedge + (int)(d1 >> 16) / 2 + k, e) = ok ? q : qnan();
+    t.f(L.pedge + (int)(d1 >> 16) / 2 + k, e) = ok ? q : 0x1p100f;  // failed: never certified (ph_BP0)
   }
 }
 
@@ -1147,34 +1141,37 @@ CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
 // upper half plane and the line distance delta = min(|qa - qb|, 2 - |qa - qb|)
 // (<= 1), |cross(a, b)| >= delta - delta^2 / 2 (equality-checked case split in
 // DESIGN.md), so delta > 2^-9 + 2^-16 -- with q rounded by at most 2^-22 --
-// certifies |cross(d_a, d_b)| > 2^-9 |d_a|_1 |d_b|_1 exactly.  A NaN
-// pseudo-angle fails the test.  False when it cannot certify (the pair takes
-// the full path).
+// certifies |cross(d_a, d_b)| > 2^-9 |d_a|_1 |d_b|_1 exactly.  A failed
+// vertex's pseudo-angle (2^100) fails the test.  False when it cannot
+// certify (the pair takes the full path).
 template <int EW>
 CX_DEV bool bp_guard(const Ctx& c, Tile<EW> t, int e, int pa, int na, int pb, int nb) {
   using namespace cx;
-  const int mv = c.sh.maxv > 2 ? c.sh.maxv : 2;  // scene constant (LunarLander: 6)
-  // every read issued before any test (clamped indices): one LDS round trip
+  // the part with fewer edges on the outer side: at most pminv of them
+  // (scene constants; LunarLander 4 x 6)
+  const bool sw = nb < na;
+  const int p0 = sw ? pb : pa, n0 = sw ? nb : na, p1 = sw ? pa : pb, n1 = sw ? na : nb;
+  const int mv = c.sh.maxv > 2 ? c.sh.maxv : 2, m0 = c.sh.pminv > 2 ? c.sh.pminv : 2;
+  // every read issued before any test; indices past a part's edge count
+  // repeat its edge 0 (a repeated test changes nothing), so the tests need no
+  // masks: dq in (T, 2 - T) <=> ||dq| - 1| < 1 - T, and the largest
+  // ||dq| - 1| over the pairs decides (a failed vertex's 2^100 gives a huge
+  // value against a finite q and 1 against itself: fails either way)
   float qa[MAXV], qb[MAXV];
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j)
-    if (j < mv) {
-      qa[j] = t.f(pa + (j < na ? j : 0), e);
-      qb[j] = t.f(pb + (j < nb ? j : 0), e);
-    }
-  constexpr float T = 0.0019683837890625f, T2 = 2.0f - T;  // 2^-9 + 2^-16
-  bool ok = true;
+  for (int j = 0; j < MAXV; ++j) {
+    if (j < m0) qa[j] = t.f(p0 + (j < n0 ? j : 0), e);
+    if (j < mv) qb[j] = t.f(p1 + (j < n1 ? j : 0), e);
+  }
+  float m = 0.0f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
-    if (i < mv) {
+    if (i < m0) {
 #pragma unroll
       for (int j = 0; j < MAXV; ++j)
-        if (j < mv) {
-          const float dq = __builtin_fabsf(qa[i] - qb[j]);
-          ok = ok & ((i >= na) | (j >= nb) | ((dq > T) & (dq < T2)));
-        }
+        if (j < mv) m = __builtin_fmaxf(m, __builtin_fabsf(__builtin_fabsf(qa[i] - qb[j]) - 1.0f));
     }
-  return ok;
+  return m < 0.9980316162109375f;  // 1 - (2^-9 + 2^-16)
 }
 
 // mutation knobs for the tests only (tests/test_broadphase_cpu.py builds the
@@ -2296,11 +2293,19 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
     if (FNSET != FNS_ANALYTIC && c.sh.nvt > 0) {
       run(PH_TV0, [&](int l) { ph_TV0<EW>(a, c, t, env0, l); });
-      run(PH_TV1, [&](int l) { ph_TV1<EW>(a, c, t, env0, l); });
-      run(PH_TV2, [&](int l) { ph_TV2<EW>(a, c, t, env0, l); });
-      run(PH_TV3, [&](int l) { ph_TV3<EW>(a, c, t, env0, l); });
+      // the rebuild flags of TV0 and the chunks they make run, wave-uniform:
+      // computed once (after TV0's sync) for TV1-TV4
+      uint64_t redo = 0ull;
+      uint32_t runs = 0u;
+      run(PH_TV1, [&](int l) {
+        redo = tv_redo_mask<EW>(c, t, l);
+        runs = tv_chunks<EW>(c, t, redo);
+        ph_TV1<EW>(a, c, t, env0, l, redo, runs);
+      });
+      run(PH_TV2, [&](int l) { ph_TV2<EW>(a, c, t, env0, l, redo, runs); });
+      run(PH_TV3, [&](int l) { ph_TV3<EW>(a, c, t, env0, l, redo, runs); });
       if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !(a.dbg_skip & 2))
-        run(PH_TV3, [&](int l) { ph_TV4<EW>(a, c, t, env0, l); });
+        run(PH_TV3, [&](int l) { ph_TV4<EW>(a, c, t, env0, l, redo, runs); });
 #if !defined(__HIP__)
       // host emulation (tests): the vertex items die with phase T -- poison
       // them so that a later step reading stale ones cannot pass by luck

@@ -276,6 +276,14 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   fnset = 0;
   s.poly = 0;
   for (int c = 0; c < s.nc; ++c) s.poly |= (cfn[c] == cx::FN_POLY_POLY || cfn[c] == cx::FN_AABB_POLY) ? 1 : 0;
+  s.pminv = 0;  // the broadphase guard's outer loop bound: max over polygon pairs of the smaller edge count
+  for (int c = 0; c < s.nc; ++c)
+    if (cfn[c] == cx::FN_POLY_POLY || cfn[c] == cx::FN_AABB_POLY) {
+      const int ea = part_kindv[cpa[c]] == cx::KIND_POLY ? part_nv[cpa[c]] : 2;
+      const int eb = part_kindv[cpb[c]] == cx::KIND_POLY ? part_nv[cpb[c]] : 2;
+      const int m = ea < eb ? ea : eb;
+      s.pminv = (uint16_t)(m > s.pminv ? m : s.pminv);
+    }
   for (int c = 0; c < s.nc; ++c) {
     int fn = cfn[c];
     fnset |= (fn == cx::FN_AABB_AABB || fn == cx::FN_CIRCLE_AABB || fn == cx::FN_CIRCLE_CIRCLE) ? FNS_ANALYTIC

@@ -502,28 +502,71 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
   // reset_mode 2 (cotix_eval's next-step autoreset): an env finished at entry
   // starts from its reset state (key chain continues, err and finished cleared)
   const bool r2 = a.reset_mode == 2 && a.dyn_reset != nullptr && a.finished != nullptr;
-  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
-    int e = w % EW, off = w / EW, g = env0 + e;
-    const bool rs = r2 && g < a.B && a.finished[g] != 0u;
-    t.f(c.L.dyn + off, e) = (g < a.B) ? (rs ? a.dyn_reset : a.dyn)[(size_t)off * a.B + g] : 0.0f;
+  uint32_t fin = 0u;  // bit e: env e restarts at entry (r2)
+  if (r2)
+    for (int e = 0; e < EW; ++e) fin |= (env0 + e < a.B && a.finished[env0 + e] != 0u) ? 1u << e : 0u;
+  // per env (lane e < EW; EW <= 64): its words, read into registers before
+  // the batch below so that every global read of the prologue is in flight
+  // together
+  const int ge = env0 + lane;
+  const bool le = lane < EW && ge < a.B, rs = le && ((fin >> lane) & 1u) != 0u;
+  const uint32_t k0 = le ? a.keys[2 * (size_t)ge] : 0u, k1 = le ? a.keys[2 * (size_t)ge + 1] : 0u;
+  const uint32_t er = (le && !rs) ? a.err[ge] : 0u;
+  // the restart counter, read here with the state (the store then writes it:
+  // no read-modify-write round trip at the end of the launch)
+  const uint32_t rc = ((le && a.resets != nullptr) ? a.resets[ge] : 0u) + (rs ? 1u : 0u);
+  uint32_t jf = 0u;
+  float jr = 0.0f;
+  if (EVAL && a.judge.on) {
+    jf = (le && !rs && a.finished != nullptr) ? (a.finished[ge] != 0u ? 1u : 0u) : 0u;
+    jr = (le && a.reward != nullptr) ? a.reward[ge] : 0.0f;
   }
-  ph_geo<EW>(a, c, t, env0, lane);
-  if (a.dyn_reset != nullptr && a.reset_mode == 1)
-    for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
-      int e = w % EW, off = w / EW, g = env0 + e;
-      t.f(c.L.rst + off, e) = (g < a.B) ? a.dyn_reset[(size_t)off * a.B + g] : 0.0f;
+  // the state, the local geometry and the restart state in ONE batch of
+  // global reads per lane (all issued before the first LDS store: one HBM
+  // round trip instead of one per loop iteration -- the K = 1 launch's
+  // fixed cost), item w over [dyn | geo | rst]
+  const int nd = c.nb * 6 * EW, ng = a.geom != nullptr ? c.sh.G * EW : 0;
+  const int nr = (a.dyn_reset != nullptr && a.reset_mode == 1) ? nd : 0, ntot = nd + ng + nr;
+  constexpr int LK = 12;
+  for (int base = 0; base < ntot; base += LK * WAVE) {
+    float r[LK];
+#pragma unroll
+    for (int q = 0; q < LK; ++q) {
+      const int w = base + q * WAVE + lane;
+      const float* src = nullptr;
+      if (w < nd) {
+        const int e = w % EW, g = env0 + e;
+        if (g < a.B) src = (((fin >> e) & 1u) ? a.dyn_reset : a.dyn) + (size_t)(w / EW) * a.B + g;
+      } else if (w < nd + ng) {
+        const int e = (w - nd) % EW, g = env0 + e;
+        if (g < a.B) src = a.geom + (a.gstride ? (size_t)g * a.gstride : (size_t)0) + (w - nd) / EW;
+      } else if (w < ntot) {
+        const int e = (w - nd - ng) % EW, g = env0 + e;
+        if (g < a.B) src = a.dyn_reset + (size_t)((w - nd - ng) / EW) * a.B + g;
+      }
+      r[q] = src != nullptr ? *src : 0.0f;
     }
-  for (int e = lane; e < EW; e += WAVE) {
-    int g = env0 + e;
-    const bool rs = r2 && g < a.B && a.finished[g] != 0u;
-    t.w(c.L.key, e) = (g < a.B) ? a.keys[2 * (size_t)g] : 0u;
-    t.w(c.L.key + 1, e) = (g < a.B) ? a.keys[2 * (size_t)g + 1] : 0u;
-    t.w(c.L.err, e) = (g < a.B && !rs) ? a.err[g] : 0u;
-    t.w(c.L.nres, e) = rs ? 1u : 0u;
+#pragma unroll
+    for (int q = 0; q < LK; ++q) {
+      const int w = base + q * WAVE + lane;
+      if (w < nd)
+        t.f(c.L.dyn + w / EW, w % EW) = r[q];
+      else if (w < nd + ng)
+        t.f(c.L.geo + (w - nd) / EW, (w - nd) % EW) = r[q];
+      else if (w < ntot)
+        t.f(c.L.rst + (w - nd - ng) / EW, (w - nd - ng) % EW) = r[q];
+    }
+  }
+  if (lane < EW) {
+    const int e = lane;
+    t.w(c.L.key, e) = k0;
+    t.w(c.L.key + 1, e) = k1;
+    t.w(c.L.err, e) = er;
+    t.w(c.L.nres, e) = rc;
     t.w(c.L.pcv, e) = 0u;  // no world part built yet in this launch (phase T)
     if (EVAL && a.judge.on) {
-      t.w(c.L.jfin, e) = (g < a.B && !rs && a.finished != nullptr) ? (a.finished[g] != 0u ? 1u : 0u) : 0u;
-      t.f(c.L.jr, e) = (g < a.B && a.reward != nullptr) ? a.reward[g] : 0.0f;
+      t.w(c.L.jfin, e) = jf;
+      t.f(c.L.jr, e) = jr;
     }
   }
 }
@@ -2102,7 +2145,7 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
       a.keys[2 * (size_t)g] = t.w(c.L.key, e);
       a.keys[2 * (size_t)g + 1] = t.w(c.L.key + 1, e);
       a.err[g] = t.w(c.L.err, e);
-      if (a.resets) a.resets[g] += t.w(c.L.nres, e);
+      if (a.resets) a.resets[g] = t.w(c.L.nres, e);
       if (ROLL) a.ret[g] += t.f(c.L.ret, e);
       if (EVAL && a.judge.on) {
         if (a.reward) a.reward[g] = t.f(c.L.jr, e);

@@ -62,7 +62,22 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   extern __shared__ uint32_t lds[];
   const SceneDev* sc = a.sc;
   const int nhot = a.sh.nhot;
-  for (int i = threadIdx.x; i < nhot; i += WPB * 64) lds[i] = sc->hot[i];
+  // the scene tables into LDS: HC reads per thread issued before any store
+  // (one global round trip per HC * 256 words, not one per 256)
+  constexpr int HC = 16;
+  for (int base = 0; base < nhot; base += HC * WPB * 64) {
+    uint32_t r[HC];
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      const int i = base + k * WPB * 64 + (int)threadIdx.x;
+      r[k] = i < nhot ? sc->hot[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      const int i = base + k * WPB * 64 + (int)threadIdx.x;
+      if (i < nhot) lds[i] = r[k];
+    }
+  }
   __syncthreads();
   const cxk::Ctx c = cxk::make_ctx<EW>(cxk::spec_hdr<SPEC>(a.sh));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;

@@ -108,21 +108,32 @@ def obs_checksum(obs):
     return a * M + b
 
 
-def timed_launches(fn, steps, warmup):
-    """`warmup` untimed calls, then `steps` calls bracketed by synchronize;
+def timed_launches(fn, steps, warmup, separate=False):
+    """`warmup` untimed calls, then `steps` calls bracketed by synchronize,
     HIP events around each call on the current stream.  Returns (wall s,
-    mean event ms per call)."""
+    mean event ms per call).  separate=True (short launches, K = 1): the wall
+    pass runs with nothing else in the stream, as an RL loop calls it, and
+    the event pass is `steps` more calls after it (event records between
+    launches inflate the wall time of a 15 us launch by several us)."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
     for e0, e1 in evs:
-        e0.record()
+        if not separate:
+            e0.record()
         fn()
-        e1.record()
+        if not separate:
+            e1.record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    if separate:
+        for e0, e1 in evs:
+            e0.record()
+            fn()
+            e1.record()
+        torch.cuda.synchronize()
     return wall, sum(a.elapsed_time(b) for a, b in evs) / steps
 
 
@@ -150,7 +161,7 @@ def finite_stats(pa, scen, substeps, launches):
             "sample": "%d envs x %d driver steps (one per launch + cotix_check_state)" % (w.B, n)}
 
 
-def valu_roofline(scenario, B, substeps, launch_ms):
+def valu_roofline(scenario, B, substeps, launch_ms, warmup=None):
     """Primary roofline: VALU issue.  SQ_INSTS_VALU per launch from the
     committed rocprofv3 PMC pass of the same workload
     (profiles/latest_pmc_<scenario>.json, tools/gpu_round.sh) over the live
@@ -162,6 +173,8 @@ def valu_roofline(scenario, B, substeps, launch_ms):
         if not (c.get("envs_per_gpu") == B and c.get("substeps_per_launch") == substeps):
             return None
         if c.get("library") != library_build():  # counters of other kernel code: no frac
+            return None
+        if warmup is not None and pmc.get("warmup") != warmup:  # another stretch of the trajectory
             return None
         return {"valu_instr_per_launch": pmc["counters_per_launch"]["SQ_INSTS_VALU"],
                 "traffic": pmc["hbm_bytes_per_launch_corrected"],
@@ -266,28 +279,46 @@ def cpu_baseline_grad(T, seconds):
 # ---------------------------------------------------------------------------
 # secondary figures (rank 0, after the headline)
 # ---------------------------------------------------------------------------
-def sub_step(pa, dev, name, B, substeps, steps, warmup):
+def sub_step(pa, dev, name, B, substeps, steps, warmup, key=None):
+    """A secondary figure; `key` names its committed PMC pass
+    (profiles/latest_pmc_<key>.json, default the scenario name), which must be
+    of the same stretch of the trajectory (warm-up launches) for LunarLander,
+    whose cost changes when the landers touch down."""
+    key = key or name
     scen = make_scenario(pa, name, dev, B)
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
-    wall, ev_ms = timed_launches(lambda: env.step(substeps), steps, warmup)
+    wall, ev_ms = timed_launches(lambda: env.step(substeps), steps, warmup, separate=substeps == 1)
     out = {"workload": WORKLOAD[name] % B, "substeps_per_launch": substeps, "launches": steps,
            "value": B * substeps * steps / wall, "unit": "env-steps/s", "launch_ms": ev_ms,
            "hbm_GBs": bytes_per_env(name, len(scen.bodies)) * B / (ev_ms * 1e-3) / 1e9}
-    v = valu_roofline(name, B, substeps, ev_ms)
-    if v is not None:  # the committed PMC pass of this workload (profiles/latest_pmc_<name>.json)
+    v = valu_roofline(key, B, substeps, ev_ms, warmup if name == "lunar" else None)
+    if v is not None:  # the committed PMC pass of this workload (profiles/latest_pmc_<key>.json)
         out["valu"] = {"achieved": v["valu_instr_per_launch"] / (ev_ms * 1e-3) / 1e9,
                        "frac": v["valu_instr_per_launch"] / (ev_ms * 1e-3) / VALU_PEAK_WAVE_INSTR_S,
                        "unit": "G wave-instr/s", "traffic": v["traffic"], "source": v["source"]}
+    out["driver_steps_timed"] = [warmup * substeps, (warmup + steps) * substeps]
+    if name == "lunar":  # the regime: envs whose lander or a leg chose a contact partner at the next step
+        tr = {}
+        env.step(1, trace=tr)
+        ch = tr["chosen"][0, :3]  # [body][B], j* of bodies 0-2 (lander, legs)
+        own = torch.arange(3, device=ch.device, dtype=ch.dtype)[:, None]
+        out["contact_env_fraction"] = float((ch != own).any(0).float().mean().item())
     out.update(finite_stats(pa, make_scenario(pa, name, dev, B), 1, 64))
     return out
 
 
-def sub_grad(pa, dev, B, T, steps, warmup):
-    r = run_grad(pa, dev, B, T, steps, warmup, rank=0, world_size=1)
-    return {"workload": "RoboCup %d envs, %d-step differentiable rollout, fwd + bwd (BASELINE config 5)" % (B, T),
-            "value": r["value"], "unit": "env-steps/s with d(return)/d(action)", "fwd_ms": r["fwd_ms"],
-            "bwd_ms": r["bwd_ms"], "finite_grad_env_fraction": r["finite"]}
+def sub_grad(pa, dev, B, T, steps, warmup, scenario="robocup"):
+    r = run_grad(pa, dev, B, T, steps, warmup, rank=0, world_size=1, scenario=scenario)
+    out = {"workload": ("BoxWorld %d envs, %d-step differentiable rollout, fwd + bwd (config 5 on a finite scene)"
+                        if scenario == "box" else
+                        "RoboCup %d envs, %d-step differentiable rollout, fwd + bwd (BASELINE config 5)") % (B, T),
+           "value": r["value"], "unit": "env-steps/s with d(return)/d(action)", "fwd_ms": r["fwd_ms"],
+           "bwd_ms": r["bwd_ms"], "finite_grad_env_fraction": r["finite"]}
+    v = grad_valu("grad_box" if scenario == "box" else "grad", B, T, r["fwd_ms"], r["bwd_ms"])
+    if v is not None:
+        out["valu"] = v
+    return out
 
 
 def sub_config1(pa, dev):
@@ -443,8 +474,11 @@ def main():
     if rank == 0 and a.extras == "auto" and a.scenario == "robocup":
         out["k1"] = sub_step(pa, dev, "robocup", B, 1, 200, 10)
         out["finite_scene"] = sub_step(pa, dev, "box", B, a.substeps, 10, 2)
-        out["lunar"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 2)
+        out["lunar"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 2)  # airborne: driver steps 128-768
+        # the landers on the terrain (touch-down at ~700 steps): driver steps 1024-1664
+        out["lunar_contact"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 16, key="lunar_contact")
         out["grad"] = sub_grad(pa, dev, B, 64, 5, 1)
+        out["grad_box"] = sub_grad(pa, dev, B, 64, 5, 1, scenario="box")
         out["config1"] = sub_config1(pa, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -456,13 +490,22 @@ def main():
 # ---------------------------------------------------------------------------
 # config 5 as its own line
 # ---------------------------------------------------------------------------
-def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None):
-    scen = pa.RoboCupEnv(batch=B, device=dev, perturb=True, env_offset=rank * B, total_envs=world_size * B)
+def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario="robocup"):
+    """Config 5: forward (cotix_rollout) + backward (cotix_rollout_backward)
+    of a T-step rollout, d(sum_t x of the action body)/d(per-step dv of it).
+    scenario "box": the same on the box world (finite dynamics), whose
+    gradients are finite -- RoboCup's degenerate reference scene makes most
+    of its envs' gradients NaN."""
+    if scenario == "box":
+        scen = pa.BoxWorld(batch=B, device=dev, env_offset=rank * B, total_envs=world_size * B)
+    else:
+        scen = pa.RoboCupEnv(batch=B, device=dev, perturb=True, env_offset=rank * B, total_envs=world_size * B)
     world = scen.world
+    nb = len(world.bodies)
     dyn0, keys0 = world.dyn.clone(), world.keys.clone()
     gen = torch.Generator(device="cpu").manual_seed(1234 + rank)
     actions = (torch.randn(T, B, 2, generator=gen) * 0.1).to(dev)  # SURVEY 8(d): ball dv ~ N(0, 0.1^2)
-    w = pa.rollout.ball_x_weights(5, 4)
+    w = pa.rollout.ball_x_weights(nb, nb - 1)  # RoboCup: the ball (body 4); box world: the last ball
     evf = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     evb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     state = {}
@@ -473,7 +516,7 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None):
         world.err.zero_()
         if i is not None:
             evf[i][0].record()
-        ret, saved = pa.rollout_forward(world, actions, 4, w)
+        ret, saved = pa.rollout_forward(world, actions, nb - 1, w)
         if i is not None:
             evf[i][1].record()
             evb[i][0].record()
@@ -507,18 +550,45 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None):
             "finite": float(torch.isfinite(ga).all(dim=2).all(dim=0).float().mean().item())}
 
 
+def grad_valu(key, B, T, fwd_ms, bwd_ms):
+    """VALU fractions of the rollout's forward (MODE 1) and backward (MODE 2)
+    kernels from the committed PMC pass of this build and workload
+    (profiles/latest_pmc_<key>.json, per-kernel counters), or None."""
+    try:
+        pmc = json.load(open(os.path.join(ROOT, "profiles", "latest_pmc_%s.json" % key)))
+        c = pmc["config"]
+        if not (c.get("envs_per_gpu") == B and c.get("rollout_steps") == T and pmc.get("library") == library_build()):
+            return None
+        out = {}
+        for part, ms in (("fwd", fwd_ms), ("bwd", bwd_ms)):
+            k = pmc["kernels"][part]
+            ach = k["counters_per_launch"]["SQ_INSTS_VALU"] / (ms * 1e-3)
+            out[part] = {"achieved": ach / 1e9, "frac": ach / VALU_PEAK_WAVE_INSTR_S, "unit": "G wave-instr/s",
+                         "kernel": k["kernel"], "pmc_avg_launch_ms": k["avg_launch_ns"] * 1e-6,
+                         "valu_active_frac_of_wave_cycles": k["valu_active_frac_of_wave_cycles"],
+                         "traffic": k["hbm_bytes_per_launch_corrected"]}
+        out["source"] = "profiles/%s_%s_summary.json" % (pmc["tag"], key)
+        return out
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
+
+
 def main_grad(a):
-    """BASELINE config 5: differentiable RoboCup rollout, forward + backward."""
+    """BASELINE config 5: differentiable RoboCup rollout, forward + backward
+    (--scenario box: the box world)."""
     dist, rank, world_size, dev = init_dist()
     import parallax_amd as pa
     B, T = a.envs, a.substeps
-    r = run_grad(pa, dev, B, T, a.steps, a.warmup, rank, world_size, dist)
+    box = a.scenario == "box"
+    r = run_grad(pa, dev, B, T, a.steps, a.warmup, rank, world_size, dist, "box" if box else "robocup")
+    nb = 7 if box else 5
     # algorithmic HBM bytes of the backward launch per env-step: saved state
-    # (5x6 f32) + key (2 u32) + action (2 f32) read, grad_action (2 f32) written
-    bwd_bytes = (5 * 6 * 4 + 8 + 8 + 8) * B * T
+    # (nb x 6 f32) + key (2 u32) + action (2 f32) read, grad_action (2 f32) written
+    bwd_bytes = (nb * 6 * 4 + 8 + 8 + 8) * B * T
     achieved = bwd_bytes / (r["bwd_ms"] * 1e-3) / 1e9
     out = {
-        "metric": "differentiable 64-step RoboCup rollout, 4096 envs/GPU: env-steps/s with d(return)/d(action)",
+        "metric": "differentiable %d-step %s rollout, %d envs/GPU: env-steps/s with d(return)/d(action)"
+                  % (T, "box-world" if box else "RoboCup", B),
         "value": r["value"],
         "unit": "env-steps/s",
         "n_gpus": world_size,
@@ -529,15 +599,19 @@ def main_grad(a):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (RoboCup scene, per-env ball perturbation; actions N(0, 0.1^2) per step)",
+        "data": "synthetic (%s; actions N(0, 0.1^2) per step)"
+                % ("box world, per-env random balls" if box else "RoboCup scene, per-env ball perturbation"),
         "config": {
-            "workload": "RoboCup (cotix/_robocup.py) %d envs/GPU, %d-step rollout, grad of sum_t ball x "
-                        "w.r.t. per-step ball dv (BASELINE config 5)" % (B, T),
+            "workload": ("BoxWorld %d envs/GPU, %d-step rollout, grad of sum_t x of the last ball w.r.t. its "
+                         "per-step dv (config 5 on a finite scene)" if box else
+                         "RoboCup (cotix/_robocup.py) %d envs/GPU, %d-step rollout, grad of sum_t ball x "
+                         "w.r.t. per-step ball dv (BASELINE config 5)") % (B, T),
             "envs_per_gpu": B,
             "rollout_steps": T,
             "fwd_ms": r["fwd_ms"],
             "bwd_ms": r["bwd_ms"],
             "finite_grad_env_fraction": r["finite"],
+            "library": library_build(),
             "parallelism": "dp%d (independent env shards)" % world_size,
         },
         "roofline": {
@@ -551,9 +625,15 @@ def main_grad(a):
             "launch_ms": r["bwd_ms"],
             "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                     "alg_bytes_per_launch": bwd_bytes},
-            "note": "VALU/latency-bound (the backward re-plays each step's forward); no PMC pass of this mode",
+            "note": "VALU/latency-bound (the backward re-plays each step's forward)",
         },
     }
+    v = grad_valu("grad_box" if box else "grad", B, T, r["fwd_ms"], r["bwd_ms"])
+    if v is None:
+        out["roofline"]["frac_note"] = "no committed PMC pass of this build and workload: frac left null"
+    else:
+        out["roofline"].update(achieved=v["bwd"]["achieved"], frac=v["bwd"]["frac"], traffic=v["bwd"]["traffic"],
+                               fwd=v["fwd"], traffic_source=v["source"])
     if rank == 0 and a.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline_grad(T, a.cpu_seconds)
     if rank == 0:

@@ -571,21 +571,42 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
   }
 }
 
+// split(key, num)[idx] by a pair of adjacent lanes (h = lane & 1, both
+// active): each lane runs the block of one of the key's two words
+// (cx::split_word, the same block), then the pair swaps words with a DPP
+// move -- half the threefry issue of split_at on the chain's critical path.
+// The host emulation runs lanes one by one, so it takes split_at (the same
+// words).
+CX_DEV cx::key2 split_at_pair(cx::key2 k, uint32_t num, uint32_t idx, int h) {
+#if defined(__HIP__)
+  const uint32_t mine = cx::split_word(k, num, 2u * idx + (uint32_t)h);
+  const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp((int)mine, (int)mine, 0xB1, 0xF, 0xF, false);
+  return h ? cx::key2{other, mine} : cx::key2{mine, other};  // quad_perm(1,0,3,2): the pair's other lane
+#else
+  (void)h;
+  return cx::split_at(k, num, idx);
+#endif
+}
+
 // phase A: Euler (cotix/_physics_solvers.py:16-33) + driver extras + key chain
 // phase K: the key window (steps step0 .. step0+n-1), three passes.
 // K0 (one lane per env): the driver key chain k_{s+1} = split(k_s)[0] and the
 // collider's skey_0 = split(k_s)[0] (cotix/_colliders.py:142,
 // examples/test_viz.py:39,66).
+// Items (env, half): the chain on a lane pair per env (split_at_pair).
 template <int EW>
 CX_DEV void ph_K0(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int n) {
   using namespace cx;
   const Lay& L = c.L;
-  for (int e = lane; e < EW; e += WAVE) {
+  for (int w = lane; w < 2 * EW; w += WAVE) {
+    const int e = w >> 1, h = w & 1;
     key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
     for (int s = 0; s < n; ++s) {
-      const key2 s0 = split_at(k, 2u, 0u);
-      t.w(L.kw + s * L.kww, e) = s0.a;
-      t.w(L.kw + s * L.kww + 1, e) = s0.b;
+      const key2 s0 = split_at_pair(k, 2u, 0u, h);
+      if (h == 0) {
+        t.w(L.kw + s * L.kww, e) = s0.a;
+        t.w(L.kw + s * L.kww + 1, e) = s0.b;
+      }
       if (a.stages & COTIX_STAGE_ADVANCE_KEY) k = s0;
     }
   }
@@ -617,6 +638,39 @@ CX_DEV void ph_K2(const Ctx& c, Tile<EW> t, int lane, int n) {
     const int so = c.nt > 0 ? o + 2 + 2 * (c.nt - 1) : o;
     const key2 ck = split_at(key2{t.w(so, e), t.w(so + 1, e)}, (uint32_t)nb, (uint32_t)i);
     t.f(o + 2 + 2 * c.nt + i, e) = unit_float(bits1(ck));
+  }
+}
+
+// a one-step window (K = 1 launches, the RL loop) in ONE pass over (body,
+// env) items: each lane derives its body's choice key through the whole
+// chain (K0 -> K1 -> K2, the same splits), body 0's lane also writes the
+// chain's keys -- no phase syncs or LDS round trips between the three levels
+template <int EW>
+CX_DEV void ph_K_one(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) {
+  using namespace cx;
+  const Lay& L = c.L;
+  const int nb = c.nb;
+  const bool coll = (a.stages & COTIX_STAGE_COLLIDER) != 0;
+  // items ((body, env), half): every split on a lane pair (split_at_pair)
+  for (int w = lane; w < 2 * (coll ? nb : 1) * EW; w += WAVE) {
+    const int p = w >> 1, h = w & 1, e = p % EW, i = p / EW, o = L.kw;
+    const bool wr = i == 0 && h == 0;
+    key2 k = split_at_pair(key2{t.w(L.key, e), t.w(L.key + 1, e)}, 2u, 0u, h);  // K0
+    if (wr) {
+      t.w(o, e) = k.a;
+      t.w(o + 1, e) = k.b;
+    }
+    for (int q = 0; q < c.nt; ++q) {  // K1
+      k = split_at_pair(k, 2u, 0u, h);
+      if (wr) {
+        t.w(o + 2 + 2 * q, e) = k.a;
+        t.w(o + 3 + 2 * q, e) = k.b;
+      }
+    }
+    if (coll) {  // K2
+      const float u = unit_float(bits1(split_at_pair(k, (uint32_t)nb, (uint32_t)i, h)));
+      if (h == 0) t.f(o + 2 + 2 * c.nt + i, e) = u;
+    }
   }
 }
 
@@ -2409,14 +2463,18 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
 // forward: n_steps fused steps; ROLL adds the trajectory save and the return
 // (cotix_rollout), EVAL the device judge and control (cotix_eval with either
 // on), both compiled out of the plain step kernel
+// the forward programs' load phase (the kernel may run it before its
+// workgroup barrier: it touches only the wave's own tile)
+template <int EW, bool ROLL, bool EVAL = false>
+CX_DEV void ph_load_fwd(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int l) {
+  ph_load<EW, EVAL>(a, c, t, env0, l);
+  if (ROLL)
+    for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
+}
 template <int EW, int FNSET, bool ROLL, bool EVAL = false, class R = void>
-CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
+CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, bool loaded = false) {
   static_assert(!(ROLL && EVAL), "the rollout has no judge");
-  run(PH_LOAD, [&](int l) {
-    ph_load<EW, EVAL>(a, c, t, env0, l);
-    if (ROLL)
-      for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
-  });
+  if (!loaded) run(PH_LOAD, [&](int l) { ph_load_fwd<EW, ROLL, EVAL>(a, c, t, env0, l); });
   const bool keys = (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !(a.dbg_skip & 16);
   if (EVAL && a.judge.on) {  // the first NFE's start
     run(PH_J, [&](int l) { ph_JB<EW>(a, c, t, env0, l); });
@@ -2428,9 +2486,13 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     const int slot = step % KWIN;
     if (keys && slot == 0) {
       const int n = a.n_steps - step < KWIN ? a.n_steps - step : KWIN;
-      run(PH_K, [&](int l) { ph_K0<EW>(a, c, t, l, n); });
-      run(PH_K, [&](int l) { ph_K1<EW>(c, t, l, n); });
-      if (a.stages & COTIX_STAGE_COLLIDER) run(PH_K, [&](int l) { ph_K2<EW>(c, t, l, n); });
+      if (n == 1) {
+        run(PH_K, [&](int l) { ph_K_one<EW>(a, c, t, l); });
+      } else {
+        run(PH_K, [&](int l) { ph_K0<EW>(a, c, t, l, n); });
+        run(PH_K, [&](int l) { ph_K1<EW>(c, t, l, n); });
+        if (a.stages & COTIX_STAGE_COLLIDER) run(PH_K, [&](int l) { ph_K2<EW>(c, t, l, n); });
+      }
     }
     const int kso = c.L.kw + slot * c.L.kww;  // this step's sk0, skt in the key window
     run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });

@@ -78,13 +78,22 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
       if (i < nhot) lds[i] = r[k];
     }
   }
-  __syncthreads();
   const cxk::Ctx c = cxk::make_ctx<EW>(cxk::spec_hdr<SPEC>(a.sh));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int env0 = (blockIdx.x * WPB + wave) * EW;
-  if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
   uint32_t* wbase = lds + nhot + wave * (c.L.S * EW + c.W.words);
   const cxk::Tile<EW> t{wbase, lds, wbase + c.L.S * EW};
+  // the forward programs load the wave's state before the barrier: it writes
+  // only the wave's own tile (disjoint from the tables), so its global reads
+  // overlap the table copy's (a launch's fixed cost, K = 1 RL loops)
+  if (MODE != 2 && env0 < a.B) {
+    if (MODE == 3)
+      cxk::ph_load_fwd<EW, false, true>(a, c, t, env0, lane);
+    else
+      cxk::ph_load_fwd<EW, MODE == 1>(a, c, t, env0, lane);
+  }
+  __syncthreads();
+  if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
 #ifdef COTIX_PHASE_PROF
   unsigned long long acc[cxk::PH_COUNT];
   for (int q = 0; q < cxk::PH_COUNT; ++q) acc[q] = 0ull;
@@ -95,9 +104,9 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   if (MODE == 2)
     cxk::run_wave_backward<EW, FNSET>(a, c, t, env0, run);
   else if (MODE == 3)
-    cxk::run_wave<EW, FNSET, false, true>(a, c, t, env0, run);
+    cxk::run_wave<EW, FNSET, false, true>(a, c, t, env0, run, true);
   else
-    cxk::run_wave<EW, FNSET, MODE == 1>(a, c, t, env0, run);
+    cxk::run_wave<EW, FNSET, MODE == 1>(a, c, t, env0, run, true);
 #ifdef COTIX_PHASE_PROF
   if (lane == 0)
     for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);

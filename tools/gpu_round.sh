@@ -13,9 +13,14 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 rc=$?; echo "smoke rc=$rc"; [ $rc -eq 0 ] || { tail -20 $O/smoke.log; exit $rc; }
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc"; cut -c1-200 $O/bench.json; [ $rc -eq 0 ] || { tail $O/bench.err; exit $rc; }
-for sc in robocup lunar; do
+# workload key : bench arguments (lunar_contact: the landers on the terrain,
+# driver steps 1024-1664, the stretch of the bench line's lunar_contact figure)
+for wl in "robocup:--scenario robocup --warmup 2" "lunar:--scenario lunar --warmup 2" \
+          "lunar_contact:--scenario lunar --warmup 16" "box:--scenario box --warmup 2" \
+          "grad:--mode grad --scenario robocup --warmup 1" "grad_box:--mode grad --scenario box --warmup 1"; do
+  sc=${wl%%:*}; args=${wl#*:}
   P=$O/prof_$sc; mkdir -p $P
-  B="python bench.py --scenario $sc --steps 10 --warmup 2 --cpu-baseline off --extras off"
+  B="python bench.py $args --steps 10 --cpu-baseline off --extras off"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- $B > $P/trace_bench.json 2> $P/trace.err || { tail $P/trace.err; exit 2; }
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $P/pmc_fetch -o run --output-format csv -- $B > /dev/null 2> $P/pmc1.err || { tail $P/pmc1.err; exit 3; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $P/pmc_write -o run --output-format csv -- $B > /dev/null 2> $P/pmc2.err || { tail $P/pmc2.err; exit 4; }

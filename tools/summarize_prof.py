@@ -26,6 +26,47 @@ def pmc(d):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+if scen.startswith("grad"):
+    # config 5: the forward (MODE 1) and backward (MODE 2) step kernels, per kernel
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    bench = json.load(open(os.path.join(src, "trace_bench.json")))
+
+    def pmc_k(d, name):
+        agg = defaultdict(list)
+        for r in csv.DictReader(open(os.path.join(src, d, "run_counter_collection.csv"))):
+            if r["Kernel_Name"] == name:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        return {k: sum(v) / len(v) for k, v in agg.items()}
+
+    kernels = {}
+    import re
+
+    def mode_of(name):  # step_kernel<EW, FNSET, MODE[, SPEC]>
+        m = re.search(r"step_kernel<\d+, \d+, (\d+)", name)
+        return int(m.group(1)) if m else -1
+
+    for part, mode in (("fwd", 1), ("bwd", 2)):
+        row = [r for r in stats if K in r["Name"] and mode_of(r["Name"]) == mode][0]
+        c = {}
+        for d in ("pmc_fetch", "pmc_write", "pmc_sq"):
+            c.update(pmc_k(d, row["Name"]))
+        kernels[part] = {"kernel": row["Name"], "calls": int(row["Calls"]), "avg_launch_ns": float(row["AverageNs"]),
+                         "counters_per_launch": c,
+                         "hbm_bytes_per_launch_raw": (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024,
+                         "hbm_bytes_per_launch_corrected": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024,
+                         "valu_active_frac_of_wave_cycles": c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"],
+                         "wait_frac_of_wave_cycles": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]}
+    summary = {"tag": tag, "scenario": scen, "config": bench["config"], "library": bench["config"]["library"],
+               "bench_value": bench["value"], "warmup": bench["warmup"], "steps": bench["steps"], "kernels": kernels}
+    os.makedirs(out, exist_ok=True)
+    json.dump(summary, open(os.path.join(out, "%s_%s_summary.json" % (tag, scen)), "w"), indent=1)
+    json.dump(summary, open(os.path.join(out, "latest_pmc_%s.json" % scen), "w"), indent=1)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(out, "%s_%s_kernel_stats.csv" % (tag, scen)))
+    print(json.dumps({p: {k: v for k, v in kk.items() if k != "counters_per_launch"} for p, kk in kernels.items()},
+                     indent=1))
+    sys.exit(0)
+
 stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
 row = [r for r in stats if K in r["Name"]][0]
 avg_ns = float(row["AverageNs"])
@@ -44,6 +85,8 @@ summary = {
     "bench_event_launch_ms": bench["roofline"]["launch_ms"],
     "bench_value": bench["value"],
     "config": bench["config"],
+    "warmup": bench["warmup"],
+    "steps": bench["steps"],
     "hbm_bytes_per_launch_raw": raw,
     "hbm_bytes_per_launch_corrected": corr,
     "alg_bytes_per_launch": bench["roofline"].get("hbm", bench["roofline"]).get("alg_bytes_per_launch"),

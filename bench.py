@@ -298,12 +298,12 @@ def sub_step(pa, dev, name, B, substeps, steps, warmup, key=None):
                        "frac": v["valu_instr_per_launch"] / (ev_ms * 1e-3) / VALU_PEAK_WAVE_INSTR_S,
                        "unit": "G wave-instr/s", "traffic": v["traffic"], "source": v["source"]}
     out["driver_steps_timed"] = [warmup * substeps, (warmup + steps) * substeps]
-    if name == "lunar":  # the regime: envs whose lander or a leg chose a contact partner at the next step
+    if name == "lunar":  # the regime: envs in which some body chose a contact partner over the next 8 steps
         tr = {}
-        env.step(1, trace=tr)
-        ch = tr["chosen"][0, :3]  # [body][B], j* of bodies 0-2 (lander, legs)
-        own = torch.arange(3, device=ch.device, dtype=ch.dtype)[:, None]
-        out["contact_env_fraction"] = float((ch != own).any(0).float().mean().item())
+        env.step(8, trace=tr)
+        ch = tr["chosen"]  # [step][body][B], j* of body i (cotix/_colliders.py:274-295; i itself: none)
+        own = torch.arange(ch.shape[1], device=ch.device, dtype=ch.dtype)[None, :, None]
+        out["contact_env_fraction"] = float((ch != own).any(1).any(0).float().mean().item())
     out.update(finite_stats(pa, make_scenario(pa, name, dev, B), 1, 64))
     return out
 

@@ -475,8 +475,9 @@ def main():
         out["k1"] = sub_step(pa, dev, "robocup", B, 1, 200, 10)
         out["finite_scene"] = sub_step(pa, dev, "box", B, a.substeps, 10, 2)
         out["lunar"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 2)  # airborne: driver steps 128-768
-        # the landers on the terrain (touch-down at ~700 steps): driver steps 1024-1664
-        out["lunar_contact"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 16, key="lunar_contact")
+        # the landers settled on the terrain (first touch-down ~770, a bounce, settled from
+        # ~2500: tools/ll_regime.py, profiles/r03_ll_regime.json): driver steps 2560-3200
+        out["lunar_contact"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 40, key="lunar_contact")
         out["grad"] = sub_grad(pa, dev, B, 64, 5, 1)
         out["grad_box"] = sub_grad(pa, dev, B, 64, 5, 1, scenario="box")
         out["config1"] = sub_config1(pa, dev)

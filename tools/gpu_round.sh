@@ -14,9 +14,9 @@ rc=$?; echo "smoke rc=$rc"; [ $rc -eq 0 ] || { tail -20 $O/smoke.log; exit $rc; 
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc"; cut -c1-200 $O/bench.json; [ $rc -eq 0 ] || { tail $O/bench.err; exit $rc; }
 # workload key : bench arguments (lunar_contact: the landers on the terrain,
-# driver steps 1024-1664, the stretch of the bench line's lunar_contact figure)
+# driver steps 2560-3200, the stretch of the bench line's lunar_contact figure)
 for wl in "robocup:--scenario robocup --warmup 2" "lunar:--scenario lunar --warmup 2" \
-          "lunar_contact:--scenario lunar --warmup 16" "box:--scenario box --warmup 2" \
+          "lunar_contact:--scenario lunar --warmup 40" "box:--scenario box --warmup 2" \
           "grad:--mode grad --scenario robocup --warmup 1" "grad_box:--mode grad --scenario box --warmup 1"; do
   sc=${wl%%:*}; args=${wl#*:}
   P=$O/prof_$sc; mkdir -p $P

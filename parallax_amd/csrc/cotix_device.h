@@ -727,6 +727,7 @@ CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters, ES& es) {
   const v2 sim[3] = {simplex[0], simplex[1], simplex[2]};
 #pragma unroll
   for (int k = 0; k < NE; ++k) dist[k] = (k < 3) ? edge_dist(sim[k], sim[(k + 1) % 3]) : ((k < ne) ? edge_dist(z, z) : finf());
+  float bd = 0.0f;    // dist of the edge argmin_d picked
   auto argmin_d = [&]() {  // first NaN, else first minimum, over the ne live edges (selects)
     int nanidx = NE, b = 0;
     float bv = dist[0];
@@ -738,22 +739,32 @@ CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters, ES& es) {
     }
 #pragma unroll
     for (int k = NE - 1; k >= 0; --k) nanidx = (k < ne && isn(dist[k])) ? k : nanidx;
+    bd = nanidx < NE ? qnan() : bv;
     return nanidx < NE ? nanidx : b;
   };
   int bei = argmin_d();
   v2 best0 = es.g0(bei), best1 = es.g1(bei);
   v2 newp = simplex[2];
-  v2 prev0 = simplex[0], prev1 = simplex[1];
+  // the previous best edge (iteration 0: the simplex's edge 0) as the loop
+  // condition reads it (:177-212): its unit normal and the norm of its
+  // closest point to the origin.  Both are carried over from where that edge
+  // was the best instead of recomputed -- the same expressions on the same
+  // operands: the normal is the one the split direction used, and
+  // nrm(closest_on_edge_to_origin(e)) == sqrt(edge_dist(e)) (the same sumsq;
+  // a len-0 edge's -a and 0 - a square alike) except for the all-zero edge,
+  // whose edge_dist is inf and whose closest point is the origin (norm 0).
+  v2 pn = fnormal(sub(simplex[0], simplex[1]));
+  pn = divs(pn, nrm(pn));
+  float pd = dist[0];
+  bool pz = simplex[0].x == 0.0f && simplex[0].y == 0.0f && simplex[1].x == 0.0f && simplex[1].y == 0.0f;
   for (int i = 0; i < iters; ++i) {
     bool c1 = sumsq(sub(best0, best1)) > 1e-9f;
     bool c2 = crs(best0, best1) >= 0.0f;
-    v2 n = fnormal(sub(prev0, prev1));
-    n = divs(n, nrm(n));
-    float d = dot(newp, n);
-    float ed = nrm(closest_on_edge_to_origin(prev0, prev1));
+    float d = dot(newp, pn);
+    float ed = pz ? 0.0f : __builtin_sqrtf(pd);
     bool c4 = (d - ed > 1e-6f) || (d <= 0.0f);
     if (!(c4 && !vnan(best0) && !vnan(best1) && c1 && c2)) break;
-    n = fnormal(sub(best0, best1));
+    v2 n = fnormal(sub(best0, best1));
     n = divs(n, nrm(n));
     newp = minkowski(a, b, n);
     const int slot = i + 3;
@@ -766,8 +777,9 @@ CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters, ES& es) {
       if (k == bei) dist[k] = dA;
       if (k == slot) dist[k] = dB;
     }
-    prev0 = best0;
-    prev1 = best1;
+    pn = n;
+    pd = bd;
+    pz = best0.x == 0.0f && best0.y == 0.0f && best1.x == 0.0f && best1.y == 0.0f;
     bei = argmin_d();
     best0 = es.g0(bei);
     best1 = es.g1(bei);
@@ -914,9 +926,17 @@ static __device__ unsigned long long g_dev_sub[4];  // phase-timing build: GJK /
     const int l_ = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));             \
     if (l_ == __builtin_amdgcn_readfirstlane(l_)) atomicAdd(&g_dev_sub[k], clock64() - cx_dsub_t0);  \
   } while (0)
+#define CX_CLOCK() clock64()
+#define CX_DSUB_ADD(k, t0)                                                                          \
+  do {                                                                                              \
+    const int l_ = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));         \
+    if (l_ == __builtin_amdgcn_readfirstlane(l_)) atomicAdd(&g_dev_sub[k], clock64() - (t0));    \
+  } while (0)
 #else
 #define CX_DSUB_T0 ((void)0)
 #define CX_DSUB_T1(k) ((void)0)
+#define CX_CLOCK() 0ull
+#define CX_DSUB_ADD(k, t0) ((void)(t0))
 #endif
 template <class SA, class SB, class MakeStore>
 CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen,
@@ -927,13 +947,20 @@ CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, 
 #if defined(COTIX_ASM_MARKERS) && (defined(__HIP__) || defined(__HIPCC__))
   asm volatile(";#GJK_BEGIN");
 #endif
+  CX_DSUB_T0;
   const bool hit = gjk(a, b, d0, simplex);
+  CX_DSUB_T1(0);
 #if defined(COTIX_ASM_MARKERS) && (defined(__HIP__) || defined(__HIPCC__))
   asm volatile(";#GJK_END");
 #endif
   if (!hit) return false;
   const int iters = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
   if (!need_pen) return true;
+  [[maybe_unused]] const unsigned long long cx_epa_t0 = CX_CLOCK();
+  struct EpaTimer {  // phase-timing build: EPA cycles into slot 1 at scope exit
+    unsigned long long t0;
+    CX_MF ~EpaTimer() { CX_DSUB_ADD(1, t0); }
+  } cx_epa_timer{cx_epa_t0};
   if (iters + 3 <= 14) {
     auto es = make.template get<14>();
     *pen = epa<14, decltype(es)>(a, b, simplex, iters, es);

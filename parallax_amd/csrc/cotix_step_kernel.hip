@@ -187,7 +187,8 @@ extern "C" int cotix_phase_cycles(unsigned long long* out, int n) {
   unsigned long long dsub[4] = {};  // GJK timer of cotix_device.h in slot 4
   if (hipMemcpyFromSymbol(dsub, HIP_SYMBOL(cx::g_dev_sub), sizeof(dsub)) != hipSuccess) return -1;
   if (hipMemcpyToSymbol(HIP_SYMBOL(cx::g_dev_sub), z8, sizeof(dsub)) != hipSuccess) return -1;
-  sub[4] = dsub[0];
+  sub[4] = dsub[0];  // GJK
+  sub[5] = dsub[1];  // EPA
   for (int q = 0; q < 8 && cxk::PH_COUNT + q < n; ++q) out[cxk::PH_COUNT + q] = sub[q];
   return cxk::PH_COUNT + 8 < n ? cxk::PH_COUNT + 8 : n;
 }

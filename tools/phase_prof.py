@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "parallax_amd", "_lib", "libcotix_amd_prof.so")
 NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
          "adj", "F", "K", "E1", "R", "trace", "B0", "B1", "F0", "F1", "F2", "F3",
-         "TV0", "TV1", "TV2", "TV3", "sub0", "sub1", "sub2", "sub3", "sub4", "sub5", "sub6", "sub7"]
+         "TV0", "TV1", "TV2", "TV3", "J", "sub0", "sub1", "sub2", "sub3", "sub4", "sub5", "sub6", "sub7"]
 
 
 def build():
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--substeps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=1, help="untimed launches first (lunar settles after ~40)")
     ap.add_argument("--lib", default=LIB)
     ap.add_argument("--no-broadphase", action="store_true", help="lunar: without COTIX_STAGE_BROADPHASE")
     ap.add_argument("--drop", type=float, default=0.0, help="lunar: lower lander and legs by this much (in contact)")
@@ -57,7 +58,8 @@ def main():
                 scen.dyn_reset[i, 3] = -0.3
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
-    env.step(a.substeps)
+    for _ in range(a.warmup):
+        env.step(a.substeps)
     buf = (ctypes.c_ulonglong * 40)()
     f(buf, 40)  # reset after warm-up
     for _ in range(a.launches):
@@ -67,7 +69,8 @@ def main():
     ew = int(os.environ.get("COTIX_ENVS_PER_WAVE", "4"))
     waves = (B + ew - 1) // ew
     steps = a.launches * a.substeps
-    tot = sum(buf[q] for q in range(min(n, 32)))  # the sub-phase timers (32..) overlap the phases
+    nph = NAMES.index("sub0")
+    tot = sum(buf[q] for q in range(min(n, nph)))  # the sub-phase timers (nph..) overlap the phases
     out = {NAMES[q]: {"cycles_per_wave_step": buf[q] / waves / steps, "share": buf[q] / tot} for q in range(n)
            if buf[q]}
     print(json.dumps({"scenario": a.scenario, "envs": B, "envs_per_wave": ew, "cycles_per_wave_step_total": tot / waves / steps,

@@ -85,9 +85,11 @@ def make_scenario(pa, name, dev, B, offset=0, total=None):
 
 
 def bytes_per_env(name, nb):
-    """Algorithmic HBM bytes per env per launch (state in + out, key in + out,
-    err in + out; LunarLander: + per-env terrain read)."""
-    b = nb * 6 * 4 * 2 + 16 + 8
+    """Algorithmic HBM bytes per env per launch of BatchedEnv.step with
+    autoreset: state in + out, key in + out, err in + out, the
+    restart state read once, the restart counter in + out, the observation
+    [nb][6] written by the kernel; LunarLander: + per-env terrain read."""
+    b = nb * 6 * 4 * 2 + 16 + 8 + nb * 6 * 4 + 8 + nb * 6 * 4
     return b + (84 * 4 if name == "lunar" else 0)
 
 

@@ -1360,11 +1360,207 @@ CX_DEV void ph_BP1(const Ctx& c, Tile<EW> t, int lane, int chunk) {
     t.ws[c.W.bl_list + base + popc64(mask & lanes_below(lane))] = (uint32_t)(chunk * WAVE + lane);
   if (lane == WAVE - 1) t.ws[c.W.bl_n] = base + (uint32_t)popc64(mask);
 }
-// BP2: round r of the B list, one item per lane
+// ---------------------------------------------------------------------------
+// GJK + EPA of a polygon pair on a PAIR of adjacent lanes (GPU, polygon-only
+// program): lane h = 0 holds polygon A, lane h = 1 polygon B; every
+// Minkowski support is one support per lane (A in d on lane 0, B in -d on
+// lane 1) whose results the pair swaps with a DPP move, so both lanes form
+// the same difference bits and then run the same GJK / EPA arithmetic in
+// lockstep (identical values: identical control flow).  Half the support
+// work of the one-lane form on the critical path; each lane keeps its own
+// EPA edge column.  The host emulation runs the one-lane form (the same
+// values); the GPU tests pin this path against the C port.
+// ---------------------------------------------------------------------------
+#if defined(__HIP__)
+constexpr bool PAIR_GJK = true;
+CX_DEV float pair_swap(float x) {  // the value of the pair's other lane (quad_perm 1,0,3,2)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0xB1, 0xF, 0xF, false));
+}
+struct PairSide {
+  const cx::Shape& mine;  // A on lane 0, B on lane 1
+  int h;
+};
+CX_DEV cx::v2 minkowski(const PairSide& p, const PairSide&, cx::v2 d) {
+  const cx::v2 s = cx::support(cx::PolyRef{p.mine}, p.h ? cx::neg(d) : d);
+  const cx::v2 o = cx::v2{pair_swap(s.x), pair_swap(s.y)};
+  return p.h ? cx::sub(o, s) : cx::sub(s, o);  // support(A, d) - support(B, -d) on both lanes
+}
+// EPA (cx::epa, cotix/_collisions.py:115-273) on the lane pair: besides the
+// supports, the pair splits the two new edges' distances (lane 0 the
+// A-side edge, lane 1 the B-side one), the two components of the split
+// direction's division, and the argmin over the edge buffer (lane h scans
+// the entries k = h mod 2; the halves combine as first NaN, else smallest
+// value, then smaller index -- the order the sequential first-min scan
+// induces), exchanging the results with DPP moves.  Buffer entries not yet
+// written read as the zero edge (no zero-fill of the column).  The same
+// expressions on the same operands as cx::epa: bit-identical.
+template <int NE>
+CX_DEV cx::v2 epa_pair(const PairSide& ps, int h, const cx::v2* simplex, int iters, float* col) {
+  using namespace cx;
+  constexpr int NH = (NE + 1) / 2;
+  EdgeCol es{col, WAVE};
+  const v2 z = v2{0.0f, 0.0f};
+  // this lane's half of the distance cache: dh[j] = dist of entry 2j + h
+  float dh[NH];
+  es.s0(0, simplex[0]); es.s1(0, simplex[1]);
+  es.s0(1, simplex[1]); es.s1(1, simplex[2]);
+  es.s0(2, simplex[2]); es.s1(2, simplex[0]);
+  uint32_t wm = 7u;  // bit k: entry k holds an edge; the others are the zero edge
+  const int ne = iters + 3;
+  const v2 sim[3] = {simplex[0], simplex[1], simplex[2]};
+  const float dzero = edge_dist(z, z);
+  {
+    const float d01 = edge_dist(h ? sim[1] : sim[0], h ? sim[2] : sim[1]);  // entry h
+    const float d2 = edge_dist(sim[2], sim[0]);                             // entry 2 (lane 0)
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      const int k = 2 * j + h;
+      dh[j] = j == 0 ? d01 : (k == 2 ? d2 : ((k < ne) ? dzero : finf()));
+    }
+  }
+  float bd = 0.0f;
+  auto argmin_d = [&]() {
+    int nanidx = NE, b = h;
+    float bv = dh[0];  // ne >= 3: entries 0 and 1 are live
+#pragma unroll
+    for (int j = 1; j < NH; ++j) {
+      const int k = 2 * j + h;
+      const bool lt = k < ne && dh[j] < bv;
+      bv = lt ? dh[j] : bv;
+      b = lt ? k : b;
+    }
+#pragma unroll
+    for (int j = NH - 1; j >= 0; --j) {
+      const int k = 2 * j + h;
+      nanidx = (k < ne && isn(dh[j])) ? k : nanidx;
+    }
+    const int onan = __builtin_amdgcn_update_dpp(nanidx, nanidx, 0xB1, 0xF, 0xF, false);
+    const int ob = __builtin_amdgcn_update_dpp(b, b, 0xB1, 0xF, 0xF, false);
+    const float obv = pair_swap(bv);
+    const int fn = nanidx < onan ? nanidx : onan;
+    const bool mine = bv < obv || (!(obv < bv) && b < ob);  // (no NaN among the live entries here)
+    bd = fn < NE ? qnan() : (mine ? bv : obv);
+    return fn < NE ? fn : (mine ? b : ob);
+  };
+  // unconditional reads (the column may hold an older item's words), selected
+  auto g0 = [&](int k) { const v2 v = es.g0(k); return ((wm >> k) & 1u) ? v : z; };
+  auto g1 = [&](int k) { const v2 v = es.g1(k); return ((wm >> k) & 1u) ? v : z; };
+  int bei = argmin_d();
+  v2 best0 = g0(bei), best1 = g1(bei);
+  v2 newp = simplex[2];
+  v2 pn = fnormal(sub(simplex[0], simplex[1]));
+  pn = divs(pn, nrm(pn));
+  float pd = pair_swap(h ? 0.0f : dh[0]);  // dist of entry 0 (lane 0's), on lane 1 ...
+  pd = h ? pd : dh[0];                     // ... and lane 0
+  bool pz = simplex[0].x == 0.0f && simplex[0].y == 0.0f && simplex[1].x == 0.0f && simplex[1].y == 0.0f;
+  for (int i = 0; i < iters; ++i) {
+    bool c1 = sumsq(sub(best0, best1)) > 1e-9f;
+    bool c2 = crs(best0, best1) >= 0.0f;
+    float d = dot(newp, pn);
+    float ed = pz ? 0.0f : __builtin_sqrtf(pd);
+    bool c4 = (d - ed > 1e-6f) || (d <= 0.0f);
+    if (!(c4 && !vnan(best0) && !vnan(best1) && c1 && c2)) break;
+    const v2 fnv = fnormal(sub(best0, best1));
+    const float len = nrm(fnv);
+    const float mc = (h ? fnv.y : fnv.x) / len, oc = pair_swap(mc);  // divs(n, nrm(n)), one component per lane
+    const v2 n = h ? v2{oc, mc} : v2{mc, oc};
+    newp = minkowski(ps, ps, n);
+    const int slot = i + 3;
+    // lane 0 the A-side edge (best0, newp), lane 1 the B-side edge (newp, best1)
+    const float md = edge_dist(h ? newp : best0, h ? best1 : newp), od = pair_swap(md);
+    const float dA = h ? od : md, dB = h ? md : od;
+    if (!((wm >> bei) & 1u)) es.s0(bei, z);  // a zero edge taken as the best: its first word stays zero
+    es.s1(bei, newp);
+    es.s0(slot, newp);
+    es.s1(slot, best1);
+    wm |= (1u << bei) | (1u << slot);
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      const int k = 2 * j + h;
+      if (k == bei) dh[j] = dA;
+      if (k == slot) dh[j] = dB;
+    }
+    pn = n;
+    pd = bd;
+    pz = best0.x == 0.0f && best0.y == 0.0f && best1.x == 0.0f && best1.y == 0.0f;
+    bei = argmin_d();
+    best0 = g0(bei);
+    best1 = g1(bei);
+  }
+  return closest_on_edge_to_origin(best0, best1);
+}
+CX_DEV bool gjk_epa_pair(const cx::Shape& mine, int h, int na, int nb, cx::v2 d0, bool need_pen, cx::v2* pen,
+                         float* col) {
+  using namespace cx;
+  const PairSide ps{mine, h};
+  v2 simplex[3];
+  *pen = v2{0.0f, 0.0f};
+  if (!gjk(ps, ps, d0, simplex)) return false;
+  if (!need_pen) return true;
+  const int iters = na + nb + 1;
+  *pen = iters + 3 <= 14 ? epa_pair<14>(ps, h, simplex, iters, col) : epa_pair<20>(ps, h, simplex, iters, col);
+  return true;
+}
+#else
+constexpr bool PAIR_GJK = false;
+#endif
+// the B list items of the polygon-only program run on lane pairs (GPU)
+template <int FNSET>
+constexpr bool b_pairs() {
+  return PAIR_GJK && FNSET == (FNS_ANALYTIC | FNS_CONVEX);
+}
+// item w on the lane pair (lane, lane ^ 1); h = lane & 1
+template <int EW, int FNSET>
+CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int w) {
+#if defined(__HIP__)
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const int h = lane & 1;
+  const int e = w % EW, ci = w / EW, g = env0 + e;
+  if (g >= a.B) return;  // both lanes of the pair
+  const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
+  const int fn = (int)((d0w >> 20) & 7u);
+  if (fn != FN_POLY_POLY) {  // (not in the reference scenes) the one-lane form on lane 0
+    if (h == 0) b_item<EW, FNSET>(a, c, t, env0, lane, w);
+    return;
+  }
+  CXK_STAT(b_items, h == 0 ? 1 : 0);
+  const int na = (int)(d1w & 255u), nb = (int)((d1w >> 8) & 255u);
+  const int wo = c.L.world + (int)(h ? (d0w >> 10) & 1023u : d0w & 1023u);
+  Shape S;
+  S.kind = KIND_POLY;
+  S.n = h ? nb : na;
+#pragma unroll
+  for (int k = 0; k < 2 * MAXV; ++k) S.w[k] = t.f(wo + k, e);  // the tile's world region has 2*MAXV words of slack
+  const bool self = ((d0w >> 27) & 1u) != 0u;
+  float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
+  Contact ct;
+  const bool hit = (a.dbg_skip & 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
+                                     : gjk_epa_pair(S, h, na, nb, v2{sc.d0x, sc.d0y}, !self, &ct.pen, col);
+  if (h != 0) return;
+  ct.cp = v2{qnan(), qnan()};
+  if (hit && self && self_cp_finite(S)) ct.cp = v2{0.0f, 0.0f};  // S is A on lane 0 (see b_item)
+  else if (hit) t.ws[c.W.cf_flag + w] = 1u;
+  const int co = c.L.con + 4 * ci;
+  t.f(co + 0, e) = ct.pen.x;
+  t.f(co + 1, e) = ct.pen.y;
+  t.f(co + 2, e) = ct.cp.x;
+  t.f(co + 3, e) = ct.cp.y;
+  if (!(isn(ct.cp.x) || isn(ct.cp.y))) atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
+#else
+  (void)a; (void)c; (void)t; (void)env0; (void)lane; (void)w;
+#endif
+}
+// BP2: round r of the B list, one item per lane (lane pairs: b_pairs)
 template <int EW, int FNSET>
 CX_DEV void ph_BP2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int r) {
-  const int k = r * WAVE + lane;
-  if (k < (int)t.ws[c.W.bl_n]) b_item<EW, FNSET>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k]);
+  if constexpr (b_pairs<FNSET>()) {
+    const int k = r * (WAVE / 2) + (lane >> 1);
+    if (k < (int)t.ws[c.W.bl_n]) b_item_pair<EW, FNSET>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k]);
+  } else {
+    const int k = r * WAVE + lane;
+    if (k < (int)t.ws[c.W.bl_n]) b_item<EW, FNSET>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k]);
+  }
 }
 
 // phase F: deferred polygon contact points (contact_from_edges,
@@ -2417,7 +2613,8 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_BP1, [&](int l) { ph_BP1<EW>(c, t, l, ch); });
     const int n = (int)t.ws[c.W.bl_n];  // uniform: read after the phase barrier
     CXK_STAT(b_items, 0);
-    for (int r = 0; r * WAVE < n; ++r) run(PH_B, [&](int l) { ph_BP2<EW, FNSET>(a, c, t, env0, l, r); });
+    constexpr int per_round = b_pairs<FNSET>() ? WAVE / 2 : WAVE;
+    for (int r = 0; r * per_round < n; ++r) run(PH_B, [&](int l) { ph_BP2<EW, FNSET>(a, c, t, env0, l, r); });
   } else if (!(a.dbg_skip & 2)) {
     run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
   }

@@ -1031,25 +1031,32 @@ CX_DEV void cvx_edge_d(const Shape& s, int k, VF vf, v2* e0, v2* e1) {
   else *e1 = vf(k == 0 ? s.n - 1 : k - 1);
 }
 template <class VFA, class VFB>
-CX_DEV v2 cfe_term(const Shape& A, const Shape& B, int s, VFA va, VFB vb) {
-  const int na = cvx_count(A), nb = cvx_count(B);
+CX_DEV v2 cfe_term_contain(const Shape& A, const Shape& B, int s, VFA va, VFB vb) {  // s < |A| + |B|
+  const int na = cvx_count(A);
   const v2 nanv = v2{qnan(), qnan()};
-  if (s < na + nb) {  // a vertex of A tested in B, or of B in A: one containment test on the selected pair
-    const bool fa = s < na;
-    const v2 vA = cvx_vert_d(A, fa ? s : 0, va), vB = cvx_vert_d(B, fa ? 0 : s - na, vb);
-    const v2 v = fa ? vA : vB;
-    Shape S;
-    S.kind = fa ? B.kind : A.kind;
-    S.n = fa ? B.n : A.n;
+  // a vertex of A tested in B, or of B in A: one containment test on the selected pair
+  const bool fa = s < na;
+  const v2 vA = cvx_vert_d(A, fa ? s : 0, va), vB = cvx_vert_d(B, fa ? 0 : s - na, vb);
+  const v2 v = fa ? vA : vB;
+  Shape S;
+  S.kind = fa ? B.kind : A.kind;
+  S.n = fa ? B.n : A.n;
 #pragma unroll
-    for (int q = 0; q < 2 * MAXV; ++q) S.w[q] = bsel(fa, B.w[q], A.w[q]);
-    return shape_contains(S, v) ? v : nanv;
-  }
+  for (int q = 0; q < 2 * MAXV; ++q) S.w[q] = bsel(fa, B.w[q], A.w[q]);
+  return shape_contains(S, v) ? v : nanv;
+}
+template <class VFA, class VFB>
+CX_DEV v2 cfe_term_edge(const Shape& A, const Shape& B, int s, VFA va, VFB vb) {  // s >= |A| + |B|
+  const int na = cvx_count(A), nb = cvx_count(B);
   const int q = s - na - nb, jb = q / na, ia = q - jb * na;
   v2 a0, a1, b0, b1;
   cvx_edge_d(A, ia, va, &a0, &a1);
   cvx_edge_d(B, jb, vb, &b0, &b1);
   return edge_vs_edge(a0, a1, b0, b1);
+}
+template <class VFA, class VFB>
+CX_DEV v2 cfe_term(const Shape& A, const Shape& B, int s, VFA va, VFB vb) {
+  return s < cvx_count(A) + cvx_count(B) ? cfe_term_contain(A, B, s, va, vb) : cfe_term_edge(A, B, s, va, vb);
 }
 
 // circle_vs_polygon :157-202

@@ -271,7 +271,7 @@ constexpr int CFB = 8;                           // items per batch
 constexpr int CFS = 2 * cx::MAXV + cx::MAXV * cx::MAXV;  // max terms per item
 constexpr int EPA_NE = 20;                        // EPA edge column length (epa<20> bound)
 struct WsLay {
-  int cf_flag, cf_list, cf_n, cf_s, cf_res, epa, bl_flag, bl_list, bl_n, bl_pad, vt, words;
+  int cf_flag, cf_list, cf_n, cf_s, cf_c, cf_res, epa, bl_flag, bl_list, bl_n, bl_mode, bl_epa, bl_pad, vt, words;
 };
 CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly, int nvt) {
   WsLay w;
@@ -280,14 +280,19 @@ CX_HD WsLay ws_layout(int nl, int nc, int ew, int poly, int nvt) {
   w.cf_list = w.cf_flag + pad;
   w.cf_n = w.cf_list + pad;
   w.cf_s = w.cf_n + 1;
-  w.cf_res = w.cf_s + CFB;
+  w.cf_c = w.cf_s + CFB;  // per batch item: its containment terms |A| + |B| (F2 runs them apart)
+  w.cf_res = w.cf_c + CFB;
   w.epa = w.cf_res + CFB * CFS * 2;  // per-lane EPA edge columns, [4*EPA_NE][64]
   // broadphase (polygon scenes): per-item keep flags (padded to 64) and the B list
   w.bl_pad = pad;
   w.bl_flag = w.epa + 4 * EPA_NE * 64;
   w.bl_list = w.bl_flag + pad;
   w.bl_n = w.bl_list + pad;
-  w.words = poly ? w.bl_n + 1 : w.cf_flag;
+  // the B list's lane mapping this step (1: lane pairs) and whether an EPA
+  // ran this step (the next step's mode); scheduling only, never results
+  w.bl_mode = w.bl_n + 1;
+  w.bl_epa = w.bl_n + 2;
+  w.words = poly ? w.bl_n + 3 : w.cf_flag;
   // phase T's polygon vertex items (x, y, sort key per vertex, [word][env]):
   // they live only from TV1 to TV3, so they share the EPA columns, which
   // phase B fills afresh each step; else an area of their own
@@ -497,8 +502,10 @@ CX_DEV void ph_geo(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
 
 template <int EW, bool EVAL = false>
 CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
-  if (c.sh.poly)  // phase F's flag array incl. its padding to a multiple of 64
+  if (c.sh.poly) {  // phase F's flag array incl. its padding to a multiple of 64
     for (int w = lane; w < c.W.cf_list - c.W.cf_flag; w += WAVE) t.ws[c.W.cf_flag + w] = 0u;
+    if (lane == 0) t.ws[c.W.bl_epa] = 0u;  // the first step's B list: one lane per item
+  }
   // reset_mode 2 (cotix_eval's next-step autoreset): an env finished at entry
   // starts from its reset state (key chain continues, err and finished cleared)
   const bool r2 = a.reset_mode == 2 && a.dyn_reset != nullptr && a.finished != nullptr;
@@ -1114,6 +1121,7 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
       // instead of by phase F
       if (hit && self && self_cp_finite(A)) ct.cp = v2{0.0f, 0.0f};
       else if (hit) t.ws[c.W.cf_flag + w] = 1u;
+      if (hit && !self) t.ws[c.W.bl_epa] = 1u;  // an EPA ran (B-list scheduling of the next step)
     } else {
       ct = run_contact_set<FNSET>(fn, A, Bs, d0, &er, ((d0w >> 27) & 1u) != 0u);
     }
@@ -1284,6 +1292,10 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int ni = c.nc * EW;
+  if (lane == 0) {  // this step's B-list mode: lane pairs when the last step ran an EPA (contacts)
+    t.ws[c.W.bl_mode] = t.ws[c.W.bl_epa];
+    t.ws[c.W.bl_epa] = 0u;
+  }
   // BQ chunks at a time: every chunk's descriptors, then every box, are read
   // before any is used (the chunks' LDS latencies overlap)
   for (int base = 0; base < c.W.bl_pad; base += BQ * WAVE) {
@@ -1372,7 +1384,11 @@ CX_DEV void ph_BP1(const Ctx& c, Tile<EW> t, int lane, int chunk) {
 // values); the GPU tests pin this path against the C port.
 // ---------------------------------------------------------------------------
 #if defined(__HIP__)
+#ifdef COTIX_NO_PAIR_GJK  // A/B tooling builds only
+constexpr bool PAIR_GJK = false;
+#else
 constexpr bool PAIR_GJK = true;
+#endif
 CX_DEV float pair_swap(float x) {  // the value of the pair's other lane (quad_perm 1,0,3,2)
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0xB1, 0xF, 0xF, false));
 }
@@ -1541,6 +1557,7 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
   ct.cp = v2{qnan(), qnan()};
   if (hit && self && self_cp_finite(S)) ct.cp = v2{0.0f, 0.0f};  // S is A on lane 0 (see b_item)
   else if (hit) t.ws[c.W.cf_flag + w] = 1u;
+  if (hit && !self) t.ws[c.W.bl_epa] = 1u;
   const int co = c.L.con + 4 * ci;
   t.f(co + 0, e) = ct.pen.x;
   t.f(co + 1, e) = ct.pen.y;
@@ -1552,9 +1569,11 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
 #endif
 }
 // BP2: round r of the B list, one item per lane (lane pairs: b_pairs)
+// pairs: the step's mode (lane pairs pay off when EPA runs -- landers on the
+// terrain -- and cost a little on GJK-only lists, e.g. the self pairs in flight)
 template <int EW, int FNSET>
-CX_DEV void ph_BP2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int r) {
-  if constexpr (b_pairs<FNSET>()) {
+CX_DEV void ph_BP2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int r, bool pairs) {
+  if (b_pairs<FNSET>() && pairs) {
     const int k = r * (WAVE / 2) + (lane >> 1);
     if (k < (int)t.ws[c.W.bl_n]) b_item_pair<EW, FNSET>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k]);
   } else {
@@ -1599,7 +1618,7 @@ template <int EW>
 CX_DEV void ph_F1(const Ctx& c, Tile<EW> t, int lane, int b) {
   if (lane >= CFB) return;
   const int n = (int)t.ws[c.W.cf_n];
-  uint32_t cnt = 0u;
+  uint32_t cnt = 0u, cc = 0u;
   if (b + lane < n) {
     const int id = (int)t.ws[c.W.cf_list + b + lane];
     const SceneHdr& sc = c.sh;
@@ -1608,19 +1627,28 @@ CX_DEV void ph_F1(const Ctx& c, Tile<EW> t, int lane, int b) {
     const int na = ((d0w >> 23) & 3u) == (uint32_t)cx::KIND_AABB ? 4 : (int)(d1w & 255u);
     const int nb = ((d0w >> 25) & 3u) == (uint32_t)cx::KIND_AABB ? 4 : (int)((d1w >> 8) & 255u);
     cnt = (uint32_t)(na + nb + na * nb);
+    cc = (uint32_t)(na + nb);
   }
   t.ws[c.W.cf_s + lane] = cnt;
+  t.ws[c.W.cf_c + lane] = cc;
 }
-// F2: round r of the batch: lane -> one term
-template <int EW>
+// F2: round r of the batch: lane -> one term; the containment terms
+// (EDGE = false: vertex k of one shape in the other) and the edge-pair terms
+// (EDGE = true) run in rounds of their own, so a round issues one of the two
+// code paths, not both (the terms land at their index s either way)
+template <int EW, bool EDGE>
 CX_DEV void ph_F2(const Ctx& c, Tile<EW> t, int lane, int b, int r) {
   using namespace cx;
   const int g = r * WAVE + lane;
-  int pre = 0, item = -1;
+  int pre = 0, item = -1, off = 0;
 #pragma unroll
   for (int i = 0; i < CFB; ++i) {
-    const int si = (int)t.ws[c.W.cf_s + i];
-    if (item < 0 && g < pre + si) item = i;
+    const int cc = (int)t.ws[c.W.cf_c + i];
+    const int si = EDGE ? (int)t.ws[c.W.cf_s + i] - cc : cc;
+    if (item < 0 && g < pre + si) {
+      item = i;
+      off = EDGE ? cc : 0;
+    }
     if (item < 0) pre += si;
   }
   if (item < 0) return;
@@ -1631,8 +1659,9 @@ CX_DEV void ph_F2(const Ctx& c, Tile<EW> t, int lane, int b, int r) {
   // per-lane vertex picks straight from the LDS world tile
   auto va = [&](int k) { return v2{t.f(wa + 2 * k, e), t.f(wa + 2 * k + 1, e)}; };
   auto vb = [&](int k) { return v2{t.f(wb + 2 * k, e), t.f(wb + 2 * k + 1, e)}; };
-  const v2 x = cfe_term(A, B, g - pre, va, vb);
-  float* res = reinterpret_cast<float*>(t.ws + c.W.cf_res) + 2 * (item * CFS + (g - pre));
+  const int sidx = off + g - pre;
+  const v2 x = EDGE ? cfe_term_edge(A, B, sidx, va, vb) : cfe_term_contain(A, B, sidx, va, vb);
+  float* res = reinterpret_cast<float*>(t.ws + c.W.cf_res) + 2 * (item * CFS + sidx);
   res[0] = x.x;
   res[1] = x.y;
 }
@@ -2613,8 +2642,9 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_BP1, [&](int l) { ph_BP1<EW>(c, t, l, ch); });
     const int n = (int)t.ws[c.W.bl_n];  // uniform: read after the phase barrier
     CXK_STAT(b_items, 0);
-    constexpr int per_round = b_pairs<FNSET>() ? WAVE / 2 : WAVE;
-    for (int r = 0; r * per_round < n; ++r) run(PH_B, [&](int l) { ph_BP2<EW, FNSET>(a, c, t, env0, l, r); });
+    const bool pairs = b_pairs<FNSET>() && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the phase barrier
+    const int per_round = pairs ? WAVE / 2 : WAVE;
+    for (int r = 0; r * per_round < n; ++r) run(PH_B, [&](int l) { ph_BP2<EW, FNSET>(a, c, t, env0, l, r, pairs); });
   } else if (!(a.dbg_skip & 2)) {
     run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
   }
@@ -2624,9 +2654,13 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     CXK_STAT(f_items, n);
     for (int b = 0; b < n; b += CFB) {
       run(PH_F1, [&](int l) { ph_F1<EW>(c, t, l, b); });
-      int T = 0;
-      for (int i = 0; i < CFB; ++i) T += (int)t.ws[c.W.cf_s + i];
-      for (int r = 0; r * WAVE < T; ++r) run(PH_F2, [&](int l) { ph_F2<EW>(c, t, l, b, r); });
+      int TC = 0, TE = 0;
+      for (int i = 0; i < CFB; ++i) {
+        TC += (int)t.ws[c.W.cf_c + i];
+        TE += (int)t.ws[c.W.cf_s + i] - (int)t.ws[c.W.cf_c + i];
+      }
+      for (int r = 0; r * WAVE < TC; ++r) run(PH_F2, [&](int l) { ph_F2<EW, false>(c, t, l, b, r); });
+      for (int r = 0; r * WAVE < TE; ++r) run(PH_F2, [&](int l) { ph_F2<EW, true>(c, t, l, b, r); });
       run(PH_F3, [&](int l) { ph_F3<EW>(c, t, l, b); });
     }
   }

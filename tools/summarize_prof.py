@@ -18,11 +18,23 @@ out = "profiles"
 K = "step_kernel"
 
 
-def pmc(d):
+def last_dispatches(rows, n):
+    """The step-kernel rows of the LAST n dispatches (the bench's timed launches:
+    with --extras off nothing runs the kernel after them), so that warm-up
+    launches of another regime (LunarLander falls before it settles) do not mix
+    into the per-launch figures."""
+    ids = sorted({int(r["Dispatch_Id"]) for r in rows})[-n:]
+    keep = set(ids)
+    return [r for r in rows if int(r["Dispatch_Id"]) in keep]
+
+
+def pmc(d, n=None):
+    rows = [r for r in csv.DictReader(open(os.path.join(src, d, "run_counter_collection.csv"))) if K in r["Kernel_Name"]]
+    if n:
+        rows = last_dispatches(rows, n)
     agg = defaultdict(list)
-    for r in csv.DictReader(open(os.path.join(src, d, "run_counter_collection.csv"))):
-        if K in r["Kernel_Name"]:
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for r in rows:
+        agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
@@ -69,11 +81,14 @@ if scen.startswith("grad"):
 
 stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
 row = [r for r in stats if K in r["Name"]][0]
-avg_ns = float(row["AverageNs"])
+bench = json.load(open(os.path.join(src, "trace_bench.json")))
+nt = int(bench["steps"])  # the timed launches
+trows = last_dispatches([r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
+                         if K in r["Kernel_Name"]], nt)
+avg_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trows) / len(trows)
 c = {}
 for d in ("pmc_fetch", "pmc_write", "pmc_sq"):
-    c.update(pmc(d))
-bench = json.load(open(os.path.join(src, "trace_bench.json")))
+    c.update(pmc(d, nt))
 raw = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
 corr = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
 summary = {
@@ -81,7 +96,8 @@ summary = {
     "scenario": scen,
     "kernel": row["Name"],
     "calls": int(row["Calls"]),
-    "avg_launch_ns": avg_ns,
+    "timed_launches": nt,
+    "avg_launch_ns": avg_ns,  # over the timed launches (trace), like the counters
     "bench_event_launch_ms": bench["roofline"]["launch_ms"],
     "bench_value": bench["value"],
     "config": bench["config"],

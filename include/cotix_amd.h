@@ -81,8 +81,9 @@ enum {
    * a polygon x polygon / AABB x polygon pair whose world AABBs are separated
    * by more than 2^-8 * S + 2^-16 (S = the pair's largest |coordinate|) and
    * whose world shapes pass the argument's shape conditions (strictly convex,
-   * no sharp vertex with sin(angle) < 2^-7, no edge of one within 2^-9 of
-   * parallel to an edge of the other; checked by the kernel per pair) skips
+   * no sharp vertex with sin(angle) < 2^-7: checked by the kernel once per
+   * rebuilt world part; no edge of one within 2^-9 of parallel to an edge of
+   * the other: checked per pair on the parts' edge pseudo-angles) skips
    * GJK, EPA and the contact points: every term of _contact_from_edges is
    * then provably NaN / false, so the reference's contact is NaN
    * ("Broadphase exactness"). */

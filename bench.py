@@ -22,8 +22,12 @@ The JSON line also carries, measured in the same process after the headline
   k1              the headline scene with ONE driver step per launch (the launch
                   rate an RL loop with per-step actions sees)
   finite_scene    BoxWorld (balls in a box, finite dynamics) at the same size
-  lunar           BASELINE config 2 (LunarLander, 4096 envs, GJK/EPA)
-  grad            BASELINE config 5 (64-step differentiable rollout, fwd + bwd)
+  lunar           BASELINE config 2 (LunarLander, 4096 envs, GJK/EPA) while the
+                  landers fall; lunar_contact: settled on the terrain
+  grad            BASELINE config 5 (64-step differentiable rollout, fwd + bwd);
+                  grad_box: the same on the box world (finite gradients)
+  eval            AbstractEnvironment.eval with a device judge and control,
+                  4 NFEs x 16 env-steps in one cotix_eval launch
   config1         BASELINE config 1 (one LunarLander env, 10,000 steps): GPU
                   and the C port on one core
   roofline        primary bound = VALU issue (SQ_INSTS_VALU of the committed
@@ -323,6 +327,36 @@ def sub_grad(pa, dev, B, T, steps, warmup, scenario="robocup"):
     return out
 
 
+def sub_eval(pa, dev, B, nfe=4, wfe=16, steps=10, warmup=2):
+    """AbstractEnvironment.eval (cotix/_envs.py:37-132) fused into one
+    cotix_eval launch per call: RoboCup, a device judge (the goals as regions
+    with their rewards, the ball's x-velocity as the reward rate, the error
+    trip as done) and a device PD control on the ball, nfe x wfe env-steps
+    at dt = 1e-2 from the same start state each call."""
+    from parallax_amd import envs as E
+    scen = make_scenario(pa, "robocup", dev, B)
+    w = scen.world
+    inf, ab = float("inf"), len(scen.bodies) - 1
+    lo_y, hi_y = [-inf] * 6, [inf] * 6
+    lo_b, hi_b = [-inf] * 6, [inf] * 6
+    hi_y[0], lo_y[1], hi_y[1] = -4.5, -0.5, 0.5
+    lo_b[0], lo_b[1], hi_b[1] = 4.5, -0.5, 0.5
+    judge = E.LinearJudge(rate_w={6 * ab + 2: 0.1}, regions=[(ab, lo_y, hi_y, -1.0), (ab, lo_b, hi_b, 1.0)],
+                          done_on_error=True)
+    control = E.AffineControl(body=ab, gain=[[0, 0, 0.1, 0, 0, 0], [0, 0, 0, 0.1, 0, 0]],
+                              target=[[0, 0, 2.0, 0, 0, 0], [0] * 6])
+    env = E.AbstractEnvironment(E.PhysicsWorld(w, scen.stages), E.WorldState(w.dyn.clone(), w.keys.clone(),
+                                                                            w.err.clone()), control, judge)
+    assert env.fused()
+    period = nfe * wfe * 1e-2
+    state = {}
+    wall, ev_ms = timed_launches(lambda: state.update(r=env.eval(period, nfe, wfe)[1]), steps, warmup)
+    return {"workload": "RoboCup %d envs, AbstractEnvironment.eval with a device judge and control, %d NFEs x %d "
+                        "env-steps in one launch (cotix_eval)" % (B, nfe, wfe),
+            "value": B * nfe * wfe * steps / wall, "unit": "env-steps/s", "launch_ms": ev_ms,
+            "reward_mean": float(state["r"].mean().item())}
+
+
 def sub_config1(pa, dev):
     """BASELINE config 1: one LunarLander env (PRNGKey(0) terrain and key
     chain), 10,000 driver steps in one launch (latency-bound: one wave)."""
@@ -482,6 +516,7 @@ def main():
         out["lunar_contact"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 40, key="lunar_contact")
         out["grad"] = sub_grad(pa, dev, B, 64, 5, 1)
         out["grad_box"] = sub_grad(pa, dev, B, 64, 5, 1, scenario="box")
+        out["eval"] = sub_eval(pa, dev, B)
         out["config1"] = sub_config1(pa, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -354,7 +354,7 @@ def sub_eval(pa, dev, B, nfe=4, wfe=16, steps=10, warmup=2):
     return {"workload": "RoboCup %d envs, AbstractEnvironment.eval with a device judge and control, %d NFEs x %d "
                         "env-steps in one launch (cotix_eval)" % (B, nfe, wfe),
             "value": B * nfe * wfe * steps / wall, "unit": "env-steps/s", "launch_ms": ev_ms,
-            "reward_mean": float(state["r"].mean().item())}
+            "finite_reward_fraction": float(torch.isfinite(state["r"]).float().mean().item())}
 
 
 def sub_config1(pa, dev):

@@ -52,7 +52,7 @@ class BatchedEnv:
         self.reward.zero_()
         return self.observation()
 
-    def step(self, n_steps=1, action=None, action_body=None, trace=None):
+    def step(self, n_steps=1, action=None, action_body=None, trace=None, obs_out=None):
         """n_steps fused driver steps in ONE launch; returns the observation
         f32 [B, n_bodies, 6] (written by the step kernel itself), or with a
         judge StepResult(obs, reward, done).  obs / reward / done are buffers
@@ -62,7 +62,10 @@ class BatchedEnv:
         (no judge), added to the velocity of `action_body` (default: the last
         body, the RoboCup ball) after Euler.  Without a judge, autoreset
         restarts an env from its reset state after any step that sets its
-        error bits (cotix_step_autoreset).  trace: see World.step."""
+        error bits (cotix_step_autoreset).  trace: see World.step.  obs_out: a
+        caller-owned f32 [B, n_bodies, 6] tensor the kernel writes the
+        observation into instead of this env's buffer (e.g. an all-gather
+        send buffer)."""
         w = self.world
         body = len(w.bodies) - 1 if action_body is None else action_body
         if self.judge is None and (trace is not None or (action is not None and action.dim() == 3)):
@@ -73,19 +76,25 @@ class BatchedEnv:
             return self.observation()
         if action is not None:
             action = action.to(w.device, torch.float32).contiguous()
+        obs = self._obs
+        if obs_out is not None:
+            if tuple(obs_out.shape) != tuple(self._obs.shape) or obs_out.dtype != torch.float32 \
+                    or not obs_out.is_contiguous() or obs_out.device != self._obs.device:
+                raise ValueError("obs_out must be a contiguous f32 [B, n_bodies, 6] tensor on the env's device")
+            obs = obs_out
         if self.judge is None:
             w.eval_state(w.dyn, w.keys, w.err, 1, n_steps, self.dt, self.scenario.stages, action=action,
                          action_body=body, control=self._control_c, reset_mode=1 if self.autoreset else 0,
                          dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
-                         resets=self.resets if self.autoreset else None, obs=self._obs)
-            return self._obs
+                         resets=self.resets if self.autoreset else None, obs=obs)
+            return obs
         self.reward.zero_()
         w.eval_state(w.dyn, w.keys, w.err, 1, n_steps, self.dt, self.scenario.stages, judge=self._judge_c,
                      control=self._control_c, reward=self.reward, finished=self.done, action=action,
                      action_body=body, reset_mode=2 if self.autoreset else 0,
                      dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
-                     resets=self.resets if self.autoreset else None, obs=self._obs)
-        return StepResult(self._obs, self.reward, self.done)
+                     resets=self.resets if self.autoreset else None, obs=obs)
+        return StepResult(obs, self.reward, self.done)
 
     def observation(self, out=None):
         """f32 [B, n_bodies, 6] (px, py, vx, vy, angle, angular_velocity),

@@ -166,10 +166,17 @@ def test_step_obs_from_kernel_equals_observe(torch_cuda):
     b = pa.BatchedEnv(pa.RoboCupEnv(batch=1000, device="cuda", perturb=True), autoreset=True)
     a.reset()
     b.reset()
-    for _ in range(7):
-        o = a.step(3)
+    outs = [torch.full((1000, 5, 6), 7.0, device="cuda") for _ in range(2)]
+    for i in range(7):
+        # odd steps: into a caller's buffer (the bench's all-gather send buffers)
+        o = a.step(3, obs_out=outs[i % 2]) if i % 2 else a.step(3)
+        if i % 2:
+            assert o.data_ptr() == outs[1].data_ptr()
         b.world.step(3, 1e-2, b.scenario.stages, dyn_reset=b.scenario.dyn_reset, resets=b.resets)
         ob = b.observation()
         torch.cuda.synchronize()
         assert torch.equal(o.view(torch.int32), ob.view(torch.int32))
     assert torch.equal(a.resets, b.resets) and int(a.resets.sum()) > 0
+    assert bool((outs[0] == 7.0).all())  # never written
+    with pytest.raises(ValueError):
+        a.step(1, obs_out=torch.empty(999, 5, 6, device="cuda"))

@@ -503,11 +503,14 @@ def main():
     }
     if gather is not None:
         out["config"]["obs_all_gather_check"] = gather
-    if rank == 0 and a.extras == "auto":
+    # the CPU baseline and the secondary figures: one-GPU runs only (an N-GPU
+    # line carries the headline; the other ranks would idle in the barrier)
+    single = world_size == 1
+    if rank == 0 and single and a.extras == "auto":
         out["workload_stats"] = finite_stats(pa, make_scenario(pa, a.scenario, dev, B), 1, 64)
-    if rank == 0 and a.cpu_baseline == "auto":
+    if rank == 0 and single and a.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline(a.scenario if a.scenario != "box" else "robocup", a.cpu_seconds)
-    if rank == 0 and a.extras == "auto" and a.scenario == "robocup":
+    if rank == 0 and single and a.extras == "auto" and a.scenario == "robocup":
         out["k1"] = sub_step(pa, dev, "robocup", B, 1, 200, 10)
         out["finite_scene"] = sub_step(pa, dev, "box", B, a.substeps, 10, 2)
         out["lunar"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 2)  # airborne: driver steps 128-768
@@ -672,7 +675,7 @@ def main_grad(a):
     else:
         out["roofline"].update(achieved=v["bwd"]["achieved"], frac=v["bwd"]["frac"], traffic=v["bwd"]["traffic"],
                                fwd=v["fwd"], traffic_source=v["source"])
-    if rank == 0 and a.cpu_baseline == "auto":
+    if rank == 0 and world_size == 1 and a.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline_grad(T, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

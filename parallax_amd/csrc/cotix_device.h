@@ -1187,6 +1187,9 @@ CX_DEV bool resolve_seq(float& vx1, float& vy1, float& w1, const Params& m1, Rcp
   const v2 v1 = v2{vx1 + (-p.r1.y) * w1, vy1 + p.r1.x * w1};  // velocity_at(b1, cp)
   const v2 v2_ = v2{vx2 + (-p.r2.y) * w2, vy2 + p.r2.x * w2};
   const v2 relv = sub(v2_, v1);
+  // moving apart (:140-146): nothing is applied, so the impulse (its divisions
+  // and sqrt) is not computed -- the same early exit as below, taken first
+  if (dot(p.pen, relv) < 0.0f) return false;
   const float vn = dot(relv, p.n);
   const float nim = p.ne * vn - p.pterm;
   const float ni = nim / p.den;
@@ -1197,7 +1200,6 @@ CX_DEV bool resolve_seq(float& vx1, float& vy1, float& w1, const Params& m1, Rcp
   float idr = (-vdn) / p.den;
   idr = clip_(idr, 0.0f, ni * p.mu);
   imp = add(imp, scl(vdu, idr));
-  if (dot(p.pen, relv) < 0.0f) return false;  // moving apart (:140-146)
   // apply_impulse(b1, -imp, cp), apply_impulse(b2, imp, cp)  (:68-73)
   const v2 i1 = neg(imp);
   const float t1 = crs(p.r1, i1), t2 = crs(p.r2, imp);

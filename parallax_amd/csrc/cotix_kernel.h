@@ -1866,10 +1866,9 @@ CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
 // M1 (n > 0 pending items): every lane draws one candidate: G = 64 / n lanes
 // per pending item, in mask order
 template <int EW>
-CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par, int kso) {
+CX_DEV uint32_t m1_pass(const Ctx& c, Tile<EW> t, int lane, uint64_t pend, int kso) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
-  const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
   const int n = popc64(pend);
   uint32_t pass = 0u;
   if (n > 0) {
@@ -1892,15 +1891,18 @@ CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par, int kso) {
       }
     }
   }
-  t.ws[WS_FLAG + lane] = pass;
+  return pass;
+}
+template <int EW>
+CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par, int kso) {
+  const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
+  t.ws[WS_FLAG + lane] = m1_pass<EW>(c, t, lane, pend, kso);
 }
 // M2: lane `lane` settles its own item: the first passing draw of its slot
 // writes the cell, else the scan position advances by G
 template <int EW>
-CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
+CX_DEV uint32_t m2_keep(const Ctx& c, Tile<EW> t, int lane, uint64_t pend, uint64_t pm) {
   const SceneHdr& sc = c.sh;
-  const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
-  const uint64_t pm = wave_ballot(t.ws + WS_FLAG, lane);
   uint32_t keep = 0u;
   if ((pend >> lane) & 1ull) {
     const int n = popc64(pend), G = WAVE / n, slot = popc64(pend & lanes_below(lane));
@@ -1917,11 +1919,35 @@ CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
       keep = (int)pos < t.ti(sc.o_ccnt + l) ? 1u : 0u;
     }
   }
+  return keep;
+}
+template <int EW>
+CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
+  const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
+  const uint64_t pm = wave_ballot(t.ws + WS_FLAG, lane);
+  const uint32_t keep = m2_keep<EW>(c, t, lane, pend, pm);
   t.ws[(par ? WS_KEEP : WS_KEEP2) + lane] = keep;
   // the next round's pending count (read after the phase: 0 ends the scan)
   const int n = wave_count_stored(t.ws + (par ? WS_KEEP : WS_KEEP2), lane, keep != 0u);
   if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)n;
 }
+#if defined(__HIP__)
+// the whole scan as ONE phase on the GPU: every round's pending items and
+// pass bits are in-register ballots (no flag round trips through LDS, no
+// phase syncs between the draw and the settle); the scan positions and the
+// cells stay in LDS, ordered between rounds by a wave fence.  The same
+// per-lane code as M1 / M2 (the host emulation runs those, phase by phase).
+template <int EW>
+CX_DEV void ph_M_fused(const Ctx& c, Tile<EW> t, int lane, int kso) {
+  uint64_t pend = (uint64_t)__ballot(t.ws[WS_KEEP + lane] != 0u);  // M0's active items
+  while (pend != 0ull) {
+    const uint64_t pm = (uint64_t)__ballot(m1_pass<EW>(c, t, lane, pend, kso) != 0u);
+    const uint32_t keep = m2_keep<EW>(c, t, lane, pend, pm);
+    wave_sync();  // the settled scan positions before the next round's draws read them
+    pend = (uint64_t)__ballot(keep != 0u);
+  }
+}
+#endif
 
 // phase D: choose_random_contact (cotix/_colliders.py:274-295)
 CX_DEV cx::Params load_par(const uint32_t* tb, int o) {
@@ -2667,6 +2693,9 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
   if (!(a.dbg_skip & 4) && c.nl > 0 && c.nl * EW <= WAVE) {
     run(PH_C0, [&](int l) { ph_M0<EW>(a, c, t, env0, l); });
     CXK_STAT(wave_steps, 1);
+#if defined(__HIP__)
+    run(PH_C1, [&](int l) { ph_M_fused<EW>(c, t, l, kso); });
+#else
     for (int par = 0; t.ws[WS_N] != 0u; par ^= 1) {  // uniform: read after the phase barrier
       CXK_STAT(rounds, 1);
       if (par == 0) CXK_STAT(active_items, t.ws[WS_N]);
@@ -2674,6 +2703,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_C1, [&](int l) { ph_M1<EW>(c, t, l, par, kso); });
       run(PH_C2, [&](int l) { ph_M2<EW>(c, t, l, par); });
     }
+#endif
   } else if (!(a.dbg_skip & 4) && c.nl > 0) {
     for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {
       run(PH_C0, [&](int l) { ph_C0<EW>(a, c, t, env0, l, ch); });

@@ -1296,10 +1296,13 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
     t.ws[c.W.bl_mode] = t.ws[c.W.bl_epa];
     t.ws[c.W.bl_epa] = 0u;
   }
+#if defined(__HIP__)
+  uint32_t nlist = 0u;  // GPU: the B list is compacted here (BP1's work, in-register ballots)
+#endif
   // BQ chunks at a time: every chunk's descriptors, then every box, are read
   // before any is used (the chunks' LDS latencies overlap)
   for (int base = 0; base < c.W.bl_pad; base += BQ * WAVE) {
-    uint32_t d1[BQ];
+    uint32_t d1[BQ], kq[BQ] = {};
     bool poly[BQ];
     float A[BQ][4], B[BQ][4];
 #pragma unroll
@@ -1360,8 +1363,22 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
         }
       }
       t.ws[c.W.bl_flag + w] = keep;
+      kq[q] = keep;
     }
+    (void)kq;  // (the host emulation compacts in BP1)
+#if defined(__HIP__)
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {  // chunk by chunk, in order: the list BP1 would build
+      if (base + q * WAVE >= c.W.bl_pad) continue;  // uniform
+      const uint64_t mask = (uint64_t)__ballot(kq[q] != 0u);
+      if (kq[q] != 0u) t.ws[c.W.bl_list + nlist + popc64(mask & lanes_below(lane))] = (uint32_t)(base + q * WAVE + lane);
+      nlist += (uint32_t)popc64(mask);
+    }
+#endif
   }
+#if defined(__HIP__)
+  if (lane == 0) t.ws[c.W.bl_n] = nlist;
+#endif
 }
 // BP1: append chunk `chunk`'s flagged items to the B list
 template <int EW>
@@ -1826,8 +1843,9 @@ CX_DEV int select_bit(uint64_t m, int k) {  // position of the k-th (0-based) se
   return pos;
 }
 // M0: activity (a cell whose distinct contacts are all NaN never writes)
+// the item's activity flag (and its scan position reset when active)
 template <int EW>
-CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV uint32_t m0_flag(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   const SceneHdr& sc = c.sh;
   uint32_t flag = 0u;
   if (lane < c.nl * EW) {
@@ -1841,6 +1859,13 @@ CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
       }
     }
   }
+  return flag;
+}
+template <int EW>
+CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  const SceneHdr& sc = c.sh;
+  const uint32_t flag = m0_flag<EW>(a, c, t, env0, lane);
+  (void)sc;
 #ifdef COTIX_STATS
   {
     static unsigned long long wsum = 0;
@@ -1938,8 +1963,10 @@ CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
 // cells stay in LDS, ordered between rounds by a wave fence.  The same
 // per-lane code as M1 / M2 (the host emulation runs those, phase by phase).
 template <int EW>
-CX_DEV void ph_M_fused(const Ctx& c, Tile<EW> t, int lane, int kso) {
-  uint64_t pend = (uint64_t)__ballot(t.ws[WS_KEEP + lane] != 0u);  // M0's active items
+CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso) {
+  // M0: the active items (each lane its own: its scan position is its own word)
+  uint64_t pend = (uint64_t)__ballot(m0_flag<EW>(a, c, t, env0, lane) != 0u);
+  wave_sync();  // the reset scan positions before the draws read them
   while (pend != 0ull) {
     const uint64_t pm = (uint64_t)__ballot(m1_pass<EW>(c, t, lane, pend, kso) != 0u);
     const uint32_t keep = m2_keep<EW>(c, t, lane, pend, pm);
@@ -2640,12 +2667,19 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
   if (!(a.dbg_skip & 1)) {
     run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
     if (FNSET != FNS_ANALYTIC && c.sh.nvt > 0) {
-      run(PH_TV0, [&](int l) { ph_TV0<EW>(a, c, t, env0, l); });
       // the rebuild flags of TV0 and the chunks they make run, wave-uniform:
-      // computed once (after TV0's sync) for TV1-TV4
+      // computed once for TV1-TV4.  On the GPU TV0 runs in TV1's phase (the
+      // flags are ballot from each lane's own word; TV1 reads none of TV0's
+      // other words); the host emulation keeps it a phase of its own
       uint64_t redo = 0ull;
       uint32_t runs = 0u;
+#if !defined(__HIP__)
+      run(PH_TV0, [&](int l) { ph_TV0<EW>(a, c, t, env0, l); });
+#endif
       run(PH_TV1, [&](int l) {
+#if defined(__HIP__)
+        ph_TV0<EW>(a, c, t, env0, l);
+#endif
         redo = tv_redo_mask<EW>(c, t, l);
         runs = tv_chunks<EW>(c, t, redo);
         ph_TV1<EW>(a, c, t, env0, l, redo, runs);
@@ -2665,7 +2699,9 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
   }
   if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !(a.dbg_skip & 2)) {
     run(PH_BP0, [&](int l) { ph_BP0<EW>(a, c, t, env0, l); });
+#if !defined(__HIP__)  // (the GPU's BP0 compacts the list itself)
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_BP1, [&](int l) { ph_BP1<EW>(c, t, l, ch); });
+#endif
     const int n = (int)t.ws[c.W.bl_n];  // uniform: read after the phase barrier
     CXK_STAT(b_items, 0);
     const bool pairs = b_pairs<FNSET>() && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the phase barrier
@@ -2691,11 +2727,11 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     }
   }
   if (!(a.dbg_skip & 4) && c.nl > 0 && c.nl * EW <= WAVE) {
+#if defined(__HIP__)
+    run(PH_C1, [&](int l) { ph_M_fused<EW>(a, c, t, env0, l, kso); });
+#else
     run(PH_C0, [&](int l) { ph_M0<EW>(a, c, t, env0, l); });
     CXK_STAT(wave_steps, 1);
-#if defined(__HIP__)
-    run(PH_C1, [&](int l) { ph_M_fused<EW>(c, t, l, kso); });
-#else
     for (int par = 0; t.ws[WS_N] != 0u; par ^= 1) {  // uniform: read after the phase barrier
       CXK_STAT(rounds, 1);
       if (par == 0) CXK_STAT(active_items, t.ws[WS_N]);

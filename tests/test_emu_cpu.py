@@ -405,35 +405,47 @@ def test_emu_static_part_straddling_chunks_vs_cport(emu_lib, EW, bp):
         assert np.array_equal(g, w)
 
 
-@pytest.mark.parametrize("circle", [False, True], ids=["aabb_poly", "aabb_circle_poly"])
-@pytest.mark.parametrize("EW", [2, 4])
-def test_emu_mixed_kinds_step_vs_cport(emu_lib, EW, circle):
-    """The step kernel's AABB x polygon (and circle x polygon) programs
-    (cxk::launch_fnset 11 / 15): two quads falling onto a static AABB floor
-    (one in contact with the other), optionally a ball; the kernel logic == the
-    C port over 20 steps, 6 envs."""
+@pytest.mark.parametrize("EW", [1, 4, 8])
+def test_emu_robocup_kept_contacts_vs_cport(emu_lib, EW):
+    """Phase B of the analytic program keeps a contact while both parts' world
+    words are the bits of the previous step: restarts into a reset state whose
+    goal body sits elsewhere, a NaN-posed play area, an infinite-mass goal that
+    moves every step in half of the envs and an AABB whose angle alone changes
+    (AABB world words ignore the angle: kept) must recompute exactly the
+    contacts whose inputs changed.  The kernel logic == the C port (trace of
+    the chosen partners and winning candidates too) over 2 launches of 9
+    fused steps; envs with an error bit at launch start restart after their
+    first step."""
     emu, lib = emu_lib
     sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
     from cotix_oracle import cport
-    from cotix_oracle import geometry as G
     from cotix_oracle import physics as P
     _build_cport()
     clib = cport.load()
-    import scene_cases
-    bodies = scene_cases.mixed_scene(circle)
-    h, geom = emu.oracle_scene(lib, bodies)
-    sc = cport.Scene(clib, bodies)
-    B, T = 6, 20
-    base = np.array([b.dyn() for b in bodies], np.float32)
-    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
-    dyn[0, 0, :] += np.linspace(-1, 1, B).astype(np.float32)
-    keys = np.ascontiguousarray(np.stack([np.arange(B), np.arange(B) * 7 + 1], 1).astype(np.uint32))
-    got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
-    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
-    gch, gcl = emu.step_ex(lib, h, *got, geom, 0, T, 1 | 4 | 16 | bp, 2, E=EW)
-    wch, wcl = sc.step_ex(*want, T, 1 | 4 | 16, trace=True)
-    assert (wcl[:, 0, 1] >= 0).sum() + (wcl[:, 1, 0] >= 0).sum() > T  # the triangle sits on the floor
-    assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+    B, T = 20, 9
+    dyn, keys = cport.robocup_batch(B)
+    dyn, keys = np.ascontiguousarray(dyn, np.float32), np.ascontiguousarray(keys, np.uint32)
+    dyn[2, 2, 0::2] = np.float32(0.5)  # a moving infinite-mass goal
+    dyn[3, 5, 1::4] = np.float32(3.0)  # a spinning AABB body: same world words every step
+    reset = dyn.copy()
+    reset[2, 0, 1::2] += np.float32(0.75)  # the goal restarts elsewhere
+    reset[1, 1, 3::5] = np.float32(np.nan)  # a NaN-posed play area
+    h, geom = emu.oracle_scene(lib, P.robocup_bodies())
+    sc = cport.Scene(clib, P.robocup_bodies())
+    err0 = np.zeros(B, np.uint32)
+    err0[1::3] = 1
+    got = [dyn.copy(), keys.copy(), err0.copy(), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), err0.copy(), np.zeros(B, np.uint32)]
+    for launch in range(2):
+        gch, gcl = emu.step_ex(lib, h, got[0], got[1], got[2], geom, 0, T, cport.STAGES_ROBOCUP, 5, E=EW,
+                               dyn_reset=reset, resets=got[3])
+        wch, wcl = sc.step_ex(want[0], want[1], want[2], T, cport.STAGES_ROBOCUP, None, None, 0, reset, want[3],
+                              trace=True)
+        assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+        if launch == 0:
+            got[2][0::4] = 1
+            want[2][0::4] = 1
+    assert want[3].sum() >= len(err0[1::3]) + len(err0[0::4])
     assert same_f32(got[0], want[0])
     for g, w in zip(got[1:], want[1:]):
         assert np.array_equal(g, w)

@@ -801,20 +801,10 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
     // circle lanes read an address register only the AABB lanes defined).
     const bool circ = kind == KIND_CIRCLE;
     const float g0 = t.f(lgo, e), g1 = t.f(lgo + 1, e), g2 = t.f(lgo + 2, e), g3 = t.f(lgo + 3, e);
-    const float n0 = circ ? g0 : g0 + px, n1 = circ ? g1 + px : g1 + py, n2 = circ ? g2 + py : g2 + px,
-                n3 = circ ? g3 : g3 + py;
-    if (FNSET == FNS_ANALYTIC) {
-      // the part keeps its contacts (ph_B_analytic) when its world words are
-      // the bits they were computed from at the previous step of this launch
-      const uint32_t o0 = t.w(wo, e), o1 = t.w(wo + 1, e), o2 = t.w(wo + 2, e), o3 = t.w(wo + 3, e);
-      const bool same = (t.w(c.L.pcv, e) != 0u) & (o0 == __float_as_uint(n0)) & (o1 == __float_as_uint(n1)) &
-                        (o2 == __float_as_uint(n2)) & (o3 == __float_as_uint(n3));
-      t.w(c.L.pbox + p, e) = same ? 1u : 0u;
-    }
-    t.f(wo + 0, e) = n0;
-    t.f(wo + 1, e) = n1;
-    t.f(wo + 2, e) = n2;
-    t.f(wo + 3, e) = n3;
+    t.f(wo + 0, e) = circ ? g0 : g0 + px;
+    t.f(wo + 1, e) = circ ? g1 + px : g1 + py;
+    t.f(wo + 2, e) = circ ? g2 + py : g2 + px;
+    t.f(wo + 3, e) = circ ? g3 : g3 + py;
     if (FNSET != FNS_ANALYTIC) {  // the part's world AABB (broadphase, ph_BP0)
       const int bo = c.L.pbox + 4 * p;
       const float w0 = t.f(wo, e), w1 = t.f(wo + 1, e), w2 = t.f(wo + 2, e), w3 = t.f(wo + 3, e);
@@ -1160,13 +1150,6 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
 // BQ chunks fetch their descriptors and both shapes first, then compute, so
 // the LDS latency of a chunk overlaps the others instead of adding up
 constexpr int BQ = 4;
-// Kept contacts: a contact function is a pure function of the bits of its
-// two world shapes, so an item whose two parts' world words are the bits of
-// the previous step (phase T's per-part flags in pbox, analytic scenes)
-// keeps the contact it holds in the tile -- the bits a recomputation gives --
-// and only re-marks its valid bit.  circle_vs_aabb is always recomputed (its
-// error bit is raised afresh every step).  The static bodies' contacts
-// (RoboCup: 32 of the 40) are computed at a launch's first step only.
 template <int EW>
 CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
@@ -1174,16 +1157,11 @@ CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, in
   const int ni = c.nc * EW;
   for (int base = 0; base < ni; base += BQ * WAVE) {
     uint32_t dw[BQ];
-    bool kept[BQ];
     float ga[BQ][4], gb[BQ][4];
 #pragma unroll
     for (int q = 0; q < BQ; ++q) {
       const int w0 = base + q * WAVE + lane, w = w0 < ni ? w0 : ni - 1;  // clamped: every read in range
-      const int e = w % EW;
       dw[q] = t.tb[sc.o_cdesc + 2 * (w / EW)];
-      const uint32_t d1 = t.tb[sc.o_cdesc + 2 * (w / EW) + 1];
-      const uint32_t ka = t.w(c.L.pbox + (int)((d1 >> 16) & 255u), e), kb = t.w(c.L.pbox + (int)(d1 >> 24), e);
-      kept[q] = (((dw[q] >> 20) & 7u) != (uint32_t)FN_CIRCLE_AABB) & (ka != 0u) & (kb != 0u);
     }
 #pragma unroll
     for (int q = 0; q < BQ; ++q) {
@@ -1200,17 +1178,6 @@ CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, in
     for (int q = 0; q < BQ; ++q) {
       const int w = base + q * WAVE + lane, e = w % EW, ci = w / EW;
       if (w >= ni || env0 + e >= a.B) continue;
-      if (kept[q]) {
-        const int co = c.L.con + 4 * ci;
-        if (!(isn(t.f(co + 2, e)) || isn(t.f(co + 3, e)))) {
-#if defined(__HIP__) || defined(__HIPCC__)
-          atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
-#else
-          t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
-#endif
-        }
-        continue;
-      }
       CXK_STAT(b_items, 1);
       Shape A, Bs;
       A.kind = (int)((dw[q] >> 23) & 3u);
@@ -1245,9 +1212,6 @@ CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, in
       }
     }
   }
-  // the world words now hold the bits of this step's contacts (phase T of
-  // the next step compares against them)
-  for (int e = lane; e < EW; e += WAVE) t.w(c.L.pcv, e) = 1u;
 }
 template <int EW, int FNSET>
 CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {

@@ -406,16 +406,14 @@ def test_emu_static_part_straddling_chunks_vs_cport(emu_lib, EW, bp):
 
 
 @pytest.mark.parametrize("EW", [1, 4, 8])
-def test_emu_robocup_kept_contacts_vs_cport(emu_lib, EW):
-    """Phase B of the analytic program keeps a contact while both parts' world
-    words are the bits of the previous step: restarts into a reset state whose
-    goal body sits elsewhere, a NaN-posed play area, an infinite-mass goal that
-    moves every step in half of the envs and an AABB whose angle alone changes
-    (AABB world words ignore the angle: kept) must recompute exactly the
-    contacts whose inputs changed.  The kernel logic == the C port (trace of
-    the chosen partners and winning candidates too) over 2 launches of 9
-    fused steps; envs with an error bit at launch start restart after their
-    first step."""
+def test_emu_robocup_moving_static_bodies_vs_cport(emu_lib, EW):
+    """The analytic program with infinite-mass bodies that do move: restarts
+    into a reset state whose goal body sits elsewhere, a NaN-posed play area,
+    an infinite-mass goal that moves every step in half of the envs and an
+    AABB body whose angle alone changes.  The kernel logic == the C port
+    (trace of the chosen partners and winning candidates too) over 2 launches
+    of 9 fused steps; envs with an error bit at launch start restart after
+    their first step."""
     emu, lib = emu_lib
     sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
     from cotix_oracle import cport

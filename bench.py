@@ -512,7 +512,7 @@ def main():
     if rank == 0 and single and a.extras == "auto":
         out["workload_stats"] = finite_stats(pa, make_scenario(pa, a.scenario, dev, B), 1, 64)
     if rank == 0 and single and a.extras == "auto" and a.scenario == "robocup":
-        out["k1"] = sub_step(pa, dev, "robocup", B, 1, 200, 10)
+        out["k1"] = sub_step(pa, dev, "robocup", B, 1, 2000, 50)
         out["finite_scene"] = sub_step(pa, dev, "box", B, a.substeps, 10, 2)
         out["lunar"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 2)  # airborne: driver steps 128-768
         # the landers settled on the terrain (first touch-down ~770, a bounce, settled from

@@ -73,7 +73,25 @@ def parse():
     ap.add_argument("--extras", default="auto", choices=["auto", "off"])
     ap.add_argument("--mode", default="step", choices=["step", "grad"])
     ap.add_argument("--dump-gather", default=None, help="save the last all-gathered and local observation (.npz)")
-    return ap.parse_args()
+    ap.add_argument("--envs-per-wave", type=int, default=0, choices=[0, 1, 2, 4, 8],
+                    help="kernel tiling (0: the library default, 4); recorded in config")
+    ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
+                    help="0: the generic kernel instead of the reference scenes' specializations")
+    a = ap.parse_args()
+    refuse_overrides()
+    return a
+
+
+# environment variables the bench itself reads; any other COTIX_* variable
+# could select another library or kernel behaviour behind the line's back
+BENCH_ENV_OK = {"COTIX_BENCH_FORCE_DIST"}
+
+
+def refuse_overrides():
+    bad = sorted(k for k in os.environ if k.startswith("COTIX_") and k not in BENCH_ENV_OK)
+    if bad:
+        sys.exit("bench.py: refusing to run with COTIX_* overrides set (%s): kernel variants are bench "
+                 "flags (--envs-per-wave, --specialize) and are recorded in the line" % ", ".join(bad))
 
 
 # ---------------------------------------------------------------------------
@@ -404,6 +422,7 @@ def main():
 
     B = a.envs
     scen = make_scenario(pa, a.scenario, dev, B, rank * B, world_size * B)
+    scen.world.set_variant(a.envs_per_wave, bool(a.specialize))
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
     nbody = len(scen.bodies)
@@ -498,6 +517,7 @@ def main():
             "substeps_per_launch": a.substeps,
             "autoreset_on_error": True,
             "library": library_build(),
+            "kernel_variant": scen.world.scene.variant(),
             "episode_restarts": resets,
             "restarts_per_env_step": resets / (B * a.substeps * (a.steps + a.warmup)),
             "parallelism": "dp%d (independent env shards by global env id, RCCL obs all-gather)" % world_size,
@@ -548,6 +568,7 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario
         scen = pa.RoboCupEnv(batch=B, device=dev, perturb=True, env_offset=rank * B, total_envs=world_size * B)
     world = scen.world
     nb = len(world.bodies)
+    variant = world.scene.variant()
     dyn0, keys0 = world.dyn.clone(), world.keys.clone()
     gen = torch.Generator(device="cpu").manual_seed(1234 + rank)
     actions = (torch.randn(T, B, 2, generator=gen) * 0.1).to(dev)  # ball dv ~ N(0, 0.1^2)
@@ -590,7 +611,7 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     wall = float(tmax.item())
     ga = state["ga"]
-    return {"value": B * T * steps * world_size / wall, "wall": wall,
+    return {"value": B * T * steps * world_size / wall, "wall": wall, "variant": variant,
             "fwd_ms": sum(e0.elapsed_time(e1) for e0, e1 in evf) / steps,
             "bwd_ms": sum(e0.elapsed_time(e1) for e0, e1 in evb) / steps,
             "finite": float(torch.isfinite(ga).all(dim=2).all(dim=0).float().mean().item())}
@@ -658,6 +679,7 @@ def main_grad(a):
             "bwd_ms": r["bwd_ms"],
             "finite_grad_env_fraction": r["finite"],
             "library": library_build(),
+            "kernel_variant": r["variant"],
             "parallelism": "dp%d (independent env shards)" % world_size,
         },
         "roofline": {

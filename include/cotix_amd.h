@@ -114,6 +114,14 @@ int cotix_scene_destroy(cotix_scene* scene);
 int cotix_scene_geom_floats(const cotix_scene* scene);
 /* introspection for tests: counts of distinct contacts / cells / candidates / type keys */
 int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, int* n_candidates, int* n_types);
+/* Kernel variant of the scene's launches (no reference counterpart: a tiling
+ * choice; every variant computes the same bits).  envs_per_wave: 0 (default,
+ * 4) | 1 | 2 | 4 | 8; specialize: 1 (default) lets the two reference scenes
+ * use their compile-time-dimension kernels, 0 forces the generic kernel.
+ * cotix_scene_variant reports what a launch uses: the tiling and the
+ * specialization id (0 generic, 1 RoboCup, 2 LunarLander). */
+int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specialize);
+int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec);
 
 /* Fused step, n_steps times, in place.
  *   dyn   device f32 [n_bodies][6][B]  (px, py, vx, vy, angle, angular_velocity)
@@ -209,8 +217,9 @@ typedef struct cotix_control {
  *   finished   device u32 [B] in/out (the carry's flag)
  *   reset_mode 0: none; 2: envs finished at entry restart from dyn_reset
  *              (err, finished cleared, resets[env]++, key chain continues) --
- *              next-step autoreset for env.step(); 1: restart on error bits
- *              after each env-step (cotix_step_autoreset; judge must be NULL)
+ *              next-step autoreset for env.step() (judge required: it is what
+ *              sets and clears `finished`); 1: restart on error bits after
+ *              each env-step (cotix_step_autoreset; judge must be NULL)
  *   obs        nullable device f32 [B][n_bodies][6]: the final observation,
  *              written by the same launch */
 int cotix_eval(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,

@@ -64,6 +64,15 @@ static __device__ unsigned long long g_sub_cycles[8];
 #define CXK_SUB_T1(k, lane) ((void)0)
 #endif
 
+// phase-cost experiments of the tooling build (-DCOTIX_TOOLING, KArgs::dbg_skip
+// from COTIX_DEBUG_SKIP) skip whole phases; the release library compiles every
+// skip out, so no environment variable can change what it computes
+#ifdef COTIX_TOOLING
+#define CXK_SKIP(a, bit) (((a).dbg_skip & (bit)) != 0)
+#else
+#define CXK_SKIP(a, bit) false
+#endif
+
 // Scene tables.  Everything the step reads per item is packed into hot[]
 // (word offsets below) and copied to LDS once per launch.
 // the scalar header (offsets, counts) travels in the kernel arguments, so
@@ -174,7 +183,9 @@ struct KArgs {
   int action_body;
   const float* dyn_reset;  // [nb][6][B] or null
   uint32_t* resets;        // [B] or null
-  int dbg_skip;            // timing only: skip phase T=1, B=2, C=4, D=8, A's key splits=16, E=32, GJK/EPA=64
+#ifdef COTIX_TOOLING
+  int dbg_skip;            // tooling builds only: skip phase T=1, B=2, C=4, D=8, A's key splits=16, E=32, GJK/EPA=64
+#endif
   // collider trace (cotix_step_ex; null = off): per step, body and env the
   // chosen partner j* (cotix/_colliders.py:274-295), and per cell (i, j) the
   // reference-scan candidate whose contact all_contacts[i, j] holds (:208-268)
@@ -758,7 +769,7 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
     for (int e = lane; e < EW; e += WAVE) {
-      if (!PRE && !(a.dbg_skip & 16)) {
+      if (!PRE && !CXK_SKIP(a, 16)) {
         key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
         key2 s = split_at(k, 2u, 0u);  // cotix/_colliders.py:142 == next driver key
         t.w(L.sk0, e) = s.a;
@@ -1110,7 +1121,7 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
       // GJK (+EPA); the contact point is deferred to phase F (wave-cooperative)
       const bool self = ((d0w >> 27) & 1u) != 0u;
       float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
-      const bool hit = (a.dbg_skip & 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
+      const bool hit = CXK_SKIP(a, 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
                        : (FNSET & FNS_AABB_POLY) == 0
                            ? convex_vs_polygon_pen_col<true>(A, Bs, d0, !self, &ct.pen, col, WAVE)
                            : convex_vs_polygon_pen_col<false>(A, Bs, d0, !self, &ct.pen, col, WAVE);
@@ -1568,7 +1579,7 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
   const bool self = ((d0w >> 27) & 1u) != 0u;
   float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
   Contact ct;
-  const bool hit = (a.dbg_skip & 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
+  const bool hit = CXK_SKIP(a, 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
                                      : gjk_epa_pair(S, h, na, nb, v2{sc.d0x, sc.d0y}, !self, &ct.pen, col);
   if (h != 0) return;
   ct.cp = v2{qnan(), qnan()};
@@ -2664,7 +2675,7 @@ enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH
 // L.sk0 where phase A splits the keys (backward re-play)
 template <int EW, int FNSET, bool PRE, class R>
 CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso) {
-  if (!(a.dbg_skip & 1)) {
+  if (!CXK_SKIP(a, 1)) {
     run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
     if (FNSET != FNS_ANALYTIC && c.sh.nvt > 0) {
       // the rebuild flags of TV0 and the chunks they make run, wave-uniform:
@@ -2686,7 +2697,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       });
       run(PH_TV2, [&](int l) { ph_TV2<EW>(a, c, t, env0, l, redo, runs); });
       run(PH_TV3, [&](int l) { ph_TV3<EW>(a, c, t, env0, l, redo, runs); });
-      if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !(a.dbg_skip & 2))
+      if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !CXK_SKIP(a, 2))
         run(PH_TV3, [&](int l) { ph_TV4<EW>(a, c, t, env0, l, redo, runs); });
 #if !defined(__HIP__)
       // host emulation (tests): the vertex items die with phase T -- poison
@@ -2697,7 +2708,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
 #endif
     }
   }
-  if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !(a.dbg_skip & 2)) {
+  if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !CXK_SKIP(a, 2)) {
     run(PH_BP0, [&](int l) { ph_BP0<EW>(a, c, t, env0, l); });
 #if !defined(__HIP__)  // (the GPU's BP0 compacts the list itself)
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_BP1, [&](int l) { ph_BP1<EW>(c, t, l, ch); });
@@ -2707,10 +2718,10 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     const bool pairs = b_pairs<FNSET>() && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the phase barrier
     const int per_round = pairs ? WAVE / 2 : WAVE;
     for (int r = 0; r * per_round < n; ++r) run(PH_B, [&](int l) { ph_BP2<EW, FNSET>(a, c, t, env0, l, r, pairs); });
-  } else if (!(a.dbg_skip & 2)) {
+  } else if (!CXK_SKIP(a, 2)) {
     run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
   }
-  if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && !(a.dbg_skip & 2)) {
+  if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && !CXK_SKIP(a, 2)) {
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_F0, [&](int l) { ph_F0<EW>(c, t, l, ch); });
     const int n = (int)t.ws[c.W.cf_n];
     CXK_STAT(f_items, n);
@@ -2726,7 +2737,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_F3, [&](int l) { ph_F3<EW>(c, t, l, b); });
     }
   }
-  if (!(a.dbg_skip & 4) && c.nl > 0 && c.nl * EW <= WAVE) {
+  if (!CXK_SKIP(a, 4) && c.nl > 0 && c.nl * EW <= WAVE) {
 #if defined(__HIP__)
     run(PH_C1, [&](int l) { ph_M_fused<EW>(a, c, t, env0, l, kso); });
 #else
@@ -2740,7 +2751,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_C2, [&](int l) { ph_M2<EW>(c, t, l, par); });
     }
 #endif
-  } else if (!(a.dbg_skip & 4) && c.nl > 0) {
+  } else if (!CXK_SKIP(a, 4) && c.nl > 0) {
     for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {
       run(PH_C0, [&](int l) { ph_C0<EW>(a, c, t, env0, l, ch); });
       run(PH_C0B, [&](int l) { ph_C0b<EW>(c, t, l, ch); });
@@ -2754,7 +2765,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_C3, [&](int l) { ph_C3<EW>(c, t, l, par); });
     }
   }
-  if (!(a.dbg_skip & 8)) run(PH_D, [&](int l) { ph_D<EW, PRE>(a, c, t, env0, l, slot); });
+  if (!CXK_SKIP(a, 8)) run(PH_D, [&](int l) { ph_D<EW, PRE>(a, c, t, env0, l, slot); });
 }
 
 // forward: n_steps fused steps; ROLL adds the trajectory save and the return
@@ -2772,7 +2783,7 @@ template <int EW, int FNSET, bool ROLL, bool EVAL = false, class R = void>
 CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, bool loaded = false) {
   static_assert(!(ROLL && EVAL), "the rollout has no judge");
   if (!loaded) run(PH_LOAD, [&](int l) { ph_load_fwd<EW, ROLL, EVAL>(a, c, t, env0, l); });
-  const bool keys = (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !(a.dbg_skip & 16);
+  const bool keys = (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !CXK_SKIP(a, 16);
   if (EVAL && a.judge.on) {  // the first NFE's start
     run(PH_J, [&](int l) { ph_JB<EW>(a, c, t, env0, l); });
     run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });
@@ -2796,7 +2807,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso);
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
-    if (!(a.dbg_skip & 32)) {
+    if (!CXK_SKIP(a, 32)) {
       run(PH_E1, [&](int l) { ph_E<EW>(a, c, t, env0, l, kso); });
       if (a.dyn_reset != nullptr && a.reset_mode == 1) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     }

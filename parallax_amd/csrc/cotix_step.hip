@@ -5,6 +5,7 @@
 // and in DESIGN.md).
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -39,7 +40,16 @@ struct cotix_scene {
   SceneDev* dev = nullptr;
   int n_candidates = 0;
   int fnset = 0;
+  // kernel variant (cotix_scene_set_variant): envs per wave and whether the
+  // reference scenes' specializations may be used -- every variant computes
+  // the same bits; the defaults are the measured best
+  int envs_per_wave = 4;
+  int specialize = 1;
 };
+// the specialization a launch of this scene uses (cxk::SPEC_*)
+static int scene_spec(const cotix_scene* scene) {
+  return scene->specialize ? cxk::spec_of(scene->host) : cxk::SPEC_GENERIC;
+}
 
 namespace {
 
@@ -215,6 +225,27 @@ int cotix_scene_destroy(cotix_scene* scene) {
   return 0;
 }
 
+int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specialize) {
+  if (!scene) return fail("null scene");
+  if (envs_per_wave == 0) envs_per_wave = 4;
+  if (envs_per_wave != 1 && envs_per_wave != 2 && envs_per_wave != 4 && envs_per_wave != 8)
+    return fail("envs_per_wave must be 0 (default), 1, 2, 4 or 8");
+#ifdef COTIX_EW4_ONLY
+  if (envs_per_wave != 4) return fail("this build carries the 4-envs-per-wave tiling only");
+#endif
+  scene->envs_per_wave = envs_per_wave;
+  scene->specialize = specialize ? 1 : 0;
+  return 0;
+}
+
+int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec) {
+  if (!scene) return fail("null scene");
+  if (envs_per_wave) *envs_per_wave = scene->envs_per_wave;
+  // the specialization is instantiated for the default tiling only
+  if (spec) *spec = scene->envs_per_wave == 4 ? scene_spec(scene) : cxk::SPEC_GENERIC;
+  return 0;
+}
+
 int cotix_scene_geom_floats(const cotix_scene* scene) { return scene ? scene->host.G : fail("null scene"); }
 
 int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, int* n_candidates, int* n_types) {
@@ -234,11 +265,6 @@ static int scene_upload(cotix_scene* sc) {
   return hip_check(hipMemcpy(sc->dev, &sc->host, sizeof(SceneDev), hipMemcpyHostToDevice), "hipMemcpy(scene)");
 }
 
-static int envs_per_wave() {
-  const char* v = getenv("COTIX_ENVS_PER_WAVE");
-  int e = v ? atoi(v) : 4;  // measured best for both scenarios (profiles/r01_sweep_*)
-  return (e == 1 || e == 2 || e == 4 || e == 8) ? e : 4;
-}
 
 static int check_step_args(const cotix_scene* scene, const float* dyn, const uint32_t* keys, const float* geom,
                            int geom_stride, int B, int n_steps, int stages, const float* action, int action_body) {
@@ -257,20 +283,20 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
 #ifdef COTIX_EW4_ONLY
   const int EW = 4;
 #else
-  const int EW = envs_per_wave();
+  const int EW = scene->envs_per_wave;
 #endif
   const size_t lds = cxk::lds_bytes(scene->host, cxl::WPB, EW);
   if (lds > 160 * 1024) return fail("scene too large for the LDS tile");
   cxk::KArgs ka = ka0;
   ka.sc = scene->dev;
   ka.sh = scene->host;  // the header by value (kernel arguments)
+#ifdef COTIX_TOOLING  // phase-cost experiments only (cotix_kernel.h CXK_SKIP)
   const char* dbg = getenv("COTIX_DEBUG_SKIP");
   ka.dbg_skip = dbg ? atoi(dbg) : 0;
+#endif
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int fs = scene->fnset;
-  // scene specialization (compile-time dimensions) unless COTIX_NO_SPEC is set
-  const char* ns = getenv("COTIX_NO_SPEC");
-  const int spec = (ns && atoi(ns)) ? cxk::SPEC_GENERIC : cxk::spec_of(scene->host);
+  const int spec = scene_spec(scene);  // scene specialization (compile-time dimensions)
   hipError_t e;
 #ifdef COTIX_EW4_ONLY  // tooling builds (phase profile, ISA markers): the default tiling only
   e = cxl::launch_step_ew4(ka, fs, mode, lds, st, spec);
@@ -317,12 +343,16 @@ int cotix_eval(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, co
                uint32_t* finished, int reset_mode, const float* dyn_reset, uint32_t* resets, float* obs,
                cotix_stream_t stream) {
   if (n_nfe < 0 || wfe < 0) return fail("negative size");
+  if (wfe > 0 && n_nfe > INT_MAX / wfe) return fail("n_nfe * wfe overflows");
   if (check_step_args(scene, dyn, keys, geom, geom_stride, B, n_nfe * wfe, stages, action, action_body)) return -1;
   if (!err) return fail("null argument");
   if (reset_mode < 0 || reset_mode > 2) return fail("reset_mode must be 0, 1 or 2");
   if (reset_mode != 0 && !dyn_reset) return fail("reset_mode needs dyn_reset");
   if (reset_mode == 1 && judge) return fail("reset_mode 1 (restart on error) cannot be combined with a judge");
   if (reset_mode == 2 && !finished) return fail("reset_mode 2 needs finished");
+  // reset_mode 2 restarts the envs the judge finished; without a judge nothing
+  // would clear `finished`, so every later call would restart them again
+  if (reset_mode == 2 && !judge) return fail("reset_mode 2 (restart finished envs) needs a judge");
   if (judge && (!reward || !finished)) return fail("a judge needs reward and finished");
   if (B == 0 || n_nfe == 0 || wfe == 0) return 0;
   cxk::KArgs ka{};

@@ -9,7 +9,7 @@ AbstractEnvironment.eval, cotix/_envs.py:37-132).
 With a device judge (parallax_amd.envs.LinearJudge) the step is an RL step:
 
   env = BatchedEnv(scen, judge=LinearJudge(...), autoreset=True)
-  obs, reward, done = env.step(action)    # action f32 [B, 2], held over n_steps
+  obs, reward, done = env.step(1, action=act)   # act f32 [B, 2], held over n_steps
 
 One launch (cotix_eval) advances every env, integrates the judge's reward
 rate, applies is_done / end_reward exactly as one NFE of the reference's eval
@@ -19,6 +19,7 @@ the previous call at the start of this one (next-step autoreset: the terminal
 observation is returned once, then the env restarts from its reset state with
 its key chain continuing).
 """
+import numbers
 from collections import namedtuple
 
 import torch
@@ -52,11 +53,13 @@ class BatchedEnv:
         self.reward.zero_()
         return self.observation()
 
-    def step(self, n_steps=1, action=None, action_body=None, trace=None, obs_out=None):
+    def step(self, n_steps=1, *, action=None, action_body=None, trace=None, obs_out=None, copy=False):
         """n_steps fused driver steps in ONE launch; returns the observation
         f32 [B, n_bodies, 6] (written by the step kernel itself), or with a
         judge StepResult(obs, reward, done).  obs / reward / done are buffers
-        of this env that the next step overwrites (clone what you keep).
+        of this env that the next step overwrites (no per-step allocation);
+        copy=True returns clones instead (for callers that keep them, e.g. a
+        trajectory list).
 
         action: f32 [B, 2] held over the n_steps, or [n_steps, B, 2] per step
         (no judge), added to the velocity of `action_body` (default: the last
@@ -67,13 +70,17 @@ class BatchedEnv:
         observation into instead of this env's buffer (e.g. an all-gather
         send buffer)."""
         w = self.world
+        if not isinstance(n_steps, numbers.Integral) or isinstance(n_steps, bool):
+            raise TypeError("n_steps must be an int (pass the action as action=...)")
+        if trace is not None and self.judge is not None:
+            raise ValueError("trace= is not available with a judge (the judge runs the cotix_eval program)")
         body = len(w.bodies) - 1 if action_body is None else action_body
         if self.judge is None and (trace is not None or (action is not None and action.dim() == 3)):
             if action is not None and action.dim() == 2:
                 action = action[None].expand(n_steps, -1, -1)
             kw = dict(dyn_reset=self.scenario.dyn_reset, resets=self.resets) if self.autoreset else {}
             w.step(n_steps, self.dt, self.scenario.stages, action=action, action_body=body, trace=trace, **kw)
-            return self.observation()
+            return self.observation()  # a fresh tensor
         if action is not None:
             action = action.to(w.device, torch.float32).contiguous()
         obs = self._obs
@@ -87,13 +94,15 @@ class BatchedEnv:
                          action_body=body, control=self._control_c, reset_mode=1 if self.autoreset else 0,
                          dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
                          resets=self.resets if self.autoreset else None, obs=obs)
-            return obs
+            return obs.clone() if copy else obs
         self.reward.zero_()
         w.eval_state(w.dyn, w.keys, w.err, 1, n_steps, self.dt, self.scenario.stages, judge=self._judge_c,
                      control=self._control_c, reward=self.reward, finished=self.done, action=action,
                      action_body=body, reset_mode=2 if self.autoreset else 0,
                      dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
                      resets=self.resets if self.autoreset else None, obs=obs)
+        if copy:
+            return StepResult(obs.clone(), self.reward.clone(), self.done.clone())
         return StepResult(obs, self.reward, self.done)
 
     def observation(self, out=None):

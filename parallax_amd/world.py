@@ -43,6 +43,22 @@ class Scene:
         _ffi.check(_ffi.lib.cotix_scene_info(self.handle, *[ctypes.byref(x) for x in v]), "cotix_scene_info")
         return dict(zip(("contacts", "cells", "candidates", "types"), [x.value for x in v]))
 
+    def set_variant(self, envs_per_wave=0, specialize=True):
+        """Kernel variant of this scene's launches: envs per wave (0 = the
+        default 4; 1, 2, 4, 8) and whether the reference scenes may use their
+        specialized kernels.  Every variant computes the same bits."""
+        _ffi.check(_ffi.lib.cotix_scene_set_variant(self.handle, int(envs_per_wave), 1 if specialize else 0),
+                   "cotix_scene_set_variant")
+
+    def variant(self):
+        """What a launch uses: {"envs_per_wave": EW, "specialization": 0
+        generic | 1 RoboCup | 2 LunarLander}."""
+        import ctypes
+        ew, sp = ctypes.c_int(), ctypes.c_int()
+        _ffi.check(_ffi.lib.cotix_scene_variant(self.handle, ctypes.byref(ew), ctypes.byref(sp)),
+                   "cotix_scene_variant")
+        return {"envs_per_wave": ew.value, "specialization": ["generic", "robocup", "lunar"][sp.value]}
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and _ffi is not None and _ffi.lib is not None:
@@ -123,6 +139,11 @@ class World:
     def _stages(self, stages):
         return stages
 
+    def set_variant(self, envs_per_wave=0, specialize=True):
+        """See Scene.set_variant (a tiling choice; results are identical)."""
+        self.scene.set_variant(envs_per_wave, specialize)
+        return self
+
     # -- state access -----------------------------------------------------
     def body(self, i):
         return BodyView(self, i)
@@ -193,11 +214,15 @@ class World:
         for t, shape in ((dyn, tuple(self.dyn.shape)), (keys, (self.B, 2)), (err, (self.B,))):
             if tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.dyn.device:
                 raise ValueError("state tensor shape/device/layout mismatch")
-        for t, shape in ((reward, (self.B,)), (finished, (self.B,)), (action, (self.B, 2)),
-                         (dyn_reset, tuple(self.dyn.shape)), (resets, (self.B,)),
-                         (obs, (self.B, len(self.bodies), 6))):
+        f32, i32 = torch.float32, torch.int32
+        for t, shape, dt_ in ((dyn, tuple(self.dyn.shape), f32), (keys, (self.B, 2), i32), (err, (self.B,), i32),
+                              (reward, (self.B,), f32), (finished, (self.B,), i32), (action, (self.B, 2), f32),
+                              (dyn_reset, tuple(self.dyn.shape), f32), (resets, (self.B,), i32),
+                              (obs, (self.B, len(self.bodies), 6), f32)):
             if t is not None and (tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.dyn.device):
                 raise ValueError("eval tensor shape/device/layout mismatch")
+            if t is not None and t.dtype != dt_:  # the kernel reads f32 / 32-bit words
+                raise ValueError("eval tensor dtype %s, expected %s" % (t.dtype, dt_))
         import ctypes
         _ffi.check(_ffi.lib.cotix_eval(
             self.scene.handle, _ffi.ptr(dyn), _ffi.ptr(keys), _ffi.ptr(err), _ffi.ptr(self.geom), self.geom_stride,

@@ -87,3 +87,79 @@ def test_product_path_does_not_import_oracle():
         for f in files:
             if f.endswith(".py"):
                 assert "cotix_oracle" not in open(os.path.join(dirpath, f)).read(), f
+
+
+def _robocup_world_cpu(B=4):
+    """A RoboCup World whose tensors live on the CPU: the host-side argument
+    checks below fail before anything is launched."""
+    import parallax_amd as pa
+    return pa.World(pa.scenarios.robocup_bodies(), B, "cpu", torch.zeros(B, 2, dtype=torch.int32))
+
+
+def test_release_library_has_no_debug_or_variant_env_knobs():
+    """The release library reads no environment variable that changes what a
+    launch computes or which kernel runs: phase skips exist only in the
+    tooling build (-DCOTIX_TOOLING), kernel variants are cotix_scene_set_variant."""
+    import parallax_amd as pa
+    blob = open(pa._ffi.LIB_PATH, "rb").read()
+    for name in (b"COTIX_DEBUG_SKIP", b"COTIX_ENVS_PER_WAVE", b"COTIX_NO_SPEC"):
+        assert name not in blob, name
+
+
+def test_scene_variant_api():
+    import parallax_amd as pa
+    s = pa.Scene(pa.scenarios.robocup_bodies())
+    assert s.variant() == {"envs_per_wave": 4, "specialization": "robocup"}
+    s.set_variant(4, False)
+    assert s.variant() == {"envs_per_wave": 4, "specialization": "generic"}
+    s.set_variant(2)
+    assert s.variant() == {"envs_per_wave": 2, "specialization": "generic"}  # specializations: 4-env tiling only
+    s.set_variant(0)
+    assert s.variant()["envs_per_wave"] == 4
+    with pytest.raises(RuntimeError, match="envs_per_wave"):
+        s.set_variant(3)
+
+
+def test_eval_rejects_reset_mode2_without_judge_and_overflow():
+    """cotix_eval: reset_mode 2 restarts the envs the judge finished, so it
+    needs a judge (else `finished` is never cleared); n_nfe * wfe must not
+    overflow int.  Both fail in the argument checks, before any launch."""
+    import ctypes
+    import parallax_amd as pa
+    lib = pa._ffi.lib
+    s = pa.Scene(pa.scenarios.robocup_bodies())
+    fake = ctypes.c_void_p(4096)  # never dereferenced: the checks fail first
+    rc = lib.cotix_eval(s.handle, fake, fake, fake, fake, 0, 8, 1, 4, 1e-2, pa._ffi.STAGES_ROBOCUP, None, None,
+                        None, 0, None, fake, 2, fake, None, None, None)
+    assert rc != 0 and b"needs a judge" in lib.cotix_last_error()
+    rc = lib.cotix_eval(s.handle, fake, fake, fake, fake, 0, 8, 1 << 16, 1 << 16, 1e-2, pa._ffi.STAGES_ROBOCUP,
+                        None, None, None, 0, None, None, 0, None, None, None, None)
+    assert rc != 0 and b"overflows" in lib.cotix_last_error()
+
+
+def test_eval_state_checks_dtypes():
+    w = _robocup_world_cpu()
+    bad = torch.zeros(w.B, dtype=torch.float64)
+    with pytest.raises(ValueError, match="dtype"):
+        w.eval_state(w.dyn, w.keys, w.err, 1, 1, 1e-2, 21, reward=bad)
+    with pytest.raises(ValueError, match="dtype"):
+        w.eval_state(w.dyn, w.keys, w.err, 1, 1, 1e-2, 21, finished=torch.zeros(w.B, dtype=torch.int64))
+    with pytest.raises(ValueError, match="dtype"):
+        w.eval_state(w.dyn, w.keys.to(torch.int64), w.err, 1, 1, 1e-2, 21)
+
+
+def test_env_step_argument_checks():
+    import parallax_amd as pa
+    from parallax_amd import envs as E
+
+    class Scen:
+        world = _robocup_world_cpu()
+        dyn_reset = world.dyn.clone()
+        stages = pa._ffi.STAGES_ROBOCUP
+
+    env = pa.BatchedEnv(Scen())
+    with pytest.raises(TypeError, match="n_steps"):
+        env.step(torch.zeros(4, 2))  # the action passed positionally
+    envj = pa.BatchedEnv(Scen(), judge=E.LinearJudge(rate_w={24: 1.0}))
+    with pytest.raises(ValueError, match="trace"):
+        envj.step(1, trace={})

@@ -828,14 +828,14 @@ def _subset_check(torch, make, big, stages, T, sizes):
 
 
 @pytest.mark.parametrize("ew", ["1", "2", "4", "8"])
-def test_ragged_batches_robocup(torch_cuda, monkeypatch, ew):
+def test_ragged_batches_robocup(torch_cuda, ew):
     torch = torch_cuda
-    monkeypatch.setenv("COTIX_ENVS_PER_WAVE", ew)  # read by the library at every launch
     import parallax_amd as pa
     env = pa.RoboCupEnv(batch=64, device="cuda", perturb=True)
+    env.world.set_variant(int(ew))
     keys = env.world.keys.clone()
-    _subset_check(torch, lambda b: pa.RoboCupEnv(batch=b, device="cuda", keys=keys[:b].clone()).world,
-                  env.world, env.stages, 8, [1, 3, 5, 13, 63])
+    _subset_check(torch, lambda b: pa.RoboCupEnv(batch=b, device="cuda", keys=keys[:b].clone()).world.set_variant(
+        int(ew)), env.world, env.stages, 8, [1, 3, 5, 13, 63])
 
 
 def test_ragged_batches_lunar(torch_cuda):
@@ -994,17 +994,17 @@ def test_regression_hipcc_support_p4xp6(torch_cuda):
 
 
 @pytest.mark.parametrize("ew", ["1", "2", "4", "8"])
-def test_regression_hipcc_mixed_kind_transform(torch_cuda, cport_lib, monkeypatch, ew):
+def test_regression_hipcc_mixed_kind_transform(torch_cuda, cport_lib, ew):
     """A divergent circle / AABB tail of the part transform (phase T) faulted
     (aperture violation: the circle lanes used an address only the AABB lanes
     had defined).  RoboCup's parts mix a circle with AABBs; every envs-per-
     wave tiling puts different kind mixes in one wave.  64 perturbed envs, 6
     fused steps with restarts, against the C port."""
     torch = torch_cuda
-    monkeypatch.setenv("COTIX_ENVS_PER_WAVE", ew)
     import parallax_amd as pa
     cport, lib = cport_lib
     env = pa.BatchedEnv(pa.RoboCupEnv(batch=64, device="cuda", perturb=True), autoreset=True)
+    env.world.set_variant(int(ew))
     env.reset()
     dyn = np.ascontiguousarray(env.world.dyn.cpu().numpy())
     keys = np.ascontiguousarray(env.world.keys.cpu().numpy().view(np.uint32))
@@ -1012,22 +1012,23 @@ def test_regression_hipcc_mixed_kind_transform(torch_cuda, cport_lib, monkeypatc
 
 
 @pytest.mark.parametrize("scene", ["robocup", "lunar"])
-def test_specialized_kernel_equals_generic(torch_cuda, monkeypatch, scene):
+def test_specialized_kernel_equals_generic(torch_cuda, scene):
     """The scene-specialized instantiations (compile-time dimensions of the
-    two reference scenes, cxk::SPEC_*) and the generic kernel (COTIX_NO_SPEC=1)
+    two reference scenes, cxk::SPEC_*) and the generic kernel (specialize=0)
     give bit-identical state, keys, error bits, restarts and collider traces."""
     torch = torch_cuda
     import parallax_amd as pa
     from cotix_oracle import prng
     outs = []
-    for nospec in ("0", "1"):
-        monkeypatch.setenv("COTIX_NO_SPEC", nospec)
+    for spec in (True, False):
         if scene == "robocup":
             env = pa.BatchedEnv(pa.RoboCupEnv(batch=1000, device="cuda", perturb=True), autoreset=True)
         else:
             tk = torch.tensor(u32_to_i32(prng.split(prng.PRNGKey(0), 1000)), device="cuda")
             env = pa.BatchedEnv(pa.LunarLander(key=tk, batch=1000, device="cuda"), autoreset=True)
             env.scenario.dyn_reset[:3, 1, ::2] -= 6.3  # half of the landers start on the ground
+        env.world.set_variant(4, spec)
+        assert env.world.scene.variant()["specialization"] == (scene if spec else "generic")
         env.reset()
         trc = {}
         env.step(24, trace=trc)
@@ -1063,7 +1064,7 @@ def _world_from_oracle(pa, torch, bodies, B, keys):
 
 
 @pytest.mark.parametrize("scene", ["aabb_poly", "aabb_circle_poly", "straddle", "straddle_ew1"])
-def test_generic_polygon_scenes_vs_cport(torch_cuda, cport_lib, monkeypatch, scene):
+def test_generic_polygon_scenes_vs_cport(torch_cuda, cport_lib, scene):
     """The generic step programs on the GPU (cxk::launch_fnset: polygon-only
     GJK/EPA for the straddling-part scene, AABB x polygon, circle x polygon)
     against the C port: 512 envs x 24 steps, state, keys, errors and every
@@ -1072,14 +1073,14 @@ def test_generic_polygon_scenes_vs_cport(torch_cuda, cport_lib, monkeypatch, sce
     torch = torch_cuda
     import parallax_amd as pa
     cport, lib = cport_lib
-    if scene == "straddle_ew1":
-        monkeypatch.setenv("COTIX_ENVS_PER_WAVE", "1")  # read by the library at every launch
     import scene_cases
     bodies = scene_cases.straddle_scene(4.0) if scene.startswith("straddle") else scene_cases.mixed_scene(
         scene == "aabb_circle_poly")
     B, T = 512, 24
     keys = np.ascontiguousarray(np.stack([np.arange(B) + 3, np.arange(B) * 5 + 1], 1).astype(np.uint32))
     w = _world_from_oracle(pa, torch, bodies, B, keys)
+    if scene == "straddle_ew1":
+        w.set_variant(1)
     base = np.array([b.dyn() for b in bodies], np.float32)
     dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
     dyn[0, 0, :] += np.linspace(-0.6, 0.6, B).astype(np.float32)

@@ -1,5 +1,5 @@
 """Config 1 (one LunarLander env, 10,000 driver steps in one launch) under
-the envs-per-wave tiling of COTIX_ENVS_PER_WAVE (perf tooling)."""
+the envs-per-wave tiling given as argv[1] (default 4; perf tooling)."""
 import json
 import os
 import sys
@@ -12,7 +12,9 @@ import parallax_amd as pa  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
+    ew = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     ll = pa.LunarLander(batch=1, device=dev)
+    ll.world.set_variant(ew)
     dyn0, keys0 = ll.world.dyn.clone(), ll.world.keys.clone()
     ts = []
     for _ in range(3):
@@ -25,7 +27,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
-    print(json.dumps({"ew": os.environ.get("COTIX_ENVS_PER_WAVE", "4"), "ms_per_10000": min(ts),
+    print(json.dumps({"ew": ew, "ms_per_10000": min(ts),
                       "env_steps_per_s": 10000 / (min(ts) * 1e-3),
                       "state_sum": float(torch.nan_to_num(ll.world.dyn).sum().item())}))
 

@@ -99,6 +99,42 @@ enum {
   COTIX_ERR_STATE_NONFINITE = 4  /* class_invariant, cotix/_design_by_contract.py:80-107: NaN/inf state */
 };
 
+/* jax.random threefry layouts (jax/_src/prng.py).  The reference
+ * pins no JAX version (pyproject.toml:16): JAX 0.4.x defaults to the legacy
+ * layout (jax_threefry_partitionable=False), JAX >= 0.5 to the partitionable
+ * one, so the collider's contact choices depend on which JAX runs it.
+ *   legacy:        split(k, n)[i] = words 2i, 2i+1 of threefry(k, iota(2n))
+ *                  split in halves; random_bits word m of a count-c draw from
+ *                  the halves of iota(c) (zero pad when c is odd)
+ *   partitionable: split(k, n)[i] = threefry(k, (0, i)); random_bits word m =
+ *                  y0 ^ y1 of threefry(k, (0, m)) */
+enum { COTIX_PRNG_LEGACY = 0, COTIX_PRNG_PARTITIONABLE = 1 };
+
+/* The reference's hard-coded constants on the hot path, as a scene parameter
+ * block (defaults = the reference's literals; cotix_params_default fills them):
+ *   prng_layout       COTIX_PRNG_LEGACY        every jax.random call of the step
+ *   baumgarte         0.3    cotix/_collision_resolution.py:105 (baumgarte_term)
+ *   baumgarte_dt      0.01   :115 (the divisor of the penetration term: "/ dt is missing")
+ *   contact_p         0.5    cotix/_colliders.py:220-223 (bernoulli p of a candidate's write)
+ *   gjk_max_steps     32     cotix/_collisions.py:101 (GJK while_loop max_steps), >= 0
+ *   epa_max_iters     48     cotix/_contacts.py:271,295 (the min(48, ...) cap of
+ *                            aabb_vs_polygon / polygon_vs_polygon), >= 3
+ *   epa_circle_iters  128    cotix/_contacts.py:162-163 (circle_vs_polygon), 3..128
+ *   epa_body_iters    48     cotix/_universal_shape.py:120 (penetration_depth), 3..128
+ * The GJK start direction random_direction(PRNGKey(1)) (cotix/_collisions.py:
+ * 287-298) follows prng_layout. */
+typedef struct cotix_params {
+  int prng_layout;
+  float baumgarte;
+  float baumgarte_dt;
+  float contact_p;
+  int gjk_max_steps;
+  int epa_max_iters;
+  int epa_circle_iters;
+  int epa_body_iters;
+} cotix_params;
+int cotix_params_default(cotix_params* out);
+
 /* Compile a scene (the collider's trace-time enumeration, cotix/_colliders.py:86-131).
  *   body_params [n_bodies][4] host: mass, inertia, elasticity, friction_coefficient
  *   part_body   [n_parts]  host: owning body (parts grouped by body, in shape order)
@@ -108,6 +144,12 @@ enum {
  * at trace time, cotix/_colliders.py:103-107). */
 int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,
                        const int* part_type, const int* part_nverts, cotix_scene** out);
+/* the same with a parameter block (NULL: the defaults); out-of-range fields
+ * are rejected here.  cotix_scene_params returns the scene's block. */
+int cotix_scene_create_ex(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                          const int* part_type, const int* part_nverts, const cotix_params* params,
+                          cotix_scene** out);
+int cotix_scene_params(const cotix_scene* scene, cotix_params* out);
 int cotix_scene_destroy(cotix_scene* scene);
 /* floats of local part geometry the scene expects per env (circle: r,cx,cy,0;
  * AABB: lo.x,lo.y,up.x,up.y; polygon: x,y per vertex), parts in order. */
@@ -315,6 +357,37 @@ int cotix_random_split(const uint32_t* keys, int n, int num, uint32_t* out, coti
 /* out [n][count] = jax.random.uniform(keys[i], (count,), lo, hi) (f32) */
 int cotix_random_uniform(const uint32_t* keys, int n, int count, float lo, float hi, float* out,
                          cotix_stream_t stream);
+/* The operators above with a parameter block (NULL: the defaults):
+ * cotix_contacts_ex  the polygon contacts' GJK steps / EPA iterations and the
+ *                    GJK start direction (prng_layout) of `params`
+ * cotix_resolve_ex   resolve_collision with its baumgarte / baumgarte_dt
+ * cotix_random_split_ex / cotix_random_uniform_ex  in layout COTIX_PRNG_* */
+int cotix_contacts_ex(int fn, int n, const float* a, const float* b, float* out, uint32_t* err,
+                      const cotix_params* params, cotix_stream_t stream);
+int cotix_resolve_ex(int n, float* dyn1, const float* par1, float* dyn2, const float* par2, const float* contact,
+                     const cotix_params* params, cotix_stream_t stream);
+int cotix_random_split_ex(const uint32_t* keys, int n, int num, int layout, uint32_t* out, cotix_stream_t stream);
+int cotix_random_uniform_ex(const uint32_t* keys, int n, int count, float lo, float hi, int layout, float* out,
+                            cotix_stream_t stream);
+
+/* GJK and EPA as operators (cotix/_collisions.py:277-329) over the shape rows
+ * of cotix_contacts (device f32 [n][18]: kind 0 circle / 1 AABB / 2 polygon,
+ * vertex count, geometry); the Minkowski difference is support(a, d) -
+ * support(b, -d) (minkowski_diff, cotix/_geometry_utils.py:49-57).
+ * cotix_gjk = check_for_collision_convex(a.get_support, b.get_support) with
+ *   its default start direction random_direction(PRNGKey(1)) (:287-298; the
+ *   layout and gjk_max_steps of `params`, NULL: defaults): hit device i32 [n];
+ *   simplex device f32 [n][3][2] -- NaN * simplex when there is no collision
+ *   (:300-310).
+ * cotix_epa = compute_penetration_vector_convex(a.get_support, b.get_support,
+ *   simplex, iters) (:313-329; _get_closest_minkowski_diff :115-273): simplex
+ *   device f32 [n][3][2], pen device f32 [n][2]; iters in 3..128 (the
+ *   reference's error_if rejects < 3, :130-135). */
+int cotix_gjk(int n, const float* a, const float* b, int32_t* hit, float* simplex, const cotix_params* params,
+              cotix_stream_t stream);
+int cotix_epa(int n, const float* a, const float* b, const float* simplex, int iters, float* pen,
+              cotix_stream_t stream);
+
 /* polygons xy device f32 [n][nverts][2] sorted in place (order_clockwise) */
 int cotix_order_clockwise(float* xy, int n, int nverts, cotix_stream_t stream);
 

@@ -27,6 +27,10 @@ def load():
     lib.oracle_step_ex.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                    ctypes.c_int, _P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int]
     lib.oracle_contacts.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P]
+    lib.oracle_contacts_ex.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P]
+    lib.oracle_scene_set_params.argtypes = [_P, _P]
+    lib.oracle_gjk.argtypes = [ctypes.c_int, _P, _P, _P, _P, _P]
+    lib.oracle_epa.argtypes = [ctypes.c_int, _P, _P, _P, ctypes.c_int, _P]
     lib.oracle_rollout.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                    ctypes.c_int, _P, ctypes.c_int, _P, _P, ctypes.c_int]
     return lib
@@ -36,11 +40,19 @@ def _p(a):
     return None if a is None else a.ctypes.data_as(_P)
 
 
-class Scene:
-    """Scene description + local geometry (row) from oracle Body objects."""
+def params_ref(params):
+    """An oracle Params (cotix_oracle.params) as a pointer to the C port's
+    OParams (the cotix_params layout), or NULL (the defaults)."""
+    return None if params is None else ctypes.cast(ctypes.pointer(params.c_struct()), _P)
 
-    def __init__(self, lib, bodies):
+
+class Scene:
+    """Scene description + local geometry (row) from oracle Body objects;
+    params: an oracle Params (None: the reference's literals)."""
+
+    def __init__(self, lib, bodies, params=None):
         self.lib = lib
+        prm = params
         params = np.array([[b.mass, b.inertia, b.elasticity, b.friction_coefficient] for b in bodies], np.float32)
         pb, pt, pn, geom = [], [], [], []
         for i, b in enumerate(bodies):
@@ -64,6 +76,9 @@ class Scene:
         rc = lib.oracle_scene_init(self.mem, len(bodies), _p(params), len(pb), *[_p(a) for a in args])
         if rc:
             raise RuntimeError("oracle_scene_init failed (%d)" % rc)
+        if prm is not None:
+            cp = prm.c_struct()
+            lib.oracle_scene_set_params(self.mem, ctypes.cast(ctypes.pointer(cp), _P))
 
     def step(self, dyn, keys, err, n_steps, stages, geom=None, dyn_reset=None, resets=None, nthreads=0, dt=1e-2):
         """dyn f32 [nb,6,B], keys u32 [B,2], err u32 [B] (in place); geom None

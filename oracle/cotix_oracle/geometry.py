@@ -20,6 +20,8 @@ implementation of this path:
 """
 import numpy as np
 
+from . import params as _params
+
 np.seterr(all="ignore")
 F = np.float32
 NAN = F(np.nan)
@@ -407,7 +409,7 @@ def gjk_simplex(a, b, d0):
         direction = vneg(direction)
     s2 = minkowski_diff(a, b, direction)
     steps = 0
-    while steps < GJK_MAX_STEPS:  # eqx while_loop(max_steps=32), :100-102
+    while steps < _params.current().gjk_max_steps:  # eqx while_loop(max_steps=32), :100-102
         c1 = dot(s2, direction) <= 0
         c2 = dot(fast_normal(vsub(s2, s0)), vneg(s2)) < 0
         c3 = dot(fast_normal(vsub(s1, s2)), vneg(s2)) < 0
@@ -603,7 +605,7 @@ def circle_vs_polygon(circle, polygon, d0, err=None):  # :157-202
     exists, simplex = check_for_collision_convex(circle, polygon, d0)
     if not exists:
         return NAN_CONTACT
-    pen = epa(circle, polygon, simplex, 128)
+    pen = epa(circle, polygon, simplex, _params.current().epa_circle_iters)
     disps = [_edge_point_displacement(e, circle.position) for e in polygon.edges()]
     dists = [sumsq(d) for d in disps]
     k = argmin(dists)
@@ -652,7 +654,7 @@ def contact_from_edges(edges_a, verts_a, in_a, edges_b, verts_b, in_b):  # :205-
 
 
 def aabb_vs_polygon(aabb, polygon, d0, err=None):  # :270-291
-    iters = min(48, 4 + len(polygon.vertices_) + 1)
+    iters = min(_params.current().epa_max_iters, 4 + len(polygon.vertices_) + 1)
     exists, simplex = check_for_collision_convex(aabb, polygon, d0)
     if not exists:
         return NAN_CONTACT
@@ -663,7 +665,7 @@ def aabb_vs_polygon(aabb, polygon, d0, err=None):  # :270-291
 
 
 def polygon_vs_polygon(pa, pb, d0, err=None):  # :294-315
-    iters = min(48, len(pa.vertices_) + len(pb.vertices_) + 1)
+    iters = min(_params.current().epa_max_iters, len(pa.vertices_) + len(pb.vertices_) + 1)
     exists, simplex = check_for_collision_convex(pa, pb, d0)
     if not exists:
         return NAN_CONTACT

@@ -23,6 +23,7 @@ import warnings
 import numpy as np
 import torch
 
+from . import params as _params
 from . import physics as P
 
 F32 = torch.float32
@@ -181,7 +182,8 @@ def resolve(b1, b2, pen, cp):
     lever1 = r1[0] * r1[0] + r1[1] * r1[1]
     lever2 = r2[0] * r2[0] + r2[1] * r2[1]
     ang = lever1 / b1.I + lever2 / b2.I
-    nim = (-(1.0 + e)) * vn - (_t(0.3) * _norm(pen)) / _t(0.01)
+    prm = _params.current()  # cotix/_collision_resolution.py:105,115
+    nim = (-(1.0 + e)) * vn - (_t(prm.baumgarte) * _norm(pen)) / _t(prm.baumgarte_dt)
     den = (1.0 / b1.m + 1.0 / b2.m) + ang
     ni = nim / den
     imp = (n[0] * ni, n[1] * ni)

@@ -22,6 +22,7 @@ import copy
 
 import numpy as np
 
+from . import params as _params
 from . import prng
 from .geometry import (AABB, CONTACT_FUNCS, clip, F, NAN, NAN_CONTACT, ONE, ZERO, Circle, ErrorFlag,
                        Polygon, Transformer, contact_isnan, cross, dot, fmin, norm, run_contact,
@@ -111,7 +112,8 @@ def resolve_collision(b1, b2, contact):
     lever1 = r1[0] * r1[0] + r1[1] * r1[1]
     lever2 = r2[0] * r2[0] + r2[1] * r2[1]
     ang = lever1 / b1.inertia + lever2 / b2.inertia
-    nim = (-(ONE + e)) * vn - (F(0.3) * norm(pen)) / F(0.01)
+    prm = _params.current()  # baumgarte_term 0.3 (:105) and the divisor 0.01 (:115)
+    nim = (-(ONE + e)) * vn - (F(prm.baumgarte) * norm(pen)) / F(prm.baumgarte_dt)
     den = (ONE / b1.mass + ONE / b2.mass) + ang
     ni = nim / den
     imp = vscale(n, ni)
@@ -195,7 +197,7 @@ def collider_resolve(bodies, rkey, d0, err=None, trace=None):
                 if contact_isnan(c):
                     continue  # bernoulli draw has no effect on a NaN candidate
                 k1 = prng.split(keys1[i1])[0]  # :222
-                if prng.bernoulli_half(k1):  # :223, :235-239
+                if prng.bernoulli(k1, _params.current().contact_p):  # :220-223, :235-239
                     bi, bj = l1[i1][0], l2[i2][0]
                     pen[bi][bj] = c[0]
                     cp[bi][bj] = c[1]

@@ -2,8 +2,15 @@
 
 Restatement of the third-party ``jax.random`` primitives the cotix hot path
 calls (jax/jaxlib >= 0.4.18, unpinned by the reference: ``pyproject.toml:16``).
-Layout: JAX's *legacy* (``jax_threefry_partitionable=False``) threefry layout,
-the default of the 0.4.x line the reference pins as its floor.
+Layouts: JAX's *legacy* (``jax_threefry_partitionable=False``) threefry
+layout, the default of the 0.4.x line the reference pins as its floor, and
+the *partitionable* one (the default from JAX 0.5), selected by the parameter
+block in force (params.current().prng_layout):
+  legacy         split(k, n) = threefry(k, iota(2n)) halves, reshaped (n, 2);
+                 random_bits(k, (m,)) from the halves of iota(m) (zero pad if odd)
+  partitionable  split(k, n)[i] = threefry(k, (0, i))  (_threefry_split_foldlike,
+                 iota_2x32_shape's (hi, lo) counter words); random_bits word i
+                 = y0 ^ y1 of threefry(k, (0, i))  (_threefry_random_bits_partitionable)
 
 Call sites in the reference:
   split            cotix/_colliders.py:142,175,254,264,295 ; examples/test_viz.py:39
@@ -18,6 +25,8 @@ tests/test_oracle_prng.py.  Everything else about jax.random here is a
 restatement of its published algorithm (jax/_src/prng.py, jax/_src/random.py).
 """
 import numpy as np
+
+from . import params as _params
 
 U32 = np.uint32
 _ROT = ((13, 15, 26, 6), (17, 29, 16, 24))
@@ -70,8 +79,16 @@ def _threefry_2x32_counts(key, counts):
     return out[:-1] if odd else out
 
 
+def _partitionable():
+    return _params.current().partitionable
+
+
 def split(key, num=2):
-    """jax.random.split(key, num), legacy layout: iota(2n) counters."""
+    """jax.random.split(key, num): legacy layout iota(2n) counters;
+    partitionable: key i = threefry(key, (0, i))."""
+    if _partitionable():
+        y0, y1 = threefry2x32(key, np.zeros(num, U32), np.arange(num, dtype=U32))
+        return np.stack([y0, y1], 1).astype(U32)
     out = _threefry_2x32_counts(key, np.arange(2 * num, dtype=U32))
     return out.reshape(num, 2)
 
@@ -79,7 +96,11 @@ def split(key, num=2):
 def split_at(key, num, idx):
     """Element ``idx`` of ``split(key, num)`` computed with two blocks only
     (what the device code does).  Key k = (flat[2k], flat[2k+1]) where flat
-    = y0 || y1 of blocks b < num with counter (b, num + b)."""
+    = y0 || y1 of blocks b < num with counter (b, num + b); partitionable:
+    the one block (0, idx)."""
+    if _partitionable():
+        y0, y1 = threefry2x32(key, np.array([0], U32), np.array([idx], U32))
+        return np.array([y0[0], y1[0]], dtype=U32)
     words = []
     for m in (2 * idx, 2 * idx + 1):
         if m < num:
@@ -93,8 +114,12 @@ def split_at(key, num, idx):
 
 
 def random_bits(key, shape):
-    """``jax.random.bits`` / ``_random_bits`` for 32-bit words, legacy layout."""
+    """``jax.random.bits`` / ``_random_bits`` for 32-bit words, in the layout
+    in force."""
     size = int(np.prod(shape)) if len(shape) else 1
+    if _partitionable():
+        y0, y1 = threefry2x32(key, np.zeros(size, U32), np.arange(size, dtype=U32))
+        return (y0 ^ y1).astype(U32).reshape(shape)
     return _threefry_2x32_counts(key, np.arange(size, dtype=U32)).reshape(shape)
 
 
@@ -119,6 +144,11 @@ def bernoulli_half(key):
     """jax.random.bernoulli(key, 0.5, ()) == uniform(key) < 0.5
     <=> the top bit of the single random word is 0."""
     return bool(uniform(key, ()) < np.float32(0.5))
+
+
+def bernoulli(key, p):
+    """jax.random.bernoulli(key, p, ()) == uniform(key) < p (p as f32)."""
+    return bool(uniform(key, ()) < np.float32(p))
 
 
 def cumsum_assoc(x):
@@ -193,7 +223,9 @@ def normal(key, shape):
 def gjk_initial_direction():
     """random_direction(PRNGKey(1)) (cotix/_geometry_utils.py:37-46 called from
     cotix/_collisions.py:287-298): x / ||x|| with x = normal(PRNGKey(1), (2,)).
-    Constant for every GJK call: (-0.05243401, 0.9986244) = (0xbd56c50b, 0x3f7fa5d9)."""
+    Constant for every GJK call: legacy layout (-0.05243401, 0.9986244) =
+    (0xbd56c50b, 0x3f7fa5d9); partitionable (-0.8767744, 0.4809021) =
+    (0xbf607449, 0x3ef638cd)."""
     x = normal(PRNGKey(1), (2,))
     n = np.sqrt(x[0] * x[0] + x[1] * x[1])
     return (np.float32(x[0] / n), np.float32(x[1] / n))

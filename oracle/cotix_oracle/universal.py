@@ -11,6 +11,7 @@ body's AABB as AABB.of (cotix/_convex_shapes.py:68-77) of its global support
 (get_global_support, :47-59) and the overlap test as the negation of
 aabb_vs_aabb's separation test (cotix/_contacts.py:62-65)."""
 from . import geometry as G
+from . import params as _params
 
 F = G.F
 NAN = G.NAN
@@ -37,7 +38,7 @@ def penetrates_with(body_a, body_b, d0):
             hit = hit or res
     if not hit:
         return False, (G.ZERO, G.ZERO)
-    return True, G.epa(first[0], first[1], simplex, 48)
+    return True, G.epa(first[0], first[1], simplex, _params.current().epa_body_iters)
 
 
 def body_aabb(body):

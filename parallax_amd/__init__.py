@@ -10,8 +10,10 @@ from .bodies import AnyBody, BodyView  # noqa: F401
 from .env import BatchedEnv, StepResult  # noqa: F401
 from .envs import (AbstractEnvironment, AffineControl, LinearJudge, PhysicsWorld, VelocityImpulse,  # noqa: F401
                    WorldState)
+from .params import Params  # noqa: F401
 from .physics import (ContactInfo, ExplicitEulerPhysics, RandomizedCollider, SimpleConstraintSolver,  # noqa: F401
-                      contact_funcs, resolve_collision, run_contacts)
+                      check_for_collision_convex, compute_penetration_vector_convex, contact_funcs,
+                      resolve_collision, run_contacts)
 from .rollout import rollout as differentiable_rollout  # noqa: F401
 from .rollout import rollout_backward, rollout_forward  # noqa: F401
 from .scenarios import BoxWorld, LunarLander, RoboCupEnv  # noqa: F401

@@ -41,7 +41,10 @@ class CotixControl(ctypes.Structure):
 
 
 SIGNATURES = {
+    "cotix_params_default": (_I, [_P]),
     "cotix_scene_create": (_I, [_I, _P, _I, _P, _P, _P, ctypes.POINTER(_P)]),
+    "cotix_scene_create_ex": (_I, [_I, _P, _I, _P, _P, _P, _P, ctypes.POINTER(_P)]),
+    "cotix_scene_params": (_I, [_P, _P]),
     "cotix_scene_destroy": (_I, [_P]),
     "cotix_scene_geom_floats": (_I, [_P]),
     "cotix_scene_info": (_I, [_P, _P, _P, _P, _P]),
@@ -60,10 +63,16 @@ SIGNATURES = {
     "cotix_collider_resolve": (_I, [_P, _P, _P, _P, _P, _I, _I, _P]),
     "cotix_lunar_constraints": (_I, [_P, _I, _P]),
     "cotix_contacts": (_I, [_I, _I, _P, _P, _P, _P, _P]),
+    "cotix_contacts_ex": (_I, [_I, _I, _P, _P, _P, _P, _P, _P]),
     "cotix_resolve": (_I, [_I, _P, _P, _P, _P, _P, _P]),
+    "cotix_resolve_ex": (_I, [_I, _P, _P, _P, _P, _P, _P, _P]),
+    "cotix_gjk": (_I, [_I, _P, _P, _P, _P, _P, _P]),
+    "cotix_epa": (_I, [_I, _P, _P, _P, _I, _P, _P]),
     "cotix_threefry2x32": (_I, [_P, _P, _P, _I, _P]),
     "cotix_random_split": (_I, [_P, _I, _I, _P, _P]),
+    "cotix_random_split_ex": (_I, [_P, _I, _I, _I, _P, _P]),
     "cotix_random_uniform": (_I, [_P, _I, _I, _F, _F, _P, _P]),
+    "cotix_random_uniform_ex": (_I, [_P, _I, _I, _F, _F, _I, _P, _P]),
     "cotix_order_clockwise": (_I, [_P, _I, _I, _P]),
     "cotix_observe": (_I, [_P, _I, _I, _P, _P]),
     "cotix_render_count": (_I, [_P]),

@@ -35,9 +35,9 @@ CX_DEV void body_frame(const float* dyn, int B, int body, int g, float* c, float
 
 // collides_with (GJK over every part pair, the first colliding pair's simplex
 // kept, :87-107), then penetrates_with / penetration_depth (EPA, 48
-// iterations, :112-132).  Returns collides; *pen = 0 when not colliding.
+// iterations by default -- cotix_params epa_body_iters --, :112-132).  Returns collides; *pen = 0 when not colliding.
 CX_DEV bool body_penetration_env(const float* dyn, int B, const float* geom, int gstride, const BodyParts& pa,
-                                 const BodyParts& pb, cx::v2 d0, int g, cx::v2* pen) {
+                                 const BodyParts& pb, const cx::NarrowParams& np, int g, cx::v2* pen) {
   const float* lg = geom + (gstride ? (size_t)g * gstride : (size_t)0);
   float ca, sa, xa, ya, cb, sb, xb, yb;
   body_frame(dyn, B, pa.body, g, &ca, &sa, &xa, &ya);
@@ -49,7 +49,7 @@ CX_DEV bool body_penetration_env(const float* dyn, int B, const float* geom, int
     for (int j = 0; j < pb.n; ++j) {
       const cx::WrappedShape A = wrapped_part(pa, i, lg, ca, sa, xa, ya), Bs = wrapped_part(pb, j, lg, cb, sb, xb, yb);
       cx::v2 sx[3];
-      const bool r = cx::gjk(A, Bs, d0, sx);
+      const bool r = cx::gjk(A, Bs, np.d0, sx, np.gjk_steps);
       if (!hit && r) {
         simplex[0] = sx[0];
         simplex[1] = sx[1];
@@ -62,7 +62,7 @@ CX_DEV bool body_penetration_env(const float* dyn, int B, const float* geom, int
   *pen = cx::v2{0.0f, 0.0f};
   if (hit) {
     const cx::WrappedShape A = wrapped_part(pa, fa, lg, ca, sa, xa, ya), Bs = wrapped_part(pb, fb, lg, cb, sb, xb, yb);
-    *pen = cx::epa_big(A, Bs, simplex, 48);
+    *pen = cx::epa_big(A, Bs, simplex, np.epa_body);  // solver_iterations=48, :120
   }
   return hit;
 }

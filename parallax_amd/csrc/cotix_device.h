@@ -185,6 +185,24 @@ CX_DEV float uniform1(key2 k, float lo, float hi) { return fmax_(lo, unit_float(
 // jax.random.bernoulli(key, 0.5, ()): top bit of the word is 0.
 CX_DEV bool bernoulli_half(key2 k) { return (bits1(k) >> 31) == 0u; }
 
+// The partitionable layout (jax_threefry_partitionable=True, the default from
+// JAX 0.5; include/cotix_amd.h COTIX_PRNG_*): _threefry_split_foldlike gives
+// split(key, n)[i] = threefry(key, (0, i)) -- the (hi, lo) words of
+// iota_2x32_shape -- and _threefry_random_bits_partitionable gives word m of a
+// 32-bit draw as y0 ^ y1 of threefry(key, (0, m)).  `part` is a scene
+// constant (wave-uniform branch).
+CX_DEV key2 split_at_l(key2 k, uint32_t num, uint32_t idx, bool part) {
+  if (part) return threefry(k, 0u, idx);
+  return split_at(k, num, idx);
+}
+// the single word of random_bits(key, ()) in either layout
+CX_DEV uint32_t bits1_l(key2 k, bool part) {
+  const key2 r = threefry(k, 0u, 0u);
+  return part ? (r.a ^ r.b) : r.a;
+}
+// jax.random.bernoulli(key, p, ()) = uniform(key) < p (p as f32)
+CX_DEV bool bernoulli_l(key2 k, float p, bool part) { return unit_float(bits1_l(k, part)) < p; }
+
 // jnp.cumsum via lax.associative_scan (CPU lowering), n <= 16.
 CX_DEV void cumsum_assoc(const float* in, int n, float* out) {
   float lv[5][16];
@@ -583,6 +601,27 @@ CX_DEV Contact circle_vs_aabb(const Shape& a, const Shape& b, uint32_t* err) {
 }
 
 // ---------------------------------------------------------------------------
+// narrow-phase parameters (cotix_params): the GJK start direction
+// random_direction(PRNGKey(1)) of the scene's PRNG layout
+// (cotix/_collisions.py:287-298), GJK steps (:101), the EPA iteration cap of
+// the polygon contacts (cotix/_contacts.py:271,295), circle x polygon's EPA
+// iterations (:162-163) and the body-level penetration_depth's
+// (cotix/_universal_shape.py:120)
+// ---------------------------------------------------------------------------
+struct NarrowParams {
+  v2 d0;
+  int gjk_steps, epa_cap, epa_cp, epa_body;
+};
+// random_direction(PRNGKey(1)) = normal(PRNGKey(1), (2,)) / norm: legacy
+// (0xbd56c50b, 0x3f7fa5d9), partitionable (0xbf607449, 0x3ef638cd)
+// (oracle/cotix_oracle/prng.py gjk_initial_direction, XLA's f32 ErfInv)
+CX_HD v2 gjk_d0(bool part) {
+  return part ? v2{__builtin_bit_cast(float, 0xbf607449u), __builtin_bit_cast(float, 0x3ef638cdu)}
+              : v2{__builtin_bit_cast(float, 0xbd56c50bu), __builtin_bit_cast(float, 0x3f7fa5d9u)};
+}
+CX_HD NarrowParams narrow_default() { return NarrowParams{gjk_d0(false), 32, 48, 128, 48}; }
+
+// ---------------------------------------------------------------------------
 // GJK (cotix/_collisions.py:20-112, 277-310)
 // ---------------------------------------------------------------------------
 CX_DEV bool point_in_triangle0(v2 v1, v2 v2_, v2 v3) {  // _geometry_utils.py:12-27, pt = 0
@@ -595,7 +634,7 @@ CX_DEV bool point_in_triangle0(v2 v1, v2 v2_, v2 v3) {  // _geometry_utils.py:12
 }
 
 template <class SA, class SB>
-CX_DEV bool gjk(const SA& a, const SB& b, v2 d0, v2* simplex) {
+CX_DEV bool gjk(const SA& a, const SB& b, v2 d0, v2* simplex, int max_steps = 32) {
   v2 s0 = minkowski(a, b, d0);
   v2 s1 = minkowski(a, b, neg(s0));
   v2 dir = fnormal(sub(s1, s0));
@@ -607,7 +646,7 @@ CX_DEV bool gjk(const SA& a, const SB& b, v2 d0, v2* simplex) {
     dir = sw ? dir : neg(dir);
   }
   v2 s2 = minkowski(a, b, dir);
-  for (int step = 0; step < 32; ++step) {
+  for (int step = 0; step < max_steps; ++step) {  // while_loop(max_steps=32), :101
     bool c1 = dot(s2, dir) <= 0.0f;
     bool c2 = dot(fnormal(sub(s2, s0)), neg(s2)) < 0.0f;
     bool c3 = dot(fnormal(sub(s1, s2)), neg(s2)) < 0.0f;
@@ -796,7 +835,7 @@ CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters) {
 // private memory.  Not on either scenario's path.
 template <class SA, class SB>
 CX_DEV v2 epa_big(const SA& a, const SB& b, const v2* simplex, int iters) {
-  constexpr int NE = 131;
+  constexpr int NE = 131;  // iters <= 128 (cotix_params bounds)
   v2 e0[NE], e1[NE];
   float dist[NE];
   const int ne = iters + 3;
@@ -939,8 +978,8 @@ static __device__ unsigned long long g_dev_sub[4];  // phase-timing build: GJK /
 #define CX_DSUB_ADD(k, t0) ((void)(t0))
 #endif
 template <class SA, class SB, class MakeStore>
-CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen,
-                      MakeStore make) {
+CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen,
+                      v2* pen, MakeStore make) {
   static_assert(2 * MAXV + 1 + 3 <= 20, "EPA buffer bound");
   v2 simplex[3];
   *pen = v2{0.0f, 0.0f};
@@ -948,13 +987,14 @@ CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, 
   asm volatile(";#GJK_BEGIN");
 #endif
   CX_DSUB_T0;
-  const bool hit = gjk(a, b, d0, simplex);
+  const bool hit = gjk(a, b, np.d0, simplex, np.gjk_steps);
   CX_DSUB_T1(0);
 #if defined(COTIX_ASM_MARKERS) && (defined(__HIP__) || defined(__HIPCC__))
   asm volatile(";#GJK_END");
 #endif
   if (!hit) return false;
-  const int iters = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
+  const int it0 = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);  // min(48, ...): :271, :295
+  const int iters = it0 < np.epa_cap ? it0 : np.epa_cap;
   if (!need_pen) return true;
   [[maybe_unused]] const unsigned long long cx_epa_t0 = CX_CLOCK();
   struct EpaTimer {  // phase-timing build: EPA cycles into slot 1 at scope exit
@@ -972,9 +1012,9 @@ CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, 
 }
 // POLY: both shapes are polygons (supports without the kind dispatch)
 template <bool POLY, class MakeStore>
-CX_DEV bool gjk_epa(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen, MakeStore make) {
-  if constexpr (POLY) return gjk_epa_t(PolyRef{A}, PolyRef{B}, A, B, d0, need_pen, pen, make);
-  else return gjk_epa_t(A, B, A, B, d0, need_pen, pen, make);
+CX_DEV bool gjk_epa(const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen, v2* pen, MakeStore make) {
+  if constexpr (POLY) return gjk_epa_t(PolyRef{A}, PolyRef{B}, A, B, np, need_pen, pen, make);
+  else return gjk_epa_t(A, B, A, B, np, need_pen, pen, make);
 }
 struct MakeRegs {
   template <int NE>
@@ -987,19 +1027,19 @@ struct MakeCol {
   CX_MF EdgeCol get() const { return EdgeCol{p, st}; }
 };
 // GJK, then EPA when the penetration is needed; EPA edges in registers
-CX_DEV bool convex_vs_polygon_pen(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen) {
-  return gjk_epa<false>(A, B, d0, need_pen, pen, MakeRegs{});
+CX_DEV bool convex_vs_polygon_pen(const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen, v2* pen) {
+  return gjk_epa<false>(A, B, np, need_pen, pen, MakeRegs{});
 }
 // the same with EPA edges in a per-lane memory column (the step kernel's LDS)
 // (POLY: both shapes are polygons)
 template <bool POLY>
-CX_DEV bool convex_vs_polygon_pen_col(const Shape& A, const Shape& B, v2 d0, bool need_pen, v2* pen, float* col,
-                                      int stride) {
-  return gjk_epa<POLY>(A, B, d0, need_pen, pen, MakeCol{col, stride});
+CX_DEV bool convex_vs_polygon_pen_col(const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen, v2* pen,
+                                      float* col, int stride) {
+  return gjk_epa<POLY>(A, B, np, need_pen, pen, MakeCol{col, stride});
 }
-CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, v2 d0, bool need_pen = true) {
+CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen = true) {
   Contact c;
-  if (!convex_vs_polygon_pen(A, B, d0, need_pen, &c.pen)) return nan_contact();
+  if (!convex_vs_polygon_pen(A, B, np, need_pen, &c.pen)) return nan_contact();
   c.cp = contact_from_edges(A, B);
   return c;
 }
@@ -1060,11 +1100,11 @@ CX_DEV v2 cfe_term(const Shape& A, const Shape& B, int s, VFA va, VFB vb) {
 }
 
 // circle_vs_polygon :157-202
-CX_DEV Contact circle_vs_polygon(const Shape& C, const Shape& P, v2 d0) {
+CX_DEV Contact circle_vs_polygon(const Shape& C, const Shape& P, const NarrowParams& np) {
   v2 simplex[3];
-  if (!gjk(C, P, d0, simplex)) return nan_contact();
+  if (!gjk(C, P, np.d0, simplex, np.gjk_steps)) return nan_contact();
   Contact c;
-  c.pen = epa_big(C, P, simplex, 128);
+  c.pen = epa_big(C, P, simplex, np.epa_cp);
   v2 pos = v2{C.d(1), C.d(2)};
   float dists[MAXV];
   v2 disps[MAXV];
@@ -1106,14 +1146,14 @@ enum : int {
   FN_AABB_POLY = 4,
   FN_CIRCLE_POLY = 5,
 };
-CX_DEV Contact run_contact(int fn, const Shape& a, const Shape& b, v2 d0, uint32_t* err) {
+CX_DEV Contact run_contact(int fn, const Shape& a, const Shape& b, const NarrowParams& np, uint32_t* err) {
   switch (fn) {
     case FN_AABB_AABB: return aabb_vs_aabb(a, b);
     case FN_CIRCLE_CIRCLE: return circle_vs_circle(a, b);
     case FN_CIRCLE_AABB: return circle_vs_aabb(a, b, err);
     case FN_POLY_POLY:
-    case FN_AABB_POLY: return convex_vs_polygon(a, b, d0);
-    default: return circle_vs_polygon(a, b, d0);
+    case FN_AABB_POLY: return convex_vs_polygon(a, b, np);
+    default: return circle_vs_polygon(a, b, np);
   }
 }
 
@@ -1161,9 +1201,15 @@ struct ResPre {
   v2 n, r1, r2, pen;  // pen / |pen|; cp - p1; cp - p2 (== velocity_at / apply_impulse arms); pen
   float den, pterm, ne, mu;  // (1/m1 + 1/m2) + ang; (0.3 |pen|) / 0.01; -(1 + e); (mu1 + mu2) / 2
 };
+// the penetration term's constants (baumgarte_term 0.3 and the divisor 0.01,
+// cotix/_collision_resolution.py:105,115; cotix_params)
+struct Baum {
+  float k, dt;
+};
+CX_HD Baum baum_default() { return Baum{0.3f, 0.01f}; }
 template <bool RCP = false>
 CX_DEV ResPre resolve_pre(const Dyn& b1, const Params& m1, Rcp q1, const Dyn& b2, const Params& m2, Rcp q2, v2 pen,
-                          v2 cp) {
+                          v2 cp, Baum bm = baum_default()) {
   ResPre p;
   const float pn = nrm(pen);
   p.n = v2{pen.x / pn, pen.y / pn};
@@ -1173,7 +1219,7 @@ CX_DEV ResPre resolve_pre(const Dyn& b1, const Params& m1, Rcp q1, const Dyn& b2
   const float lev1 = p.r1.x * p.r1.x + p.r1.y * p.r1.y, lev2 = p.r2.x * p.r2.x + p.r2.y * p.r2.y;
   const float ang = div_r<RCP>(lev1, m1.inertia, q1.i) + div_r<RCP>(lev2, m2.inertia, q2.i);
   p.den = (div_r<RCP>(1.0f, m1.mass, q1.m) + div_r<RCP>(1.0f, m2.mass, q2.m)) + ang;
-  p.pterm = (0.3f * nrm(pen)) / 0.01f;
+  p.pterm = (bm.k * nrm(pen)) / bm.dt;
   p.ne = -(1.0f + e);
   p.mu = (m1.fric + m2.fric) / 2.0f;
   p.pen = pen;
@@ -1211,9 +1257,10 @@ CX_DEV bool resolve_seq(float& vx1, float& vy1, float& w1, const Params& m1, Rcp
   w2 = w2 + div_r<RCP>(t2, m2.inertia, q2.i);
   return true;
 }
-CX_DEV bool resolve_collision(Dyn& b1, const Params& m1, Dyn& b2, const Params& m2, v2 pen, v2 cp) {  // :52-151
+CX_DEV bool resolve_collision(Dyn& b1, const Params& m1, Dyn& b2, const Params& m2, v2 pen, v2 cp,
+                             Baum bm = baum_default()) {  // :52-151
   if (vnan(cp)) return false;
-  const ResPre p = resolve_pre(b1, m1, no_rcp(), b2, m2, no_rcp(), pen, cp);
+  const ResPre p = resolve_pre(b1, m1, no_rcp(), b2, m2, no_rcp(), pen, cp, bm);
   return resolve_seq(b1.vx, b1.vy, b1.w, m1, no_rcp(), b2.vx, b2.vy, b2.w, m2, no_rcp(), p);
 }
 CX_DEV v2 rotate(v2 v, float ang) {  // _geometry_utils.py:81-88

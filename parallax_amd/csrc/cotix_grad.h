@@ -175,7 +175,7 @@ CX_DEV void contact_vjp(int fn, const Shape& a, const Shape& b, v2 gpen, v2 gcp,
 // cotangents g1/g2 of the post-resolution bodies.  Out: g1/g2 become the
 // cotangents of the pre-resolution bodies; gpen/gcp those of the contact.
 CX_DEV void resolve_vjp(const Dyn& b1, const Params& m1, const Dyn& b2, const Params& m2, v2 pen, v2 cp, Dyn& g1,
-                        Dyn& g2, v2& gpen, v2& gcp) {
+                        Dyn& g2, v2& gpen, v2& gcp, Baum bm = baum_default()) {
   // forward values (cotix_device.h resolve_collision)
   const v2 r1 = sub(cp, v2{b1.px, b1.py}), r2 = sub(cp, v2{b2.px, b2.py});
   const v2 v1 = velocity_at(b1, cp), v2_ = velocity_at(b2, cp);
@@ -186,7 +186,7 @@ CX_DEV void resolve_vjp(const Dyn& b1, const Params& m1, const Dyn& b2, const Pa
   const float e = fmin_(m1.elast, m2.elast);
   const float lev1 = r1.x * r1.x + r1.y * r1.y, lev2 = r2.x * r2.x + r2.y * r2.y;
   const float ang = lev1 / m1.inertia + lev2 / m2.inertia;
-  const float nim = (-(1.0f + e)) * vn - (0.3f * nrm(pen)) / 0.01f;
+  const float nim = (-(1.0f + e)) * vn - (bm.k * nrm(pen)) / bm.dt;
   const float den = (1.0f / m1.mass + 1.0f / m2.mass) + ang;
   const float ni = nim / den;
   const float mu = (m1.fric + m2.fric) / 2.0f;
@@ -233,9 +233,9 @@ CX_DEV void resolve_vjp(const Dyn& b1, const Params& m1, const Dyn& b2, const Pa
   gden += -gni * nim / (den * den);
   gr1 = add(gr1, scl(r1, 2.0f * (gden / m1.inertia)));
   gr2 = add(gr2, scl(r2, 2.0f * (gden / m2.inertia)));
-  // nim = -(1 + e) * vn - 0.3 * |pen| / 0.01
+  // nim = -(1 + e) * vn - k * |pen| / dt
   gvn += -(1.0f + e) * gnim;
-  float gpn = -(0.3f / 0.01f) * gnim;
+  float gpn = -(bm.k / bm.dt) * gnim;
   // vn = relv . n
   grelv = add(grelv, scl(n, gvn));
   gn = add(gn, scl(relv, gvn));

@@ -97,7 +97,16 @@ struct SceneHdr {
   uint32_t rcp_mask; // bit b: body b's mass and inertia have exact reciprocals (bodies < 32)
   uint16_t maxv;     // the most vertices of any polygon part (0: none) -- bounds the broadphase guard's loops
   uint16_t pminv;    // max over polygon pairs of the smaller edge count (AABB: 2) -- the guard's outer loop
+  // cotix_params (include/cotix_amd.h): PRNG layout (1: partitionable), GJK
+  // steps, EPA iteration cap / circle x polygon / body-level iterations,
+  // Baumgarte factor and divisor, the candidates' bernoulli p
+  uint16_t prng, gjk_steps, epa_cap, epa_cp, epa_body;
+  float baum, baum_dt, pc;
 };
+CX_HD cx::NarrowParams narrow_of(const SceneHdr& h) {
+  return cx::NarrowParams{cx::v2{h.d0x, h.d0y}, (int)h.gjk_steps, (int)h.epa_cap, (int)h.epa_cp, (int)h.epa_body};
+}
+CX_HD cx::Baum baum_of(const SceneHdr& h) { return cx::Baum{h.baum, h.baum_dt}; }
 struct SceneDev : SceneHdr {
   uint32_t hot[MAXHOT];
 };
@@ -383,8 +392,8 @@ CX_HD int launch_fnset(int fs, int mode) {
   return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
 }
 template <int FNSET>
-CX_DEV cx::Contact run_contact_set(int fn, const cx::Shape& a, const cx::Shape& b, cx::v2 d0, uint32_t* err,
-                                   bool self_pair) {
+CX_DEV cx::Contact run_contact_set(int fn, const cx::Shape& a, const cx::Shape& b, const cx::NarrowParams& np,
+                                   uint32_t* err, bool self_pair) {
   using namespace cx;
   if ((FNSET & FNS_ANALYTIC) != 0) {
     if (fn == FN_AABB_AABB) return aabb_vs_aabb(a, b);
@@ -392,10 +401,10 @@ CX_DEV cx::Contact run_contact_set(int fn, const cx::Shape& a, const cx::Shape& 
     if (fn == FN_CIRCLE_CIRCLE) return circle_vs_circle(a, b);
   }
   if ((FNSET & FNS_CONVEX) != 0) {
-    if (fn == FN_POLY_POLY || fn == FN_AABB_POLY) return convex_vs_polygon(a, b, d0, !self_pair);
+    if (fn == FN_POLY_POLY || fn == FN_AABB_POLY) return convex_vs_polygon(a, b, np, !self_pair);
   }
   if ((FNSET & FNS_CIRCLE_POLY) != 0) {
-    if (fn == FN_CIRCLE_POLY) return circle_vs_polygon(a, b, d0);
+    if (fn == FN_CIRCLE_POLY) return circle_vs_polygon(a, b, np);
   }
   return nan_contact();
 }
@@ -595,7 +604,10 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
 // move -- half the threefry issue of split_at on the chain's critical path.
 // The host emulation runs lanes one by one, so it takes split_at (the same
 // words).
-CX_DEV cx::key2 split_at_pair(cx::key2 k, uint32_t num, uint32_t idx, int h) {
+// The partitionable layout's split is ONE block (both words), which each
+// lane of the pair runs itself (no exchange).
+CX_DEV cx::key2 split_at_pair(cx::key2 k, uint32_t num, uint32_t idx, int h, bool part) {
+  if (part) return cx::threefry(k, 0u, idx);
 #if defined(__HIP__)
   const uint32_t mine = cx::split_word(k, num, 2u * idx + (uint32_t)h);
   const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp((int)mine, (int)mine, 0xB1, 0xF, 0xF, false);
@@ -620,7 +632,7 @@ CX_DEV void ph_K0(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int n) {
     const int e = w >> 1, h = w & 1;
     key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
     for (int s = 0; s < n; ++s) {
-      const key2 s0 = split_at_pair(k, 2u, 0u, h);
+      const key2 s0 = split_at_pair(k, 2u, 0u, h, c.sh.prng != 0);
       if (h == 0) {
         t.w(L.kw + s * L.kww, e) = s0.a;
         t.w(L.kw + s * L.kww + 1, e) = s0.b;
@@ -638,7 +650,7 @@ CX_DEV void ph_K1(const Ctx& c, Tile<EW> t, int lane, int n) {
     const int e = w % EW, o = L.kw + (w / EW) * L.kww;
     key2 k = key2{t.w(o, e), t.w(o + 1, e)};
     for (int q = 0; q < c.nt; ++q) {
-      k = split_at(k, 2u, 0u);
+      k = split_at_l(k, 2u, 0u, c.sh.prng != 0);
       t.w(o + 2 + 2 * q, e) = k.a;
       t.w(o + 3 + 2 * q, e) = k.b;
     }
@@ -654,8 +666,9 @@ CX_DEV void ph_K2(const Ctx& c, Tile<EW> t, int lane, int n) {
   for (int w = lane; w < n * nb * EW; w += WAVE) {
     const int e = w % EW, i = (w / EW) % nb, o = L.kw + (w / EW / nb) * L.kww;
     const int so = c.nt > 0 ? o + 2 + 2 * (c.nt - 1) : o;
-    const key2 ck = split_at(key2{t.w(so, e), t.w(so + 1, e)}, (uint32_t)nb, (uint32_t)i);
-    t.f(o + 2 + 2 * c.nt + i, e) = unit_float(bits1(ck));
+    const bool part = c.sh.prng != 0;
+    const key2 ck = split_at_l(key2{t.w(so, e), t.w(so + 1, e)}, (uint32_t)nb, (uint32_t)i, part);
+    t.f(o + 2 + 2 * c.nt + i, e) = unit_float(bits1_l(ck, part));
   }
 }
 
@@ -673,20 +686,21 @@ CX_DEV void ph_K_one(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) {
   for (int w = lane; w < 2 * (coll ? nb : 1) * EW; w += WAVE) {
     const int p = w >> 1, h = w & 1, e = p % EW, i = p / EW, o = L.kw;
     const bool wr = i == 0 && h == 0;
-    key2 k = split_at_pair(key2{t.w(L.key, e), t.w(L.key + 1, e)}, 2u, 0u, h);  // K0
+    const bool part = c.sh.prng != 0;
+    key2 k = split_at_pair(key2{t.w(L.key, e), t.w(L.key + 1, e)}, 2u, 0u, h, part);  // K0
     if (wr) {
       t.w(o, e) = k.a;
       t.w(o + 1, e) = k.b;
     }
     for (int q = 0; q < c.nt; ++q) {  // K1
-      k = split_at_pair(k, 2u, 0u, h);
+      k = split_at_pair(k, 2u, 0u, h, part);
       if (wr) {
         t.w(o + 2 + 2 * q, e) = k.a;
         t.w(o + 3 + 2 * q, e) = k.b;
       }
     }
     if (coll) {  // K2
-      const float u = unit_float(bits1(split_at_pair(k, (uint32_t)nb, (uint32_t)i, h)));
+      const float u = unit_float(bits1_l(split_at_pair(k, (uint32_t)nb, (uint32_t)i, h, part), part));
       if (h == 0) t.f(o + 2 + 2 * c.nt + i, e) = u;
     }
   }
@@ -770,12 +784,13 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
     for (int e = lane; e < EW; e += WAVE) {
       if (!PRE && !CXK_SKIP(a, 16)) {
+        const bool part = c.sh.prng != 0;
         key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
-        key2 s = split_at(k, 2u, 0u);  // cotix/_colliders.py:142 == next driver key
+        key2 s = split_at_l(k, 2u, 0u, part);  // cotix/_colliders.py:142 == next driver key
         t.w(L.sk0, e) = s.a;
         t.w(L.sk0 + 1, e) = s.b;
         for (int q = 0; q < c.nt; ++q) {  // :175, one split per type key
-          s = split_at(s, 2u, 0u);
+          s = split_at_l(s, 2u, 0u, part);
           t.w(L.skt + 2 * q, e) = s.a;
           t.w(L.skt + 2 * q + 1, e) = s.b;
         }
@@ -1094,7 +1109,7 @@ template <int EW, int FNSET>
 CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int w) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
-  const v2 d0 = v2{sc.d0x, sc.d0y};
+  const NarrowParams np = narrow_of(sc);
   {
     int e = w % EW, ci = w / EW, g = env0 + e;
     if (g >= a.B) return;
@@ -1123,8 +1138,8 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
       float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
       const bool hit = CXK_SKIP(a, 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
                        : (FNSET & FNS_AABB_POLY) == 0
-                           ? convex_vs_polygon_pen_col<true>(A, Bs, d0, !self, &ct.pen, col, WAVE)
-                           : convex_vs_polygon_pen_col<false>(A, Bs, d0, !self, &ct.pen, col, WAVE);
+                           ? convex_vs_polygon_pen_col<true>(A, Bs, np, !self, &ct.pen, col, WAVE)
+                           : convex_vs_polygon_pen_col<false>(A, Bs, np, !self, &ct.pen, col, WAVE);
       ct.cp = v2{qnan(), qnan()};
       // a part paired with itself: only the NaN-ness of its contact point is
       // observable (such a cell is only ever chosen as j == i, which
@@ -1134,7 +1149,7 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
       else if (hit) t.ws[c.W.cf_flag + w] = 1u;
       if (hit && !self) t.ws[c.W.bl_epa] = 1u;  // an EPA ran (B-list scheduling of the next step)
     } else {
-      ct = run_contact_set<FNSET>(fn, A, Bs, d0, &er, ((d0w >> 27) & 1u) != 0u);
+      ct = run_contact_set<FNSET>(fn, A, Bs, np, &er, ((d0w >> 27) & 1u) != 0u);
     }
     const int co = c.L.con + 4 * ci;
     t.f(co + 0, e) = ct.pen.x;
@@ -1200,7 +1215,7 @@ CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, in
         Bs.w[k] = k < 4 ? gb[q][k] : 0.0f;
       }
       uint32_t er = 0u;
-      const Contact ct = run_contact_set<FNS_ANALYTIC>((int)((dw[q] >> 20) & 7u), A, Bs, v2{sc.d0x, sc.d0y}, &er,
+      const Contact ct = run_contact_set<FNS_ANALYTIC>((int)((dw[q] >> 20) & 7u), A, Bs, narrow_of(sc), &er,
                                                        ((dw[q] >> 27) & 1u) != 0u);
       const int co = c.L.con + 4 * ci;
       t.f(co + 0, e) = ct.pen.x;
@@ -1533,15 +1548,15 @@ CX_DEV cx::v2 epa_pair(const PairSide& ps, int h, const cx::v2* simplex, int ite
   }
   return closest_on_edge_to_origin(best0, best1);
 }
-CX_DEV bool gjk_epa_pair(const cx::Shape& mine, int h, int na, int nb, cx::v2 d0, bool need_pen, cx::v2* pen,
-                         float* col) {
+CX_DEV bool gjk_epa_pair(const cx::Shape& mine, int h, int na, int nb, const cx::NarrowParams& np, bool need_pen,
+                         cx::v2* pen, float* col) {
   using namespace cx;
   const PairSide ps{mine, h};
   v2 simplex[3];
   *pen = v2{0.0f, 0.0f};
-  if (!gjk(ps, ps, d0, simplex)) return false;
+  if (!gjk(ps, ps, np.d0, simplex, np.gjk_steps)) return false;
   if (!need_pen) return true;
-  const int iters = na + nb + 1;
+  const int it0 = na + nb + 1, iters = it0 < np.epa_cap ? it0 : np.epa_cap;  // min(48, ...), cotix/_contacts.py:295
   *pen = iters + 3 <= 14 ? epa_pair<14>(ps, h, simplex, iters, col) : epa_pair<20>(ps, h, simplex, iters, col);
   return true;
 }
@@ -1580,7 +1595,7 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
   float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
   Contact ct;
   const bool hit = CXK_SKIP(a, 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
-                                     : gjk_epa_pair(S, h, na, nb, v2{sc.d0x, sc.d0y}, !self, &ct.pen, col);
+                                     : gjk_epa_pair(S, h, na, nb, narrow_of(sc), !self, &ct.pen, col);
   if (h != 0) return;
   ct.cp = v2{qnan(), qnan()};
   if (hit && self && self_cp_finite(S)) ct.cp = v2{0.0f, 0.0f};  // S is A on lane 0 (see b_item)
@@ -1788,9 +1803,10 @@ CX_DEV void ph_C1(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int par, i
       const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
       if (!(isn(cpx) || isn(cpy))) {  // a NaN candidate never writes
         const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
-        const key2 k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
-        const key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);   // :254
-        pass = bernoulli_half(split_at(k, 2u, 0u)) ? 1u : 0u;                      // :222-223
+        const bool part = sc.prng != 0;
+        const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
+        const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
+        pass = bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part) ? 1u : 0u;           // :222-223
       }
     }
   }
@@ -1920,9 +1936,10 @@ CX_DEV uint32_t m1_pass(const Ctx& c, Tile<EW> t, int lane, uint64_t pend, int k
         if (!(isn(cpx) || isn(cpy))) {  // a NaN candidate never writes
           CXK_STAT(valid_draws, 1);
           const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
-          const key2 k2 = split_at(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2);  // :264
-          const key2 k = split_at(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1);   // :254
-          pass = bernoulli_half(split_at(k, 2u, 0u)) ? 1u : 0u;                      // :222-223
+          const bool part = sc.prng != 0;
+          const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
+          const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
+          pass = bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part) ? 1u : 0u;           // :222-223
         }
       }
     }
@@ -2016,7 +2033,7 @@ CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid) {
   const Params pj = load_par(t.tb, sc.o_par + 4 * jc);
   const Rcp qj = load_rcp(t.tb, sc.o_rcp + 2 * jc);
   const ResPre p = resolve_pre<RCP>(bi, load_par(t.tb, sc.o_par + 4 * i), load_rcp(t.tb, sc.o_rcp + 2 * i), bj, pj, qj,
-                                    v2{t.f(co, e), t.f(co + 1, e)}, cp);
+                                    v2{t.f(co, e), t.f(co + 1, e)}, cp, baum_of(sc));
   t.f(ro + RP_NX, e) = p.n.x;
   t.f(ro + RP_NY, e) = p.n.y;
   t.f(ro + RP_R1X, e) = p.r1.x;
@@ -2074,8 +2091,9 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
       u = t.f(L.kw + slot * L.kww + 2 + 2 * nt + i, e);
     } else {
       const int so = nt > 0 ? L.skt + 2 * (nt - 1) : L.sk0;
-      key2 ck = split_at(key2{t.w(so, e), t.w(so + 1, e)}, (uint32_t)nb, (uint32_t)i);
-      u = unit_float(bits1(ck));
+      const bool part = c.sh.prng != 0;
+      key2 ck = split_at_l(key2{t.w(so, e), t.w(so + 1, e)}, (uint32_t)nb, (uint32_t)i, part);
+      u = unit_float(bits1_l(ck, part));
     }
     float last = cs[0];
 #pragma unroll
@@ -2590,7 +2608,8 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         Dyn gj = Dyn{t.f(aj, e), t.f(aj + 1, e), t.f(aj + 2, e), t.f(aj + 3, e), t.f(aj + 4, e), t.f(aj + 5, e)};
         v2 gpen = v2{0.0f, 0.0f}, gcp = v2{0.0f, 0.0f};
         resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
-                    v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp);
+                    v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp,
+                    baum_of(sc));
         // the contact: fn(world(part pa), world(part pb)); world = local + body position
         const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
         const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);

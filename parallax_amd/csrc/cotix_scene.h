@@ -48,11 +48,64 @@ inline int registry_fn(int ta, int tb) {
 }
 
 
+// the reference's literals (include/cotix_amd.h cotix_params)
+inline cotix_params default_params() {
+  cotix_params p;
+  p.prng_layout = COTIX_PRNG_LEGACY;
+  p.baumgarte = 0.3f;      // cotix/_collision_resolution.py:105
+  p.baumgarte_dt = 0.01f;  // :115
+  p.contact_p = 0.5f;      // cotix/_colliders.py:220
+  p.gjk_max_steps = 32;    // cotix/_collisions.py:101
+  p.epa_max_iters = 48;    // cotix/_contacts.py:271,295
+  p.epa_circle_iters = 128;  // cotix/_contacts.py:162-163
+  p.epa_body_iters = 48;   // cotix/_universal_shape.py:120
+  return p;
+}
+inline int check_params(const cotix_params& p, std::string& err) {
+  if (p.prng_layout != COTIX_PRNG_LEGACY && p.prng_layout != COTIX_PRNG_PARTITIONABLE)
+    return scene_fail(err, "prng_layout must be COTIX_PRNG_LEGACY or COTIX_PRNG_PARTITIONABLE");
+  if (p.gjk_max_steps < 0 || p.gjk_max_steps > 4096) return scene_fail(err, "gjk_max_steps outside 0..4096");
+  // the reference's error_if rejects fewer than 3 EPA iterations (cotix/_collisions.py:130-135)
+  if (p.epa_max_iters < 3 || p.epa_max_iters > 65535) return scene_fail(err, "epa_max_iters outside 3..65535");
+  if (p.epa_circle_iters < 3 || p.epa_circle_iters > 128) return scene_fail(err, "epa_circle_iters outside 3..128");
+  if (p.epa_body_iters < 3 || p.epa_body_iters > 128) return scene_fail(err, "epa_body_iters outside 3..128");
+  return 0;
+}
+// the scene header's parameter fields
+inline void set_params(SceneHdr& s, const cotix_params& p) {
+  s.prng = (uint16_t)p.prng_layout;
+  const cx::v2 d0 = cx::gjk_d0(p.prng_layout == COTIX_PRNG_PARTITIONABLE);  // random_direction(PRNGKey(1))
+  s.d0x = d0.x;
+  s.d0y = d0.y;
+  s.gjk_steps = (uint16_t)p.gjk_max_steps;
+  s.epa_cap = (uint16_t)p.epa_max_iters;
+  s.epa_cp = (uint16_t)p.epa_circle_iters;
+  s.epa_body = (uint16_t)p.epa_body_iters;
+  s.baum = p.baumgarte;
+  s.baum_dt = p.baumgarte_dt;
+  s.pc = p.contact_p;
+}
+inline cotix_params params_of(const SceneHdr& s) {
+  cotix_params p;
+  p.prng_layout = s.prng;
+  p.baumgarte = s.baum;
+  p.baumgarte_dt = s.baum_dt;
+  p.contact_p = s.pc;
+  p.gjk_max_steps = s.gjk_steps;
+  p.epa_max_iters = s.epa_cap;
+  p.epa_circle_iters = s.epa_cp;
+  p.epa_body_iters = s.epa_body;
+  return p;
+}
+
 // Compiles the body/part description into SceneDev tables.  Returns 0 or -1
 // (message in err).  n_cand / fnset: candidate count and contact-function set.
+// prm: cotix_params (nullable: the reference's literals).
 inline int compile_scene(int n_bodies, const float* body_params, int n_parts, const int* part_body,
                          const int* part_type, const int* part_nverts, SceneDev& s, int& n_cand, int& fnset,
-                         std::string& err) {
+                         std::string& err, const cotix_params* prm = nullptr) {
+  const cotix_params par = prm ? *prm : default_params();
+  if (check_params(par, err)) return -1;
   if (!body_params || !part_body || !part_type) return scene_fail(err, "null argument");
 
   if (n_bodies < 1 || n_bodies > MAXB) return scene_fail(err, "n_bodies out of range (1..16)");
@@ -60,10 +113,7 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   std::memset(&s, 0, sizeof(s));
   s.nb = n_bodies;
   s.np = n_parts;
-  // GJK start direction: random_direction(PRNGKey(1)) (cotix/_collisions.py:287-298)
-  uint32_t bx = 0xbd56c50bu, by = 0x3f7fa5d9u;
-  std::memcpy(&s.d0x, &bx, 4);
-  std::memcpy(&s.d0y, &by, 4);
+  set_params(s, par);  // incl. the GJK start direction (cotix/_collisions.py:287-298)
   std::vector<int> part_bodyv(n_parts), part_kindv(n_parts), part_nv(n_parts), part_goffv(n_parts),
       part_woffv(n_parts);
   std::vector<std::vector<int>> parts_of(n_bodies);

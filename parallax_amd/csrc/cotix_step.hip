@@ -64,13 +64,13 @@ __device__ __forceinline__ cx::Shape load_shape(const float* p) {
   for (int k = 0; k < 2 * cx::MAXV; ++k) s.w[k] = p[2 + k];
   return s;
 }
-__global__ void contacts_kernel(int fn, int n, const float* a, const float* b, float* out, uint32_t* err, float d0x,
-                                float d0y) {
+__global__ void contacts_kernel(int fn, int n, const float* a, const float* b, float* out, uint32_t* err,
+                                cx::NarrowParams np) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const cx::Shape A = load_shape(a + 18 * (size_t)i), Bs = load_shape(b + 18 * (size_t)i);
   uint32_t er = 0u;
-  cx::Contact c = cx::run_contact(fn, A, Bs, cx::v2{d0x, d0y}, &er);
+  cx::Contact c = cx::run_contact(fn, A, Bs, np, &er);
   out[4 * (size_t)i + 0] = c.pen.x;
   out[4 * (size_t)i + 1] = c.pen.y;
   out[4 * (size_t)i + 2] = c.cp.x;
@@ -80,11 +80,11 @@ __global__ void contacts_kernel(int fn, int n, const float* a, const float* b, f
 using cxk::BodyParts;
 using cxk::MAXBP;
 __global__ void body_pen_kernel(const float* dyn, int B, const float* geom, int gstride, BodyParts pa, BodyParts pb,
-                                float d0x, float d0y, int* collides, float* pen) {
+                                cx::NarrowParams np, int* collides, float* pen) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= B) return;
   cx::v2 p;
-  collides[g] = cxk::body_penetration_env(dyn, B, geom, gstride, pa, pb, cx::v2{d0x, d0y}, g, &p) ? 1 : 0;
+  collides[g] = cxk::body_penetration_env(dyn, B, geom, gstride, pa, pb, np, g, &p) ? 1 : 0;
   pen[2 * (size_t)g] = p.x;
   pen[2 * (size_t)g + 1] = p.y;
 }
@@ -116,7 +116,8 @@ __global__ void check_state_kernel(const float* dyn, int nb, int B, uint32_t* er
   const uint32_t e = cxk::state_check_env(dyn, nb, B, g);
   if (e) err[g] |= e;
 }
-__global__ void resolve_kernel(int n, float* d1, const float* p1, float* d2, const float* p2, const float* con) {
+__global__ void resolve_kernel(int n, float* d1, const float* p1, float* d2, const float* p2, const float* con,
+                               cx::Baum bm) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float* a = d1 + 6 * (size_t)i;
@@ -126,7 +127,7 @@ __global__ void resolve_kernel(int n, float* d1, const float* p1, float* d2, con
   const float* q2 = p2 + 4 * (size_t)i;
   cx::Params m1 = cx::Params{q1[0], q1[1], q1[2], q1[3]}, m2 = cx::Params{q2[0], q2[1], q2[2], q2[3]};
   const float* c = con + 4 * (size_t)i;
-  cx::resolve_collision(x, m1, y, m2, cx::v2{c[0], c[1]}, cx::v2{c[2], c[3]});
+  cx::resolve_collision(x, m1, y, m2, cx::v2{c[0], c[1]}, cx::v2{c[2], c[3]}, bm);
   a[2] = x.vx; a[3] = x.vy; a[5] = x.w;
   b[2] = y.vx; b[3] = y.vy; b[5] = y.w;
 }
@@ -137,23 +138,30 @@ __global__ void threefry_kernel(const uint32_t* k, const uint32_t* c, uint32_t* 
   o[2 * i] = r.a;
   o[2 * i + 1] = r.b;
 }
-__global__ void split_kernel(const uint32_t* k, int n, int num, uint32_t* o) {
+__global__ void split_kernel(const uint32_t* k, int n, int num, uint32_t* o, int part) {
   long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)n * num) return;
   int i = (int)(t / num), j = (int)(t % num);
-  cx::key2 r = cx::split_at(cx::key2{k[2 * i], k[2 * i + 1]}, (uint32_t)num, (uint32_t)j);
+  cx::key2 r = cx::split_at_l(cx::key2{k[2 * i], k[2 * i + 1]}, (uint32_t)num, (uint32_t)j, part != 0);
   o[2 * t] = r.a;
   o[2 * t + 1] = r.b;
 }
-// uniform(key, (count,)): word m of iota(count) counters, legacy layout
-__global__ void uniform_kernel(const uint32_t* k, int n, int count, float lo, float hi, float* o) {
+// uniform(key, (count,)): word m of the draw.  Legacy: iota(count) counters
+// split in halves (zero pad when odd); partitionable: y0 ^ y1 of block (0, m)
+__global__ void uniform_kernel(const uint32_t* k, int n, int count, float lo, float hi, float* o, int part) {
   long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)n * count) return;
   int i = (int)(t / count), m = (int)(t % count);
   cx::key2 key = cx::key2{k[2 * i], k[2 * i + 1]};
   int half = (count + 1) / 2;  // padded counter array split in two halves
-  uint32_t w = (m < half) ? cx::threefry(key, (uint32_t)m, (uint32_t)(m + half < count ? m + half : 0)).a
-                          : cx::threefry(key, (uint32_t)(m - half), (uint32_t)m).b;
+  uint32_t w;
+  if (part) {
+    const cx::key2 r = cx::threefry(key, 0u, (uint32_t)m);
+    w = r.a ^ r.b;
+  } else {
+    w = (m < half) ? cx::threefry(key, (uint32_t)m, (uint32_t)(m + half < count ? m + half : 0)).a
+                   : cx::threefry(key, (uint32_t)(m - half), (uint32_t)m).b;
+  }
   // the odd pad counter is 0: block (half-1, pad) only feeds word half-1
   o[t] = cx::fmax_(lo, cx::unit_float(w) * (hi - lo) + lo);
 }
@@ -164,6 +172,31 @@ __global__ void order_cw_kernel(float* xy, int n, int nv) {
   for (int k = 0; k < 2 * nv; ++k) v[k] = xy[(size_t)i * 2 * nv + k];
   cx::order_clockwise(v, nv);
   for (int k = 0; k < 2 * nv; ++k) xy[(size_t)i * 2 * nv + k] = v[k];
+}
+// check_for_collision_convex (cotix/_collisions.py:277-310): hit and the
+// simplex, NaN * simplex when there is no collision
+__global__ void gjk_kernel(int n, const float* a, const float* b, int32_t* hit, float* simplex, cx::NarrowParams np) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const cx::Shape A = load_shape(a + 18 * (size_t)i), Bs = load_shape(b + 18 * (size_t)i);
+  cx::v2 sx[3];
+  const bool h = cx::gjk(A, Bs, np.d0, sx, np.gjk_steps);
+  hit[i] = h ? 1 : 0;
+  for (int k = 0; k < 3; ++k) {  // (False, nan * simplex) when there is no collision
+    simplex[6 * (size_t)i + 2 * k] = h ? sx[k].x : sx[k].x * cx::qnan();
+    simplex[6 * (size_t)i + 2 * k + 1] = h ? sx[k].y : sx[k].y * cx::qnan();
+  }
+}
+// compute_penetration_vector_convex (:313-329): EPA from a given simplex
+__global__ void epa_kernel(int n, const float* a, const float* b, const float* simplex, int iters, float* pen) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const cx::Shape A = load_shape(a + 18 * (size_t)i), Bs = load_shape(b + 18 * (size_t)i);
+  const float* s = simplex + 6 * (size_t)i;
+  const cx::v2 sx[3] = {cx::v2{s[0], s[1]}, cx::v2{s[2], s[3]}, cx::v2{s[4], s[5]}};
+  const cx::v2 p = cx::epa_big(A, Bs, sx, iters);
+  pen[2 * (size_t)i] = p.x;
+  pen[2 * (size_t)i + 1] = p.y;
 }
 __global__ void euler_kernel(float* dyn, int nb, int B, float dt) {
   long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -205,16 +238,34 @@ const char* cotix_last_error(void) { return g_err.c_str(); }
 const char* cotix_version(void) { return "cotix_amd 0.2 (gfx950) build " COTIX_BUILD_ID; }
 
 
-int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,
-                       const int* part_type, const int* part_nverts, cotix_scene** out) {
+int cotix_params_default(cotix_params* out) {
+  if (!out) return fail("null argument");
+  *out = cxk::default_params();
+  return 0;
+}
+
+int cotix_scene_create_ex(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                          const int* part_type, const int* part_nverts, const cotix_params* params,
+                          cotix_scene** out) {
   if (!out) return fail("null argument");
   cotix_scene* sc = new cotix_scene();
   if (cxk::compile_scene(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, sc->host,
-                         sc->n_candidates, sc->fnset, g_err)) {
+                         sc->n_candidates, sc->fnset, g_err, params)) {
     delete sc;
     return -1;
   }
   *out = sc;
+  return 0;
+}
+
+int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                       const int* part_type, const int* part_nverts, cotix_scene** out) {
+  return cotix_scene_create_ex(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, nullptr, out);
+}
+
+int cotix_scene_params(const cotix_scene* scene, cotix_params* out) {
+  if (!scene || !out) return fail("null argument");
+  *out = cxk::params_of(scene->host);
   return 0;
 }
 
@@ -511,7 +562,7 @@ int cotix_body_penetration(const cotix_scene* scene, const float* dyn, const flo
   BodyParts pa, pb;
   if (body_parts(scene, body_a, &pa) || body_parts(scene, body_b, &pb)) return -1;
   hipLaunchKernelGGL(body_pen_kernel, dim3((B + 63) / 64), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), dyn,
-                     B, geom, geom_stride, pa, pb, scene->host.d0x, scene->host.d0y, collides, pen);
+                     B, geom, geom_stride, pa, pb, cxk::narrow_of(scene->host), collides, pen);
   return hip_check(hipGetLastError(), "body_pen_kernel launch");
 }
 
@@ -581,26 +632,67 @@ int cotix_check_state(const float* dyn, int n_bodies, int B, uint32_t* err, coti
   return hip_check(hipGetLastError(), "check_state_kernel launch");
 }
 
-int cotix_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err, cotix_stream_t stream) {
+// a parameter block (NULL: the defaults), validated, as the narrow phase's / resolution's arguments
+static int op_params(const cotix_params* params, cotix_params* out) {
+  *out = params ? *params : cxk::default_params();
+  return cxk::check_params(*out, g_err);
+}
+static cx::NarrowParams narrow_params(const cotix_params& p) {
+  return cx::NarrowParams{cx::gjk_d0(p.prng_layout == COTIX_PRNG_PARTITIONABLE), p.gjk_max_steps, p.epa_max_iters,
+                          p.epa_circle_iters, p.epa_body_iters};
+}
+
+int cotix_contacts_ex(int fn, int n, const float* a, const float* b, float* out, uint32_t* err,
+                      const cotix_params* params, cotix_stream_t stream) {
   if (!a || !b || !out) return fail("null argument");
   if (fn < 0 || fn > 5) return fail("unknown contact function");
+  cotix_params p;
+  if (op_params(params, &p)) return -1;
   if (n <= 0) return 0;
-  float d0x, d0y;
-  uint32_t bx = 0xbd56c50bu, by = 0x3f7fa5d9u;
-  std::memcpy(&d0x, &bx, 4);
-  std::memcpy(&d0y, &by, 4);
   hipLaunchKernelGGL(contacts_kernel, dim3((n + 127) / 128), dim3(128), 0, reinterpret_cast<hipStream_t>(stream), fn,
-                     n, a, b, out, err, d0x, d0y);
+                     n, a, b, out, err, narrow_params(p));
   return hip_check(hipGetLastError(), "contacts_kernel launch");
+}
+
+int cotix_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err, cotix_stream_t stream) {
+  return cotix_contacts_ex(fn, n, a, b, out, err, nullptr, stream);
+}
+
+int cotix_resolve_ex(int n, float* dyn1, const float* par1, float* dyn2, const float* par2, const float* contact,
+                     const cotix_params* params, cotix_stream_t stream) {
+  if (!dyn1 || !dyn2 || !par1 || !par2 || !contact) return fail("null argument");
+  cotix_params p;
+  if (op_params(params, &p)) return -1;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n,
+                     dyn1, par1, dyn2, par2, contact, cx::Baum{p.baumgarte, p.baumgarte_dt});
+  return hip_check(hipGetLastError(), "resolve_kernel launch");
 }
 
 int cotix_resolve(int n, float* dyn1, const float* par1, float* dyn2, const float* par2, const float* contact,
                   cotix_stream_t stream) {
-  if (!dyn1 || !dyn2 || !par1 || !par2 || !contact) return fail("null argument");
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n,
-                     dyn1, par1, dyn2, par2, contact);
-  return hip_check(hipGetLastError(), "resolve_kernel launch");
+  return cotix_resolve_ex(n, dyn1, par1, dyn2, par2, contact, nullptr, stream);
+}
+
+int cotix_gjk(int n, const float* a, const float* b, int32_t* hit, float* simplex, const cotix_params* params,
+              cotix_stream_t stream) {
+  if (!a || !b || !hit || !simplex) return fail("null argument");
+  cotix_params p;
+  if (op_params(params, &p)) return -1;
+  if (n <= 0) return n == 0 ? 0 : fail("negative size");
+  hipLaunchKernelGGL(gjk_kernel, dim3((n + 127) / 128), dim3(128), 0, reinterpret_cast<hipStream_t>(stream), n, a, b,
+                     hit, simplex, narrow_params(p));
+  return hip_check(hipGetLastError(), "gjk_kernel launch");
+}
+
+int cotix_epa(int n, const float* a, const float* b, const float* simplex, int iters, float* pen,
+              cotix_stream_t stream) {
+  if (!a || !b || !simplex || !pen) return fail("null argument");
+  if (iters < 3 || iters > 128) return fail("iters outside 3..128 (cotix/_collisions.py:130-135)");
+  if (n <= 0) return n == 0 ? 0 : fail("negative size");
+  hipLaunchKernelGGL(epa_kernel, dim3((n + 63) / 64), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), n, a, b,
+                     simplex, iters, pen);
+  return hip_check(hipGetLastError(), "epa_kernel launch");
 }
 
 int cotix_threefry2x32(const uint32_t* keys, const uint32_t* ctr, uint32_t* out, int n, cotix_stream_t stream) {
@@ -611,25 +703,41 @@ int cotix_threefry2x32(const uint32_t* keys, const uint32_t* ctr, uint32_t* out,
   return hip_check(hipGetLastError(), "threefry_kernel launch");
 }
 
-int cotix_random_split(const uint32_t* keys, int n, int num, uint32_t* out, cotix_stream_t stream) {
+static int check_layout(int layout) {
+  if (layout != COTIX_PRNG_LEGACY && layout != COTIX_PRNG_PARTITIONABLE) return fail("unknown PRNG layout");
+  return 0;
+}
+
+int cotix_random_split_ex(const uint32_t* keys, int n, int num, int layout, uint32_t* out, cotix_stream_t stream) {
   if (!keys || !out) return fail("null argument");
   if (num <= 0) return fail("num must be positive");
+  if (check_layout(layout)) return -1;
   long long t = (long long)n * num;
   if (t <= 0) return 0;
   hipLaunchKernelGGL(split_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), keys, n, num, out);
+                     reinterpret_cast<hipStream_t>(stream), keys, n, num, out, layout);
   return hip_check(hipGetLastError(), "split_kernel launch");
+}
+
+int cotix_random_split(const uint32_t* keys, int n, int num, uint32_t* out, cotix_stream_t stream) {
+  return cotix_random_split_ex(keys, n, num, COTIX_PRNG_LEGACY, out, stream);
+}
+
+int cotix_random_uniform_ex(const uint32_t* keys, int n, int count, float lo, float hi, int layout, float* out,
+                            cotix_stream_t stream) {
+  if (!keys || !out) return fail("null argument");
+  if (count <= 0) return fail("count must be positive");
+  if (check_layout(layout)) return -1;
+  long long t = (long long)n * count;
+  if (t <= 0) return 0;
+  hipLaunchKernelGGL(uniform_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), keys, n, count, lo, hi, out, layout);
+  return hip_check(hipGetLastError(), "uniform_kernel launch");
 }
 
 int cotix_random_uniform(const uint32_t* keys, int n, int count, float lo, float hi, float* out,
                          cotix_stream_t stream) {
-  if (!keys || !out) return fail("null argument");
-  if (count <= 0) return fail("count must be positive");
-  long long t = (long long)n * count;
-  if (t <= 0) return 0;
-  hipLaunchKernelGGL(uniform_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), keys, n, count, lo, hi, out);
-  return hip_check(hipGetLastError(), "uniform_kernel launch");
+  return cotix_random_uniform_ex(keys, n, count, lo, hi, COTIX_PRNG_LEGACY, out, stream);
 }
 
 int cotix_order_clockwise(float* xy, int n, int nverts, cotix_stream_t stream) {

@@ -78,14 +78,45 @@ def shape_rows(shapes_geometry, kind, nverts=0):
 KIND = {Circle: 0, AABB: 1}
 
 
-def run_contacts(fn, a_rows, b_rows):
-    """cotix_contacts over [n, 18] shape rows -> (ContactInfo, err[n])."""
+def _params_ref(params):
+    import ctypes
+    return None if params is None else ctypes.byref(params.c_struct())
+
+
+def run_contacts(fn, a_rows, b_rows, params=None):
+    """cotix_contacts_ex over [n, 18] shape rows -> (ContactInfo, err[n]);
+    params: parallax_amd.Params (GJK steps, EPA iterations, the GJK start
+    direction's PRNG layout), None: the reference's literals."""
     n = a_rows.shape[0]
     out = torch.empty(n, 4, dtype=torch.float32, device=a_rows.device)
     err = torch.zeros(n, dtype=torch.int32, device=a_rows.device)
-    _ffi.check(_ffi.lib.cotix_contacts(fn, n, _ffi.ptr(a_rows.contiguous()), _ffi.ptr(b_rows.contiguous()),
-                                       _ffi.ptr(out), _ffi.ptr(err), _ffi.stream_ptr(a_rows.device)), "cotix_contacts")
+    _ffi.check(_ffi.lib.cotix_contacts_ex(fn, n, _ffi.ptr(a_rows.contiguous()), _ffi.ptr(b_rows.contiguous()),
+                                          _ffi.ptr(out), _ffi.ptr(err), _params_ref(params),
+                                          _ffi.stream_ptr(a_rows.device)), "cotix_contacts_ex")
     return ContactInfo(out[:, 0:2], out[:, 2:4]), err
+
+
+def check_for_collision_convex(a_rows, b_rows, params=None):
+    """check_for_collision_convex(a.get_support, b.get_support)
+    (cotix/_collisions.py:277-310) over [n, 18] shape rows: (hit bool [n],
+    simplex f32 [n, 3, 2]) -- NaN * simplex where there is no collision."""
+    n = a_rows.shape[0]
+    hit = torch.empty(n, dtype=torch.int32, device=a_rows.device)
+    simplex = torch.empty(n, 3, 2, dtype=torch.float32, device=a_rows.device)
+    _ffi.check(_ffi.lib.cotix_gjk(n, _ffi.ptr(a_rows.contiguous()), _ffi.ptr(b_rows.contiguous()), _ffi.ptr(hit),
+                                  _ffi.ptr(simplex), _params_ref(params), _ffi.stream_ptr(a_rows.device)), "cotix_gjk")
+    return hit.bool(), simplex
+
+
+def compute_penetration_vector_convex(a_rows, b_rows, simplex, solver_iterations=48):
+    """compute_penetration_vector_convex (cotix/_collisions.py:313-329): EPA
+    from the given simplices [n, 3, 2] -> penetration f32 [n, 2]."""
+    n = a_rows.shape[0]
+    pen = torch.empty(n, 2, dtype=torch.float32, device=a_rows.device)
+    _ffi.check(_ffi.lib.cotix_epa(n, _ffi.ptr(a_rows.contiguous()), _ffi.ptr(b_rows.contiguous()),
+                                  _ffi.ptr(simplex.to(torch.float32).contiguous()), int(solver_iterations),
+                                  _ffi.ptr(pen), _ffi.stream_ptr(a_rows.device)), "cotix_epa")
+    return pen
 
 
 # _contact_funcs registry (cotix/_colliders.py:21-35): (type, type) -> fn id
@@ -106,14 +137,15 @@ contact_funcs = {
 }
 
 
-def resolve_collision(dyn1, par1, dyn2, par2, contact):
+def resolve_collision(dyn1, par1, dyn2, par2, contact, params=None):
     """Batched resolve_collision: dyn [n, 6] updated in place, par [n, 4]
-    (mass, inertia, elasticity, friction), contact [n, 4] (pen, cp)."""
+    (mass, inertia, elasticity, friction), contact [n, 4] (pen, cp); params:
+    the Baumgarte constants (parallax_amd.Params, None: 0.3 / 0.01)."""
     n = dyn1.shape[0]
     for t in (dyn1, dyn2):
         if not t.is_contiguous():
             raise ValueError("dyn tensors must be contiguous")
-    _ffi.check(_ffi.lib.cotix_resolve(n, _ffi.ptr(dyn1), _ffi.ptr(par1.contiguous()), _ffi.ptr(dyn2),
-                                      _ffi.ptr(par2.contiguous()), _ffi.ptr(contact.contiguous()),
-                                      _ffi.stream_ptr(dyn1.device)), "cotix_resolve")
+    _ffi.check(_ffi.lib.cotix_resolve_ex(n, _ffi.ptr(dyn1), _ffi.ptr(par1.contiguous()), _ffi.ptr(dyn2),
+                                         _ffi.ptr(par2.contiguous()), _ffi.ptr(contact.contiguous()),
+                                         _params_ref(params), _ffi.stream_ptr(dyn1.device)), "cotix_resolve_ex")
     return dyn1, dyn2

@@ -1,13 +1,17 @@
 """jax.random surface used by cotix, executed by the HIP PRNG kernels.
 
 Keys are int32 tensors [..., 2] holding the uint32 bit patterns of JAX's
-legacy threefry keys (uint32 arithmetic happens only in the kernels).
+threefry keys (uint32 arithmetic happens only in the kernels).  ``layout``:
+"legacy" (jax_threefry_partitionable=False, the default here and in JAX
+0.4.x), "partitionable" (the default from JAX 0.5), or a Params (its
+prng_layout) -- include/cotix_amd.h COTIX_PRNG_*.
 Call sites replaced: cotix/_colliders.py:142-295, cotix/_lunar_lander.py:109-123,
 examples/test_viz.py:39,46.
 """
 import torch
 
 from . import _ffi
+from .params import layout_id
 
 
 def PRNGKey(seed, device="cuda"):
@@ -25,22 +29,23 @@ def _keys2d(keys):
     return keys.reshape(-1, 2).contiguous()
 
 
-def split(keys, num=2):
+def split(keys, num=2, layout=None):
     """jax.random.split(key, num) for every key of a [..., 2] batch."""
     k = _keys2d(keys)
     out = torch.empty((k.shape[0], num, 2), dtype=torch.int32, device=k.device)
-    _ffi.check(_ffi.lib.cotix_random_split(_ffi.ptr(k), k.shape[0], num, _ffi.ptr(out),
-                                           _ffi.stream_ptr(k.device)), "cotix_random_split")
+    _ffi.check(_ffi.lib.cotix_random_split_ex(_ffi.ptr(k), k.shape[0], num, layout_id(layout), _ffi.ptr(out),
+                                              _ffi.stream_ptr(k.device)), "cotix_random_split_ex")
     return out.reshape(*keys.shape[:-1], num, 2)
 
 
-def uniform(keys, count=None, minval=0.0, maxval=1.0):
+def uniform(keys, count=None, minval=0.0, maxval=1.0, layout=None):
     """jax.random.uniform(key, (count,) or (), minval, maxval) (f32) per key."""
     k = _keys2d(keys)
     n = 1 if count is None else int(count)
     out = torch.empty((k.shape[0], n), dtype=torch.float32, device=k.device)
-    _ffi.check(_ffi.lib.cotix_random_uniform(_ffi.ptr(k), k.shape[0], n, float(minval), float(maxval),
-                                             _ffi.ptr(out), _ffi.stream_ptr(k.device)), "cotix_random_uniform")
+    _ffi.check(_ffi.lib.cotix_random_uniform_ex(_ffi.ptr(k), k.shape[0], n, float(minval), float(maxval),
+                                                layout_id(layout), _ffi.ptr(out), _ffi.stream_ptr(k.device)),
+               "cotix_random_uniform_ex")
     shape = keys.shape[:-1] if count is None else (*keys.shape[:-1], n)
     return out.reshape(shape)
 

@@ -71,23 +71,24 @@ def robocup_bodies():
     ]
 
 
-def robocup_perturbation(B, seed=2, device="cuda", offset=0, total=None):
+def robocup_perturbation(B, seed=2, device="cuda", offset=0, total=None, layout=None):
     """The build's batched-reset scheme for the envs
     with GLOBAL ids offset .. offset+B-1 of a `total`-env batch (default: B,
     offset 0), so a rank's shard equals the same envs of one big run: global
     env 0 is the exact reference state; env g >= 1 gets, from
     split(PRNGKey(seed), total)[g] -> (kp, kv, kw) = split(., 3): ball position
     U([-4.4,4.4] x [-2.9,2.9]), velocity U([-2,2]^2), angular velocity
-    U(-10,10).  Returns the ball's [6, B] dynamic columns."""
+    U(-10,10).  Returns the ball's [6, B] dynamic columns.  layout: the PRNG
+    layout of every draw (parallax_amd.random)."""
     total = env_range(B, offset, total)
-    k = jr.split(jr.PRNGKey(seed, device), total)[offset:offset + B].contiguous()
-    kk = jr.split(k, 3)
-    u = jr.uniform(kk[:, 0], 2)
+    k = jr.split(jr.PRNGKey(seed, device), total, layout)[offset:offset + B].contiguous()
+    kk = jr.split(k, 3, layout)
+    u = jr.uniform(kk[:, 0], 2, layout=layout)
     lo = torch.tensor([-4.4, -2.9], dtype=torch.float32, device=device)
     hi = torch.tensor([4.4, 2.9], dtype=torch.float32, device=device)
     pos = torch.maximum(lo, u * (hi - lo) + lo)
-    vel = jr.uniform(kk[:, 1], 2, -2.0, 2.0)
-    w = jr.uniform(kk[:, 2], None, -10.0, 10.0)
+    vel = jr.uniform(kk[:, 1], 2, -2.0, 2.0, layout)
+    w = jr.uniform(kk[:, 2], None, -10.0, 10.0, layout)
     cols = torch.stack([pos[:, 0], pos[:, 1], vel[:, 0], vel[:, 1], torch.zeros_like(w), w], 0)
     if offset == 0 and B > 0:
         cols[:, 0] = torch.tensor([0.0, 0.0, 1.0, 0.01, 0.0, 10.0], dtype=torch.float32, device=device)
@@ -99,19 +100,21 @@ class RoboCupEnv:
     (default split(PRNGKey(3), total)[offset:offset+B]); ``perturb``: apply
     robocup_perturbation.  ``env_offset`` / ``total_envs``: this batch holds the
     envs with global ids env_offset .. env_offset+B-1 of a total_envs-env run
-    (a rank's shard); defaults: 0 and B."""
+    (a rank's shard); defaults: 0 and B.  ``params``: the scene's
+    parameter block (parallax_amd.Params; its PRNG layout also draws the keys
+    and perturbations)."""
 
     stages = _ffi.STAGES_ROBOCUP
 
     def __init__(self, batch=1, device="cuda", keys=None, perturb=False, perturb_seed=2, env_offset=0,
-                 total_envs=None):
+                 total_envs=None, params=None):
         self.bodies = robocup_bodies()
         total = env_range(batch, env_offset, total_envs)
         if keys is None:
-            keys = jr.split(jr.PRNGKey(3, device), total)[env_offset:env_offset + batch].contiguous()
-        self.world = World(self.bodies, batch, device, keys)
+            keys = jr.split(jr.PRNGKey(3, device), total, params)[env_offset:env_offset + batch].contiguous()
+        self.world = World(self.bodies, batch, device, keys, params)
         if perturb:
-            self.world.dyn[4] = robocup_perturbation(batch, perturb_seed, device, env_offset, total)
+            self.world.dyn[4] = robocup_perturbation(batch, perturb_seed, device, env_offset, total, params)
         self.dyn_reset = self.world.dyn.clone()
 
     # field green, goals yellow / blue, ball red; white field outlines, no
@@ -156,19 +159,20 @@ class BoxWorld:
     env_offset+B-1 of total_envs) the 4 balls start at uniform positions in
     [-2.8, 2.8] x [-1.5, 2.5], velocities U(-3, 3)^2 and spins U(-5, 5) drawn
     from split(PRNGKey(seed), total)[id]; collider keys split(PRNGKey(seed+1),
-    total)[id].  Driver stages as RoboCup (Euler -> collider -> key split)."""
+    total)[id].  Driver stages as RoboCup (Euler -> collider -> key split).
+    ``params``: the scene's parameter block (its PRNG layout draws the keys too)."""
 
     stages = _ffi.STAGES_ROBOCUP
 
-    def __init__(self, batch=1, device="cuda", seed=9, env_offset=0, total_envs=None):
+    def __init__(self, batch=1, device="cuda", seed=9, env_offset=0, total_envs=None, params=None):
         self.bodies = box_world_bodies()
         total = env_range(batch, env_offset, total_envs)
         sl = slice(env_offset, env_offset + batch)
-        keys = jr.split(jr.PRNGKey(seed + 1, device), total)[sl].contiguous()
-        self.world = World(self.bodies, batch, device, keys)
-        kb = jr.split(jr.split(jr.PRNGKey(seed, device), total)[sl].contiguous(), 4)  # [B, 4, 2]: one key per ball
+        keys = jr.split(jr.PRNGKey(seed + 1, device), total, params)[sl].contiguous()
+        self.world = World(self.bodies, batch, device, keys, params)
+        kb = jr.split(jr.split(jr.PRNGKey(seed, device), total, params)[sl].contiguous(), 4, params)  # [B, 4, 2]
         for k in range(4):
-            u = jr.uniform(kb[:, k].contiguous(), 5)
+            u = jr.uniform(kb[:, k].contiguous(), 5, layout=params)
             d = self.world.dyn[3 + k]
             d[0] = u[:, 0] * 5.6 - 2.8
             d[1] = u[:, 1] * 4.0 - 1.5
@@ -196,11 +200,11 @@ LEFT_LEG = _bits(0x3CB9BFBD, 0xBED2C897, 0x3E5ADF1D, 0xBEB485B4, 0xBCB9BFBD, 0x3
 RIGHT_LEG = LEFT_LEG * np.array([-1.0, 1.0], dtype=np.float32)  # :68-72 (not re-sorted)
 
 
-def lunar_terrain(keys):
+def lunar_terrain(keys, layout=None):
     """cotix/_lunar_lander.py:109-132 per env: keys [B, 2] -> quads [B, 7, 4, 2]
     (unsorted; Polygon4 sorts them when the world uploads geometry)."""
-    ks = jr.split(keys, 5)
-    h = jr.uniform(ks[:, 0], 8, -5.0, 5.0).clone()
+    ks = jr.split(keys, 5, layout)
+    h = jr.uniform(ks[:, 0], 8, -5.0, 5.0, layout).clone()
     h[:, 0] = h[:, 0] * 10.0
     h[:, 3] = -2.0
     h[:, 4] = -2.0
@@ -209,12 +213,12 @@ def lunar_terrain(keys):
     dev = keys.device
     pos = torch.empty(B, 8, dtype=torch.float32, device=dev)
     pos[:, 0] = -100.0
-    pos[:, 1] = jr.uniform(ks[:, 1], None, -12.0, -9.0)
-    pos[:, 2] = jr.uniform(ks[:, 2], None, -8.0, -4.0)
+    pos[:, 1] = jr.uniform(ks[:, 1], None, -12.0, -9.0, layout)
+    pos[:, 2] = jr.uniform(ks[:, 2], None, -8.0, -4.0, layout)
     pos[:, 3] = -2.0
     pos[:, 4] = 2.0
-    pos[:, 5] = jr.uniform(ks[:, 3], None, 4.0, 8.0)
-    pos[:, 6] = jr.uniform(ks[:, 4], None, 9.0, 12.0)
+    pos[:, 5] = jr.uniform(ks[:, 3], None, 4.0, 8.0, layout)
+    pos[:, 6] = jr.uniform(ks[:, 4], None, 9.0, 12.0, layout)
     pos[:, 7] = 100.0
     m10 = torch.full((B, 7), -10.0, device=dev)
     p1 = torch.stack([pos[:, :7], h[:, :7]], -1)
@@ -246,21 +250,22 @@ class LunarLander:
     """LunarLander with a batch dimension.  ``key``: terrain key(s) -- one
     key [2] (every env the same terrain) or [B, 2]; default PRNGKey(0).
     ``collider_keys`` default split(PRNGKey(1), B) (env 0 of a batch of 1:
-    PRNGKey(0), the reference's examples/test_viz.py:46)."""
+    PRNGKey(0), the reference's examples/test_viz.py:46).  ``params``: the
+    scene's parameter block (its PRNG layout also draws the terrain)."""
 
     stages = _ffi.STAGES_LUNAR
 
-    def __init__(self, key=None, batch=1, device="cuda", collider_keys=None):
+    def __init__(self, key=None, batch=1, device="cuda", collider_keys=None, params=None):
         if key is None:
             key = jr.PRNGKey(0, device)
         key = key.to(device)
         keys = key.expand(batch, 2).contiguous() if key.dim() == 1 else key
-        terrain = lunar_terrain(keys)
+        terrain = lunar_terrain(keys, params)
         self.bodies = lunar_lander_bodies(terrain)
         if collider_keys is None:
             collider_keys = (jr.PRNGKey(0, device)[None] if batch == 1
-                             else jr.split(jr.PRNGKey(1, device), batch))
-        self.world = World(self.bodies, batch, device, collider_keys)
+                             else jr.split(jr.PRNGKey(1, device), batch, params))
+        self.world = World(self.bodies, batch, device, collider_keys, params)
         self.dyn_reset = self.world.dyn.clone()
         # the polygon broadphase (results unchanged: the kernel certifies every pair it skips)
         self.stages = _ffi.STAGES_LUNAR | _ffi.STAGE_BROADPHASE

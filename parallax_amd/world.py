@@ -10,15 +10,22 @@ import torch
 
 from . import _ffi
 from .bodies import AnyBody, BodyView
+from .params import DEFAULT as DEFAULT_PARAMS
+from .params import CotixParams, Params
 from .shapes import AbstractPolygon
 
 
 class Scene:
-    """cotix_scene_create: the collider's trace-time enumeration
-    (cotix/_colliders.py:86-131) compiled once into device tables."""
+    """cotix_scene_create_ex: the collider's trace-time enumeration
+    (cotix/_colliders.py:86-131) compiled once into device tables, with the
+    parameter block `params` (parallax_amd.Params; None: the reference's
+    literals)."""
 
-    def __init__(self, bodies):
+    def __init__(self, bodies, params=None):
         import ctypes
+        self.params = DEFAULT_PARAMS if params is None else params
+        if not isinstance(self.params, Params):
+            raise TypeError("params must be a parallax_amd.Params")
         self.n_bodies = len(bodies)
         params = torch.tensor([b.params() for b in bodies], dtype=torch.float32)
         part_body, part_type, part_nv = [], [], []
@@ -32,8 +39,10 @@ class Scene:
         pt = torch.tensor(part_type, dtype=torch.int32)
         pn = torch.tensor(part_nv, dtype=torch.int32)
         h = ctypes.c_void_p()
-        _ffi.check(_ffi.lib.cotix_scene_create(self.n_bodies, _ffi.ptr(params), len(part_body), _ffi.ptr(pb),
-                                               _ffi.ptr(pt), _ffi.ptr(pn), ctypes.byref(h)), "cotix_scene_create")
+        cp = self.params.c_struct()
+        _ffi.check(_ffi.lib.cotix_scene_create_ex(self.n_bodies, _ffi.ptr(params), len(part_body), _ffi.ptr(pb),
+                                                  _ffi.ptr(pt), _ffi.ptr(pn), ctypes.byref(cp), ctypes.byref(h)),
+                   "cotix_scene_create_ex")
         self.handle = h
         self.geom_floats = _ffi.lib.cotix_scene_geom_floats(h)
 
@@ -42,6 +51,13 @@ class Scene:
         v = [ctypes.c_int() for _ in range(4)]
         _ffi.check(_ffi.lib.cotix_scene_info(self.handle, *[ctypes.byref(x) for x in v]), "cotix_scene_info")
         return dict(zip(("contacts", "cells", "candidates", "types"), [x.value for x in v]))
+
+    def compiled_params(self):
+        """The scene's parameter block as the library holds it (cotix_scene_params)."""
+        import ctypes
+        c = CotixParams()
+        _ffi.check(_ffi.lib.cotix_scene_params(self.handle, ctypes.byref(c)), "cotix_scene_params")
+        return Params.from_c(c)
 
     def set_variant(self, envs_per_wave=0, specialize=True):
         """Kernel variant of this scene's launches: envs per wave (0 = the
@@ -67,13 +83,14 @@ class Scene:
 
 
 class World:
-    def __init__(self, bodies, batch=1, device="cuda", keys=None):
+    def __init__(self, bodies, batch=1, device="cuda", keys=None, params=None):
         if not all(isinstance(b, AnyBody) for b in bodies):
             raise TypeError("bodies must be AnyBody")
         self.bodies = list(bodies)
         self.B = int(batch)
         self.device = torch.device(device)
-        self.scene = Scene(self.bodies)
+        self.scene = Scene(self.bodies, params)
+        self.params = self.scene.params
         self.geom = self._upload_geometry()
         self.geom_stride = 0 if self.geom.dim() == 1 else self.geom.shape[1]
         self.dyn = torch.stack([b.dyn_columns(self.B) for b in self.bodies], 0).to(self.device).contiguous()

@@ -73,16 +73,20 @@ void run_any(const cxk::KArgs& a, int E, int mode) {
 extern "C" {
 const char* emu_last_error(void) { return g_err.c_str(); }
 
-int emu_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body, const int* part_type,
-                     const int* part_nverts, void** out) {
+int emu_scene_create_ex(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                        const int* part_type, const int* part_nverts, const cotix_params* params, void** out) {
   EmuScene* s = new EmuScene();
   if (cxk::compile_scene(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, s->s, s->n_cand,
-                         s->fnset, g_err)) {
+                         s->fnset, g_err, params)) {
     delete s;
     return -1;
   }
   *out = s;
   return 0;
+}
+int emu_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body, const int* part_type,
+                     const int* part_nverts, void** out) {
+  return emu_scene_create_ex(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, nullptr, out);
 }
 
 int emu_scene_destroy(void* s) {
@@ -229,30 +233,60 @@ int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* sa
   return 0;
 }
 
-int emu_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err) {
-  const cx::v2 d0{-0.05243401f, 0.9986244f};
-  uint32_t bx = 0xbd56c50bu, by = 0x3f7fa5d9u;
-  cx::v2 dd;
-  std::memcpy(&dd.x, &bx, 4);
-  std::memcpy(&dd.y, &by, 4);
-  (void)d0;
+static cx::Shape emu_shape(const float* p) {
+  cx::Shape S;
+  S.kind = (int)p[0];
+  S.n = (int)p[1];
+  for (int k = 0; k < 16; ++k) S.w[k] = p[2 + k];
+  return S;
+}
+static cx::NarrowParams emu_narrow(const cotix_params* prm) {
+  const cotix_params p = prm ? *prm : cxk::default_params();
+  return cx::NarrowParams{cx::gjk_d0(p.prng_layout == COTIX_PRNG_PARTITIONABLE), p.gjk_max_steps, p.epa_max_iters,
+                          p.epa_circle_iters, p.epa_body_iters};
+}
+int emu_contacts_ex(int fn, int n, const float* a, const float* b, float* out, uint32_t* err,
+                    const cotix_params* prm) {
+  const cx::NarrowParams np = emu_narrow(prm);
   for (int i = 0; i < n; ++i) {
-    cx::Shape A, Bs;
-    A.kind = (int)a[18 * i];
-    A.n = (int)a[18 * i + 1];
-    Bs.kind = (int)b[18 * i];
-    Bs.n = (int)b[18 * i + 1];
-    for (int k = 0; k < 16; ++k) {
-      A.w[k] = a[18 * i + 2 + k];
-      Bs.w[k] = b[18 * i + 2 + k];
-    }
+    const cx::Shape A = emu_shape(a + 18 * i), Bs = emu_shape(b + 18 * i);
     uint32_t er = 0;
-    cx::Contact c = cx::run_contact(fn, A, Bs, dd, &er);
+    cx::Contact c = cx::run_contact(fn, A, Bs, np, &er);
     out[4 * i] = c.pen.x;
     out[4 * i + 1] = c.pen.y;
     out[4 * i + 2] = c.cp.x;
     out[4 * i + 3] = c.cp.y;
     if (err) err[i] = er;
+  }
+  return 0;
+}
+int emu_contacts(int fn, int n, const float* a, const float* b, float* out, uint32_t* err) {
+  return emu_contacts_ex(fn, n, a, b, out, err, nullptr);
+}
+// the GJK / EPA operators (host builds of cotix_gjk / cotix_epa)
+int emu_gjk(int n, const float* a, const float* b, int32_t* hit, float* simplex, const cotix_params* prm) {
+  const cx::NarrowParams np = emu_narrow(prm);
+  for (int i = 0; i < n; ++i) {
+    const cx::Shape A = emu_shape(a + 18 * i), Bs = emu_shape(b + 18 * i);
+    cx::v2 sx[3];
+    const bool h = cx::gjk(A, Bs, np.d0, sx, np.gjk_steps);
+    hit[i] = h ? 1 : 0;
+    for (int k = 0; k < 3; ++k) {
+      simplex[6 * i + 2 * k] = h ? sx[k].x : sx[k].x * cx::qnan();
+      simplex[6 * i + 2 * k + 1] = h ? sx[k].y : sx[k].y * cx::qnan();
+    }
+  }
+  return 0;
+}
+int emu_epa(int n, const float* a, const float* b, const float* simplex, int iters, float* pen) {
+  if (iters < 3 || iters > 128) return -1;
+  for (int i = 0; i < n; ++i) {
+    const cx::Shape A = emu_shape(a + 18 * i), Bs = emu_shape(b + 18 * i);
+    const float* s = simplex + 6 * i;
+    const cx::v2 sx[3] = {cx::v2{s[0], s[1]}, cx::v2{s[2], s[3]}, cx::v2{s[4], s[5]}};
+    const cx::v2 p = cx::epa_big(A, Bs, sx, iters);
+    pen[2 * i] = p.x;
+    pen[2 * i + 1] = p.y;
   }
   return 0;
 }
@@ -290,7 +324,7 @@ extern "C" int emu_body_penetration(void* scene, const float* dyn, const float* 
   if (emu_body_parts(es, ba, &pa) || emu_body_parts(es, bb, &pb)) return -1;
   for (int g = 0; g < B; ++g) {
     cx::v2 p;
-    collides[g] = cxk::body_penetration_env(dyn, B, geom, gstride, pa, pb, cx::v2{es->s.d0x, es->s.d0y}, g, &p);
+    collides[g] = cxk::body_penetration_env(dyn, B, geom, gstride, pa, pb, cxk::narrow_of(es->s), g, &p);
     pen[2 * g] = p.x;
     pen[2 * g + 1] = p.y;
   }

@@ -17,6 +17,10 @@ def load(asan=False):
         raise FileNotFoundError("%s missing: run `make -C tests/emu` (or python __graft_entry__.py)" % path)
     lib = ctypes.CDLL(path)
     lib.emu_scene_create.argtypes = [ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.POINTER(P_)]
+    lib.emu_scene_create_ex.argtypes = [ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, ctypes.POINTER(P_)]
+    lib.emu_contacts_ex.argtypes = [ctypes.c_int, ctypes.c_int, P_, P_, P_, P_, P_]
+    lib.emu_gjk.argtypes = [ctypes.c_int, P_, P_, P_, P_, P_]
+    lib.emu_epa.argtypes = [ctypes.c_int, P_, P_, P_, ctypes.c_int, P_]
     lib.emu_step.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                              ctypes.c_int, P_, ctypes.c_int, P_, P_, ctypes.c_int]
     lib.emu_step_ex.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
@@ -43,9 +47,16 @@ def _p(a):
 TYPE_ID = {"Circle": 0, "AABB": 1, "Polygon": 2, "Polygon3": 3, "Polygon4": 4, "Polygon5": 5, "Polygon6": 6}
 
 
-def oracle_scene(lib, bodies):
-    """Scene + local geometry from oracle Body objects."""
-    params = np.array([[b.mass, b.inertia, b.elasticity, b.friction_coefficient] for b in bodies], np.float32)
+def params_ref(params):
+    """An oracle Params (cotix_oracle.params) as a cotix_params pointer, or NULL."""
+    return None if params is None else ctypes.cast(ctypes.pointer(params.c_struct()), P_)
+
+
+def oracle_scene(lib, bodies, params=None):
+    """Scene + local geometry from oracle Body objects; params: an oracle
+    Params (cotix_oracle.params), None: the defaults."""
+    prm = params
+    bparams = np.array([[b.mass, b.inertia, b.elasticity, b.friction_coefficient] for b in bodies], np.float32)
     pb, pt, pn, geom = [], [], [], []
     for i, b in enumerate(bodies):
         for p in b.parts:
@@ -63,7 +74,9 @@ def oracle_scene(lib, bodies):
                     geom += [v[0], v[1]]
     pb, pt, pn = (np.array(x, np.int32) for x in (pb, pt, pn))
     h = P_()
-    rc = lib.emu_scene_create(len(bodies), _p(params), len(pb), _p(pb), _p(pt), _p(pn), ctypes.byref(h))
+    cp = None if prm is None else prm.c_struct()
+    rc = lib.emu_scene_create_ex(len(bodies), _p(bparams), len(pb), _p(pb), _p(pt), _p(pn),
+                                 None if cp is None else ctypes.cast(ctypes.pointer(cp), P_), ctypes.byref(h))
     if rc:
         raise RuntimeError(lib.emu_last_error().decode())
     return h, np.array(geom, np.float32)

@@ -15,11 +15,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 
 from cotix_oracle import geometry as G  # noqa: E402
+from cotix_oracle import params as PR  # noqa: E402
 from cotix_oracle import physics as P  # noqa: E402
 from cotix_oracle import prng  # noqa: E402
 
+sys.path.insert(0, os.path.join(HERE, ".."))
+from param_sets import oracle_params  # noqa: E402
+
 F = np.float32
-D0 = prng.gjk_initial_direction()
+D0 = prng.gjk_initial_direction()  # the legacy layout's (the contact fixtures)
 
 
 # ---------------------------------------------------------------------------
@@ -148,6 +152,7 @@ def robocup_perturb(B, seed=2):
 
 def trace(make_bodies, step_fn, keys, T, init=None):
     B = len(keys)
+    d0 = prng.gjk_initial_direction()  # of the parameter block in force
     dyn, ks, errs, chosen, cells = [], [], [], [], []
     envs = []
     for e in range(B):
@@ -163,7 +168,7 @@ def trace(make_bodies, step_fn, keys, T, init=None):
         er_t, ch_t, cl_t = [], [], []
         for e in range(B):
             err, tr = G.ErrorFlag(), {}
-            envs[e], cur[e] = step_fn(envs[e], cur[e], D0, err, tr)
+            envs[e], cur[e] = step_fn(envs[e], cur[e], d0, err, tr)
             er_t.append(err.bits)
             ch_t.append(tr["chosen"])
             cl_t.append(tr["cells"])
@@ -176,7 +181,7 @@ def trace(make_bodies, step_fn, keys, T, init=None):
                 chosen=np.array(chosen, np.int32), cells=np.array(cells, np.int32))
 
 
-def make_robocup(B=8, T=12):
+def make_robocup(B=8, T=12, suffix=""):
     keys = prng.split(prng.PRNGKey(3), B)
     pert = robocup_perturb(B)
     init = []
@@ -185,13 +190,13 @@ def make_robocup(B=8, T=12):
         d[4] = list(pert[e])
         init.append(d)
     tr = trace(lambda e: P.robocup_bodies(), P.robocup_step, keys, T, init)
-    np.savez_compressed(os.path.join(HERE, "robocup_trace.npz"), **tr)
+    np.savez_compressed(os.path.join(HERE, "robocup_trace%s.npz" % suffix), **tr)
 
 
 LL_DROP = [0.0, 6.0, 6.2, 6.4, 6.8, 7.5]
 
 
-def make_lunar(T=12):
+def make_lunar(T=12, suffix=""):
     B = len(LL_DROP)
     tkeys = prng.split(prng.PRNGKey(0), B)
     ckeys = prng.split(prng.PRNGKey(1), B)
@@ -207,7 +212,7 @@ def make_lunar(T=12):
     tr["terrain_keys"] = np.array(tkeys, np.uint32)
     tr["drop"] = np.array(LL_DROP, F)
     tr["init"] = tr["dyn"][0]
-    np.savez_compressed(os.path.join(HERE, "lunar_trace.npz"), **tr)
+    np.savez_compressed(os.path.join(HERE, "lunar_trace%s.npz" % suffix), **tr)
 
 
 def box_world_bodies(e):
@@ -238,7 +243,7 @@ def make_box_world(B=6, T=40):
     np.savez_compressed(os.path.join(HERE, "box_world_trace.npz"), **tr)
 
 
-def make_prng():
+def make_prng(suffix=""):
     rng = np.random.default_rng(5)
     keys = rng.integers(0, 2 ** 32, size=(64, 2), dtype=np.uint64).astype(np.uint32)
     ctr = rng.integers(0, 2 ** 32, size=(64, 2), dtype=np.uint64).astype(np.uint32)
@@ -247,15 +252,78 @@ def make_prng():
     splits = np.array([prng.split(k, 5) for k in keys[:16]], np.uint32)
     unif = np.array([prng.uniform(k, (7,), -3.0, 2.0) for k in keys[:16]], F)
     unif1 = np.array([prng.uniform(k, (), 4.0, 8.0) for k in keys[:16]], F)
-    np.savez_compressed(os.path.join(HERE, "prng.npz"), keys=keys, ctr=ctr, blocks=blocks, splits=splits,
-                        uniform7=unif, uniform1=unif1)
+    np.savez_compressed(os.path.join(HERE, "prng%s.npz" % suffix), keys=keys, ctr=ctr, blocks=blocks,
+                        splits=splits, uniform7=unif, uniform1=unif1)
+
+
+# ---------------------------------------------------------------------------
+# GJK / EPA as operators (cotix/_collisions.py:277-329)
+# ---------------------------------------------------------------------------
+def gjk_epa_pairs(rng):
+    """polygon x polygon, AABB x polygon, circle x polygon, circle x circle,
+    AABB x AABB, and degenerate inputs: identical shapes, touching edges,
+    collinear (zero-area) polygons, far-apart shapes, NaN vertices."""
+    pairs = [(rand_poly(rng, 4), rand_poly(rng, 6)) for _ in range(200)]
+    pairs += [(rand_poly(rng, 4), rand_poly(rng, 4)) for _ in range(150)]
+    pairs += [(rand_poly(rng, 3), rand_poly(rng, 8)) for _ in range(50)]
+    pairs += [(rand_aabb(rng, 0.6), rand_poly(rng, n)) for n in (4, 6) for _ in range(80)]
+    pairs += [(G.Circle(F(rng.uniform(0.2, 1.5)), (F(rng.normal() * 0.7), F(rng.normal() * 0.7))),
+               rand_poly(rng, n)) for n in (4, 6) for _ in range(60)]
+    pairs += [(rand_circle(rng), rand_circle(rng)) for _ in range(60)]
+    pairs += [(rand_aabb(rng), rand_aabb(rng)) for _ in range(60)]
+    sq = G.Polygon([(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0)], kind="Polygon4")
+    pairs += [(sq, sq),                                                                          # identical
+              (sq, G.Polygon([(1.0, 0.0), (2.0, 0.0), (2.0, 1.0), (1.0, 1.0)], kind="Polygon4")),  # shared edge
+              (sq, G.Polygon([(1.0, 1.0), (2.0, 1.0), (2.0, 2.0), (1.0, 2.0)], kind="Polygon4")),  # shared corner
+              (sq, G.Polygon([(0.0, 0.5), (1.0, 0.5), (2.0, 0.5), (0.5, 0.5)], kind="Polygon4", sort=False)),  # collinear
+              (sq, G.Polygon([(5.0, 5.0), (6.0, 5.0), (6.0, 6.0), (5.0, 6.0)], kind="Polygon4")),  # far apart
+              (sq, G.Polygon([(0.5, 0.5), (F(np.nan), 0.5), (1.5, 1.5), (0.5, 1.5)], kind="Polygon4", sort=False)),
+              (G.AABB((0.0, 0.0), (1.0, 1.0)), G.Polygon([(1.0, 0.0), (2.0, 0.0), (2.0, 1.0), (1.0, 1.0)],
+                                                          kind="Polygon4")),
+              (G.Circle(F(0.5), (0.5, 0.5)), sq)]
+    return pairs
+
+
+def make_gjk_epa(suffix=""):
+    """hit / simplex of check_for_collision_convex and the EPA penetration at
+    3 iteration counts (the reference's own count for the pair's type, 3, 48)
+    from the GJK simplex of every colliding pair (NaN simplices included)."""
+    rng = np.random.default_rng(77)
+    pairs = gjk_epa_pairs(rng)
+    A, B, H, S = [], [], [], []
+    for a, b in pairs:
+        A.append(row(a))
+        B.append(row(b))
+        h, sx = G.check_for_collision_convex(a, b, prng.gjk_initial_direction())
+        H.append(1 if h else 0)
+        S.append(np.array(sx, F).reshape(3, 2))
+    out = dict(a=np.array(A, F), b=np.array(B, F), hit=np.array(H, np.int32), simplex=np.array(S, F))
+    for it in (3, 11, 48):
+        out["pen%d" % it] = np.array([G.epa(a, b, [tuple(v) for v in s], it) for (a, b), s in zip(pairs, S)], F)
+    np.savez_compressed(os.path.join(HERE, "gjk_epa%s.npz" % suffix), **out)
+
+
+def make_variants():
+    """The fixtures of the non-default parameter blocks (tests/param_sets.py)."""
+    make_gjk_epa()
+    for suffix in ("_part", "_alt"):
+        with PR.use(oracle_params(suffix)):
+            make_robocup(suffix=suffix)
+            make_lunar(suffix=suffix)
+            make_gjk_epa(suffix)
+            if suffix == "_part":
+                make_prng(suffix)
 
 
 if __name__ == "__main__":
-    make_prng()
-    make_contacts()
-    make_robocup()
-    make_lunar()
-    make_box_world()
+    if sys.argv[1:] == ["variants"]:
+        make_variants()
+    else:
+        make_prng()
+        make_contacts()
+        make_robocup()
+        make_lunar()
+        make_box_world()
+        make_variants()
     for f in sorted(os.listdir(HERE)):
         print(f, os.path.getsize(os.path.join(HERE, f)))

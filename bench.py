@@ -77,8 +77,17 @@ def parse():
                     help="kernel tiling (0: the library default, 4); recorded in config")
     ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
                     help="0: the generic kernel instead of the reference scenes' specializations")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the multi-GPU path); gloo: ranks that share one GPU (tests), the "
+                         "observation all-gather through host memory")
+    ap.add_argument("--prng-layout", default="legacy", choices=["legacy", "partitionable"],
+                    help="the jax.random threefry layout of the collider (cotix_params; JAX 0.4.x: legacy, "
+                         "JAX >= 0.5: partitionable)")
+    ap.add_argument("--lib", default=None, help="another build of libcotix_amd.so (A/B tooling); recorded in config")
     a = ap.parse_args()
     refuse_overrides()
+    if a.lib:  # read by parallax_amd._ffi at import
+        os.environ["COTIX_AMD_LIB"] = os.path.abspath(a.lib)
     return a
 
 
@@ -97,16 +106,16 @@ def refuse_overrides():
 # ---------------------------------------------------------------------------
 # scenarios (global env ids [offset, offset+B) of a `total`-env run)
 # ---------------------------------------------------------------------------
-def make_scenario(pa, name, dev, B, offset=0, total=None):
+def make_scenario(pa, name, dev, B, offset=0, total=None, params=None):
     total = B if total is None else total
     sl = slice(offset, offset + B)
     if name == "robocup":
-        return pa.RoboCupEnv(batch=B, device=dev, perturb=True, env_offset=offset, total_envs=total)
+        return pa.RoboCupEnv(batch=B, device=dev, perturb=True, env_offset=offset, total_envs=total, params=params)
     if name == "box":
-        return pa.BoxWorld(batch=B, device=dev, env_offset=offset, total_envs=total)
-    tk = pa.random.split(pa.random.PRNGKey(0, dev), total)[sl].contiguous()
-    ck = pa.random.split(pa.random.PRNGKey(1, dev), total)[sl].contiguous()
-    return pa.LunarLander(key=tk, batch=B, device=dev, collider_keys=ck)
+        return pa.BoxWorld(batch=B, device=dev, env_offset=offset, total_envs=total, params=params)
+    tk = pa.random.split(pa.random.PRNGKey(0, dev), total, params)[sl].contiguous()
+    ck = pa.random.split(pa.random.PRNGKey(1, dev), total, params)[sl].contiguous()
+    return pa.LunarLander(key=tk, batch=B, device=dev, collider_keys=ck, params=params)
 
 
 def bytes_per_env(name, nb):
@@ -188,7 +197,7 @@ def finite_stats(pa, scen, substeps, launches):
             "sample": "%d envs x %d driver steps (one per launch + cotix_check_state)" % (w.B, n)}
 
 
-def valu_roofline(scenario, B, substeps, launch_ms, warmup=None):
+def valu_roofline(scenario, B, substeps, launch_ms, warmup=None, layout="legacy"):
     """Primary roofline: VALU issue.  SQ_INSTS_VALU per launch from the
     committed rocprofv3 PMC pass of the same workload
     (profiles/latest_pmc_<scenario>.json, tools/gpu_round.sh) over the live
@@ -202,6 +211,8 @@ def valu_roofline(scenario, B, substeps, launch_ms, warmup=None):
         if c.get("library") != library_build():  # counters of other kernel code: no frac
             return None
         if warmup is not None and pmc.get("warmup") != warmup:  # another stretch of the trajectory
+            return None
+        if c.get("prng_layout", "legacy") != layout:  # counters of the other PRNG layout's workload
             return None
         return {"valu_instr_per_launch": pmc["counters_per_launch"]["SQ_INSTS_VALU"],
                 "traffic": pmc["hbm_bytes_per_launch_corrected"],
@@ -219,7 +230,7 @@ def library_build():
     return _ffi.lib.cotix_version().decode()
 
 
-def roofline(scenario, B, substeps, launch_ms, nb):
+def roofline(scenario, B, substeps, launch_ms, nb, layout="legacy"):
     alg = bytes_per_env(scenario, nb) * B
     hbm = alg / (launch_ms * 1e-3) / 1e9
     out = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_WAVE_INSTR_S / 1e9, "unit": "G wave-instr/s",
@@ -230,7 +241,7 @@ def roofline(scenario, B, substeps, launch_ms, nb):
                    "achieved = SQ_INSTS_VALU per launch / live launch time; peak = 256 CU x 4 SIMD x 2.4 GHz / "
                    "2 cycles per wave64 instruction (one wave per SIMD issues at most half of it); "
                    "hbm = algorithmic bytes / launch time, reported because north_star asks"}
-    v = valu_roofline(scenario, B, substeps, launch_ms)
+    v = valu_roofline(scenario, B, substeps, launch_ms, layout=layout)
     if v is None:
         out["frac_note"] = ("no committed PMC pass (profiles/latest_pmc_%s.json) of this library build and "
                             "workload: frac left null rather than mixing counters of other code" % scenario)
@@ -399,7 +410,7 @@ def sub_config1(pa, dev):
 # ---------------------------------------------------------------------------
 # headline
 # ---------------------------------------------------------------------------
-def init_dist(force=False):
+def init_dist(force=False, backend="nccl"):
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -409,7 +420,10 @@ def init_dist(force=False):
     if world_size > 1 or force:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     return dist, rank, world_size, torch.device("cuda", local_rank)
 
 
@@ -417,11 +431,14 @@ def main():
     a = parse()
     if a.mode == "grad":
         return main_grad(a)
-    dist, rank, world_size, dev = init_dist(os.environ.get("COTIX_BENCH_FORCE_DIST") == "1")
+    dist, rank, world_size, dev = init_dist(os.environ.get("COTIX_BENCH_FORCE_DIST") == "1", a.dist_backend)
     import parallax_amd as pa
+    gloo = dist is not None and a.dist_backend == "gloo"
+    cdev = torch.device("cpu") if gloo else dev  # where the collectives' tensors live
 
     B = a.envs
-    scen = make_scenario(pa, a.scenario, dev, B, rank * B, world_size * B)
+    params = pa.Params(prng_layout=a.prng_layout)
+    scen = make_scenario(pa, a.scenario, dev, B, rank * B, world_size * B, params)
     scen.world.set_variant(a.envs_per_wave, bool(a.specialize))
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
@@ -429,7 +446,7 @@ def main():
     # observation all-gather, double-buffered and asynchronous: the RCCL
     # collective of launch i runs on its own stream while launch i+1 computes;
     # a buffer is rewritten only after the collective that read it is done
-    obs_all = [torch.empty(world_size * B, nbody, 6, device=dev) for _ in range(2)] if dist else None
+    obs_all = [torch.empty(world_size * B, nbody, 6, device=cdev) for _ in range(2)] if dist else None
     obs_local = [torch.empty(B, nbody, 6, device=dev) for _ in range(2)] if dist else None
     pending = [None, None]
     launches = [0]
@@ -447,7 +464,8 @@ def main():
             evs[i][1].record()
         if dist is not None:  # north star: RCCL all-gather of the observation tensor
             launches[0] += 1
-            pending[k] = dist.all_gather_into_tensor(obs_all[k], obs_local[k], async_op=True)
+            send = obs_local[k].cpu() if gloo else obs_local[k]
+            pending[k] = dist.all_gather_into_tensor(obs_all[k], send, async_op=True)
 
     def drain():
         for k in range(2):
@@ -472,7 +490,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ev_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs)
-    tmax = torch.tensor([wall], device=dev, dtype=torch.float64)
+    tmax = torch.tensor([wall], device=cdev, dtype=torch.float64)
     if dist:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     wall = float(tmax.item())
@@ -483,11 +501,11 @@ def main():
         # each rank publishes a checksum of its own obs bits, every rank checks all slices
         last = (launches[0] - 1) % 2
         local = env.observation()
-        sums = torch.zeros(world_size, dtype=torch.int64, device=dev)
-        sums[rank] = obs_checksum(local)
+        sums = torch.zeros(world_size, dtype=torch.int64, device=cdev)
+        sums[rank] = obs_checksum(local).to(cdev)
         dist.all_reduce(sums)
-        got = torch.stack([obs_checksum(obs_all[last][r * B:(r + 1) * B]) for r in range(world_size)])
-        bad = torch.tensor([int((got != sums).sum().item())], dtype=torch.int64, device=dev)
+        got = torch.stack([obs_checksum(obs_all[last][r * B:(r + 1) * B]) for r in range(world_size)]).to(cdev)
+        bad = torch.tensor([int((got != sums).sum().item())], dtype=torch.int64, device=cdev)
         dist.all_reduce(bad)
         gather = "ok (%d slices checked on every rank)" % world_size if int(bad.item()) == 0 else "MISMATCH"
         if a.dump_gather and rank == 0:
@@ -517,12 +535,15 @@ def main():
             "substeps_per_launch": a.substeps,
             "autoreset_on_error": True,
             "library": library_build(),
+            "library_path": a.lib or "parallax_amd/_lib/libcotix_amd.so",
             "kernel_variant": scen.world.scene.variant(),
+            "prng_layout": a.prng_layout,
             "episode_restarts": resets,
             "restarts_per_env_step": resets / (B * a.substeps * (a.steps + a.warmup)),
-            "parallelism": "dp%d (independent env shards by global env id, RCCL obs all-gather)" % world_size,
+            "parallelism": "dp%d (independent env shards by global env id, %s obs all-gather)"
+                           % (world_size, "gloo (host)" if gloo else "RCCL"),
         },
-        "roofline": roofline(a.scenario, B, a.substeps, launch_ms, nbody),
+        "roofline": roofline(a.scenario, B, a.substeps, launch_ms, nbody, a.prng_layout),
     }
     if gather is not None:
         out["config"]["obs_all_gather_check"] = gather

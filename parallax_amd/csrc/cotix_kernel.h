@@ -87,6 +87,7 @@ struct SceneHdr {
   uint16_t o_ci, o_cj, o_cbeg, o_ccnt, o_tn1, o_tn2, o_cand;
   uint16_t o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts, part ids
   uint16_t o_cmask;  // per cell nmw words: bitmask of the cell's distinct contacts
+  uint16_t o_cbody;  // per contact: the bodies of its two parts (body_a | body_b << 8)
   uint16_t nmw;      // contact-mask words = ceil(nc / 32)
   uint16_t poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
   uint16_t rcp_all;  // 1: every mass and inertia has an exact reciprocal (o_rcp): resolutions multiply
@@ -1236,6 +1237,116 @@ CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, in
         t.w(c.L.err, e) |= er;
 #endif
       }
+    }
+  }
+}
+// phases A, T and B as ONE phase for the forward programs of analytic
+// (circle / AABB) scenes.  Circles and AABBs transform by translation only
+// (cotix/_convex_shapes.py:37-41,113-117), so a contact item builds both world
+// parts itself from the launch-constant local geometry and its bodies'
+// post-Euler positions -- p + v dt, phase A's expression on the same
+// operands -- instead of reading phase T's world parts: every LDS read of the
+// phase (descriptors, bodies, local geometry, the pre-Euler state) is issued
+// before phase A's writes, one round trip for the three phases, and the
+// world parts are never stored (no forward phase of these scenes reads them).
+// The phase's per-lane registers between its three stages (fetch, phase A,
+// contacts): on the GPU they stay in VGPRs (WaveRun::staged runs the stages
+// back to back on the lane); the host emulation keeps one per lane.
+constexpr int ABQ = 4;  // chunks of 64 items prefetched (RoboCup: 160 items, 3 chunks)
+struct ABRegs {
+  uint32_t dw[ABQ], bw[ABQ];
+  float ga[ABQ][4], gb[ABQ][4], pa[ABQ][4], pb[ABQ][4];  // local geometry; px, py, vx, vy of the bodies
+};
+template <int EW>
+CX_DEV int ab_chunks(const KArgs& a, const Ctx& c) {
+  return (a.stages & COTIX_STAGE_COLLIDER) ? (c.nc * EW + WAVE - 1) / WAVE : 0;
+}
+// stage 1: every LDS read of the phase (the pre-Euler state)
+template <int EW>
+CX_DEV void ab_fetch(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, ABRegs& r) {
+  const SceneHdr& sc = c.sh;
+  const int ni = c.nc * EW, nch = ab_chunks<EW>(a, c);
+#pragma unroll
+  for (int q = 0; q < ABQ; ++q) {
+    if (q >= nch) continue;  // uniform
+    const int w0 = q * WAVE + lane, w = w0 < ni ? w0 : ni - 1;  // clamped: every read in range
+    r.dw[q] = t.tb[sc.o_cdesc + 2 * (w / EW)];
+    r.bw[q] = t.tb[sc.o_cbody + w / EW];
+  }
+#pragma unroll
+  for (int q = 0; q < ABQ; ++q) {
+    if (q >= nch) continue;
+    const int w0 = q * WAVE + lane, w = w0 < ni ? w0 : ni - 1, e = w % EW;
+    // analytic scenes: a part's world offset is its local-geometry offset (4 words per part)
+    const int la = c.L.geo + (int)(r.dw[q] & 1023u), lb = c.L.geo + (int)((r.dw[q] >> 10) & 1023u);
+    const int oa = c.L.dyn + 6 * (int)(r.bw[q] & 255u), ob = c.L.dyn + 6 * (int)((r.bw[q] >> 8) & 255u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r.ga[q][k] = t.f(la + k, e);
+      r.gb[q][k] = t.f(lb + k, e);
+      r.pa[q][k] = t.f(oa + k, e);
+      r.pb[q][k] = t.f(ob + k, e);
+    }
+  }
+}
+// stage 3: the contacts from the fetched words
+template <int EW>
+CX_DEV void ab_contacts(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, const ABRegs& r) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const int ni = c.nc * EW, nch = ab_chunks<EW>(a, c);
+  const bool eul = (a.stages & COTIX_STAGE_EULER) != 0;
+#pragma unroll
+  for (int q = 0; q < ABQ; ++q) {
+    if (q >= nch) continue;
+    const int w = q * WAVE + lane, e = w % EW, ci = w / EW;
+    if (w >= ni || env0 + e >= a.B) continue;
+    CXK_STAT(b_items, 1);
+    const uint32_t dw = r.dw[q];
+    Shape A, Bs;
+    A.kind = (int)((dw >> 23) & 3u);
+    Bs.kind = (int)((dw >> 25) & 3u);
+    A.n = Bs.n = 0;
+    // post-Euler positions (euler_item: p + v * dt) and the translate-only
+    // transforms of phase T (circle: (r, cx + px, cy + py); AABB: lo + p, up + p)
+    const float* pa = r.pa[q];
+    const float* pb = r.pb[q];
+    const float* ga = r.ga[q];
+    const float* gb = r.gb[q];
+    const float pxa = eul ? pa[0] + pa[2] * a.dt : pa[0], pya = eul ? pa[1] + pa[3] * a.dt : pa[1];
+    const float pxb = eul ? pb[0] + pb[2] * a.dt : pb[0], pyb = eul ? pb[1] + pb[3] * a.dt : pb[1];
+    const bool ca = A.kind == KIND_CIRCLE, cb = Bs.kind == KIND_CIRCLE;
+#pragma unroll
+    for (int k = 0; k < 2 * MAXV; ++k) A.w[k] = Bs.w[k] = 0.0f;
+    A.w[0] = ca ? ga[0] : ga[0] + pxa;
+    A.w[1] = ca ? ga[1] + pxa : ga[1] + pya;
+    A.w[2] = ca ? ga[2] + pya : ga[2] + pxa;
+    A.w[3] = ca ? ga[3] : ga[3] + pya;
+    Bs.w[0] = cb ? gb[0] : gb[0] + pxb;
+    Bs.w[1] = cb ? gb[1] + pxb : gb[1] + pyb;
+    Bs.w[2] = cb ? gb[2] + pyb : gb[2] + pxb;
+    Bs.w[3] = cb ? gb[3] : gb[3] + pyb;
+    uint32_t er = 0u;
+    const Contact ct = run_contact_set<FNS_ANALYTIC>((int)((dw >> 20) & 7u), A, Bs, narrow_of(sc), &er,
+                                                     ((dw >> 27) & 1u) != 0u);
+    const int co = c.L.con + 4 * ci;
+    t.f(co + 0, e) = ct.pen.x;
+    t.f(co + 1, e) = ct.pen.y;
+    t.f(co + 2, e) = ct.cp.x;
+    t.f(co + 3, e) = ct.cp.y;
+    if (!(isn(ct.cp.x) || isn(ct.cp.y))) {
+#if defined(__HIP__) || defined(__HIPCC__)
+      atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
+#else
+      t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
+#endif
+    }
+    if (er) {
+#if defined(__HIP__) || defined(__HIPCC__)
+      atomicOr(&t.w(c.L.err, e), er);
+#else
+      t.w(c.L.err, e) |= er;
+#endif
     }
   }
 }
@@ -2692,9 +2803,10 @@ enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH
 // ---------------------------------------------------------------------------
 // kso: tile offset of this step's sk0 (skt follows): the key window slot, or
 // L.sk0 where phase A splits the keys (backward re-play)
-template <int EW, int FNSET, bool PRE, class R>
+// AB: phases A, T and B ran as one (ab_fetch / ph_A / ab_contacts, analytic forward programs)
+template <int EW, int FNSET, bool PRE, class R, bool AB = false>
 CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso) {
-  if (!CXK_SKIP(a, 1)) {
+  if (!AB && !CXK_SKIP(a, 1)) {
     run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
     if (FNSET != FNS_ANALYTIC && c.sh.nvt > 0) {
       // the rebuild flags of TV0 and the chunks they make run, wave-uniform:
@@ -2737,7 +2849,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     const bool pairs = b_pairs<FNSET>() && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the phase barrier
     const int per_round = pairs ? WAVE / 2 : WAVE;
     for (int r = 0; r * per_round < n; ++r) run(PH_B, [&](int l) { ph_BP2<EW, FNSET>(a, c, t, env0, l, r, pairs); });
-  } else if (!CXK_SKIP(a, 2)) {
+  } else if (!AB && !CXK_SKIP(a, 2)) {
     run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
   }
   if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && !CXK_SKIP(a, 2)) {
@@ -2822,8 +2934,21 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       }
     }
     const int kso = c.L.kw + slot * c.L.kww;  // this step's sk0, skt in the key window
-    run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
-    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso);
+    // phases A, T, B as one (circle / AABB scenes whose contact items fit the
+    // phase's ABQ prefetched chunks; uniform)
+    if (FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE) {
+      // stage 1 reads the pre-Euler state: every read is issued before phase
+      // A's writes (stage 2); stage 3 computes the contacts
+      run.template staged<ABRegs>(
+          PH_B, [&](int l, ABRegs& r) { ab_fetch<EW>(a, c, t, l, r); },
+          [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); },
+          [&](int l, const ABRegs& r) { ab_contacts<EW>(a, c, t, env0, l, r); });
+      if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true, R, FNSET == FNS_ANALYTIC>(
+          a, c, t, env0, run, slot, kso);
+    } else {
+      run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
+      if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso);
+    }
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {

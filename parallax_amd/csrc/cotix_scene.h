@@ -288,6 +288,11 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
                   ((uint32_t)(pa == pb) << 27));  // a part paired with itself: penetration never used
     hot.push_back((uint32_t)part_nv[pa] | ((uint32_t)part_nv[pb] << 8) | ((uint32_t)pa << 16) | ((uint32_t)pb << 24));
   }
+  {  // per contact the bodies of its two parts (phase AB of the analytic programs)
+    std::vector<int> cb(s.nc);
+    for (int c = 0; c < s.nc; ++c) cb[c] = part_bodyv[cpa[c]] | (part_bodyv[cpb[c]] << 8);
+    put(s.o_cbody, cb);
+  }
   s.nmw = (s.nc + 31) / 32;
   std::vector<int> ci, cj, cbeg, ccnt;
   std::vector<uint32_t> cmask;

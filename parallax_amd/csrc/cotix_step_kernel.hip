@@ -26,9 +26,21 @@ using cxl::WPB;
 #ifdef COTIX_PHASE_PROF
 __device__ unsigned long long g_phase_cycles[cxk::PH_COUNT];
 #endif
-// one phase on this lane, then wave-local ordering before the next phase
+// one phase on this lane, then wave-local ordering before the next phase.
+// staged(ph, fetch, mid, finish): a phase of three stages whose per-lane
+// state S passes from the first to the last in registers (the host emulation
+// runs each stage for all lanes before the next, cxk::ph_AB)
 struct WaveRun {
   int lane;
+  template <class S, class F1, class F2, class F3>
+  __device__ __forceinline__ void staged(int ph, F1 fetch, F2 mid, F3 finish) const {
+    (*this)(ph, [&](int l) {
+      S s;
+      fetch(l, s);
+      mid(l);
+      finish(l, s);
+    });
+  }
 #ifdef COTIX_PHASE_PROF
   unsigned long long* acc;  // per-phase cycle accumulators (registers after inlining)
   template <class F>

@@ -28,6 +28,16 @@ struct HostRun {
   void operator()(int, F f) const {
     for (int l = 0; l < cxk::WAVE; ++l) f(l);
   }
+  // a phase of three stages with per-lane state (WaveRun::staged keeps it in
+  // registers): each stage runs for all lanes before the next, as the GPU's
+  // lanes run the stages' instructions in lockstep
+  template <class S, class F1, class F2, class F3>
+  void staged(int, F1 fetch, F2 mid, F3 finish) const {
+    std::vector<S> s(cxk::WAVE);
+    for (int l = 0; l < cxk::WAVE; ++l) fetch(l, s[l]);
+    for (int l = 0; l < cxk::WAVE; ++l) mid(l);
+    for (int l = 0; l < cxk::WAVE; ++l) finish(l, s[l]);
+  }
 };
 
 // one wave at a time (waves are independent), through the kernel's own

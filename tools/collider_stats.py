@@ -35,7 +35,7 @@ def main():
     from cotix_oracle import prng
     lib = ctypes.CDLL(LIB)
     real = emu.load()  # the plain build: borrow its ctypes signatures
-    for name in ("emu_scene_create", "emu_step"):
+    for name in ("emu_scene_create", "emu_scene_create_ex", "emu_step"):
         getattr(lib, name).argtypes = getattr(real, name).argtypes
     lib.emu_last_error.restype = ctypes.c_char_p
     B = a.envs

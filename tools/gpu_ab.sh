@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-ab}; mkdir -p $O
 for r in $(seq 1 ${REP:-2}); do
   for L in $LIBS; do
-    COTIX_AMD_LIB=$PWD/parallax_amd/_lib/$L timeout -k 10 200 python bench.py $ARGS --cpu-baseline off --extras off > $O/ab_${L}_$r.json 2> $O/ab.err || { tail $O/ab.err; exit 1; }
+    timeout -k 10 200 python bench.py --lib parallax_amd/_lib/$L $ARGS --cpu-baseline off --extras off > $O/ab_${L}_$r.json 2> $O/ab.err || { tail $O/ab.err; exit 1; }
     python -c "import json;d=json.load(open('$O/ab_${L}_$r.json'));print('$L', round(d['value']/1e6,1), round(d['roofline']['launch_ms'],4))"
   done
 done

@@ -159,9 +159,11 @@ int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, in
 /* Kernel variant of the scene's launches (no reference counterpart: a tiling
  * choice; every variant computes the same bits).  envs_per_wave: 0 (default,
  * 4) | 1 | 2 | 4 | 8; specialize: 1 (default) lets the two reference scenes
- * use their compile-time-dimension kernels, 0 forces the generic kernel.
- * cotix_scene_variant reports what a launch uses: the tiling and the
- * specialization id (0 generic, 1 RoboCup, 2 LunarLander). */
+ * under the default constants use kernels with their whole scene header as a
+ * compile-time constant, 0 forces the generic kernel.
+ * cotix_scene_variant reports what a step launch uses: the tiling and the
+ * specialization id (0 generic, 1 RoboCup, 2 LunarLander, 3 RoboCup and 4
+ * LunarLander in the partitionable PRNG layout). */
 int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specialize);
 int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec);
 

@@ -77,33 +77,60 @@ static __device__ unsigned long long g_sub_cycles[8];
 // (word offsets below) and copied to LDS once per launch.
 // the scalar header (offsets, counts) travels in the kernel arguments, so
 // phases read it from registers, never from global memory
+//
+// 16-bit fields: the generic kernel keeps the header in scalar registers for
+// the whole launch (every table offset is < MAXHOT, every count < 4096), so
+// packing halves its register footprint.  The fields, in declaration order:
+//   nb, np, nc, nl, nt, G, W, ncand: bodies, parts, contacts, cells, types,
+//     geom / world floats, candidates
+//   d0x, d0y: GJK start direction (constant)
+//   o_*: word offsets of the hot tables; o_cdesc: per contact 2 words (world
+//     offsets of both parts, fn, kinds | vertex counts, part ids); o_cmask: per
+//     cell nmw words (bitmask of the cell's distinct contacts); o_cbody: per
+//     contact the bodies of its two parts (body_a | body_b << 8); o_vit: per
+//     polygon vertex 2 words (part, vertex, count, first item, body | offsets)
+//   nmw: contact-mask words = ceil(nc / 32)
+//   poly: 1 -- the scene has polygon-polygon / AABB-polygon contacts
+//     (deferred contact points)
+//   rcp_all: 1 -- every mass and inertia has an exact reciprocal (o_rcp):
+//     resolutions multiply; rcp_mask: bit b -- body b's do (bodies < 32)
+//   fnset: FNS_* bits of the contact functions the scene uses
+//   nhot: hot-table words; nvt: polygon vertices over all parts (phase T's
+//     vertex items); maxv: the most vertices of any polygon part (0: none);
+//     pminv: max over polygon pairs of the smaller edge count (AABB: 2) --
+//     the broadphase guard's loop bounds
+//   prng .. pc: cotix_params (include/cotix_amd.h) -- PRNG layout (1:
+//     partitionable), GJK steps, EPA iteration cap / circle x polygon /
+//     body-level iterations, Baumgarte factor and divisor, the candidates'
+//     bernoulli p
+// One list (CXK_HDR_FIELDS) declares them, compares headers (hdr_equal) and
+// prints the specializations' constant headers (cotix_spec_hdrs.h).
+#define CXK_HDR_FIELDS(X)                                                                                          \
+  X(uint16_t, nb) X(uint16_t, np) X(uint16_t, nc) X(uint16_t, nl) X(uint16_t, nt) X(uint16_t, G) X(uint16_t, W)   \
+  X(uint16_t, ncand) X(float, d0x) X(float, d0y) X(uint16_t, o_par) X(uint16_t, o_rcp) X(uint16_t, o_pbody)     \
+  X(uint16_t, o_pkind) X(uint16_t, o_pn) X(uint16_t, o_pgoff) X(uint16_t, o_pwoff) X(uint16_t, o_cpa)           \
+  X(uint16_t, o_cpb) X(uint16_t, o_cfn) X(uint16_t, o_ci) X(uint16_t, o_cj) X(uint16_t, o_cbeg) X(uint16_t, o_ccnt) \
+  X(uint16_t, o_tn1) X(uint16_t, o_tn2) X(uint16_t, o_cand) X(uint16_t, o_cdesc) X(uint16_t, o_cmask)          \
+  X(uint16_t, o_cbody) X(uint16_t, nmw) X(uint16_t, poly) X(uint16_t, rcp_all) X(uint16_t, fnset)               \
+  X(uint16_t, nhot) X(uint16_t, nvt) X(uint16_t, o_vit) X(uint32_t, rcp_mask) X(uint16_t, maxv)                 \
+  X(uint16_t, pminv) X(uint16_t, prng) X(uint16_t, gjk_steps) X(uint16_t, epa_cap) X(uint16_t, epa_cp)          \
+  X(uint16_t, epa_body) X(float, baum) X(float, baum_dt) X(float, pc)
 struct SceneHdr {
-  // 16-bit fields: the header lives in scalar registers for the whole launch
-  // (every table offset is < MAXHOT, every count < 4096), so packing halves
-  // its register footprint
-  uint16_t nb, np, nc, nl, nt, G, W, ncand;  // bodies, parts, contacts, cells, types, geom/world floats, candidates
-  float d0x, d0y;                            // GJK start direction (constant)
-  uint16_t o_par, o_rcp, o_pbody, o_pkind, o_pn, o_pgoff, o_pwoff, o_cpa, o_cpb, o_cfn;
-  uint16_t o_ci, o_cj, o_cbeg, o_ccnt, o_tn1, o_tn2, o_cand;
-  uint16_t o_cdesc;  // per contact 2 words: world offsets of both parts, fn, kinds | vertex counts, part ids
-  uint16_t o_cmask;  // per cell nmw words: bitmask of the cell's distinct contacts
-  uint16_t o_cbody;  // per contact: the bodies of its two parts (body_a | body_b << 8)
-  uint16_t nmw;      // contact-mask words = ceil(nc / 32)
-  uint16_t poly;     // 1: the scene has polygon-polygon / AABB-polygon contacts (deferred contact points)
-  uint16_t rcp_all;  // 1: every mass and inertia has an exact reciprocal (o_rcp): resolutions multiply
-  uint16_t fnset;    // FNS_* bits of the contact functions the scene uses (kernel instantiation)
-  uint16_t nhot;
-  uint16_t nvt;      // polygon vertices over all parts (phase T's vertex items)
-  uint16_t o_vit;    // per polygon vertex 2 words (cotix_scene.h): part, vertex, count, first item, body | offsets
-  uint32_t rcp_mask; // bit b: body b's mass and inertia have exact reciprocals (bodies < 32)
-  uint16_t maxv;     // the most vertices of any polygon part (0: none) -- bounds the broadphase guard's loops
-  uint16_t pminv;    // max over polygon pairs of the smaller edge count (AABB: 2) -- the guard's outer loop
-  // cotix_params (include/cotix_amd.h): PRNG layout (1: partitionable), GJK
-  // steps, EPA iteration cap / circle x polygon / body-level iterations,
-  // Baumgarte factor and divisor, the candidates' bernoulli p
-  uint16_t prng, gjk_steps, epa_cap, epa_cp, epa_body;
-  float baum, baum_dt, pc;
+#define CXK_HDR_DECL(T, n) T n;
+  CXK_HDR_FIELDS(CXK_HDR_DECL)
+#undef CXK_HDR_DECL
 };
+// field bits (floats by their bit pattern: -0.0 != 0.0 here)
+CX_HD uint32_t hdr_bits(uint16_t v) { return v; }
+CX_HD uint32_t hdr_bits(uint32_t v) { return v; }
+CX_HD uint32_t hdr_bits(float v) { return __builtin_bit_cast(uint32_t, v); }
+CX_HD bool hdr_equal(const SceneHdr& a, const SceneHdr& b) {
+  bool eq = true;
+#define CXK_HDR_EQ(T, n) eq = eq && hdr_bits(a.n) == hdr_bits(b.n);
+  CXK_HDR_FIELDS(CXK_HDR_EQ)
+#undef CXK_HDR_EQ
+  return eq;
+}
 CX_HD cx::NarrowParams narrow_of(const SceneHdr& h) {
   return cx::NarrowParams{cx::v2{h.d0x, h.d0y}, (int)h.gjk_steps, (int)h.epa_cap, (int)h.epa_cp, (int)h.epa_body};
 }
@@ -113,52 +140,36 @@ struct SceneDev : SceneHdr {
 };
 
 // Scene specializations of the step kernel.  The phases are generic over the
-// scene (body / part / contact / cell counts in the header); for the two
-// reference scenes the launcher picks an instantiation whose header copy has
-// these dimensions as compile-time constants, so every per-item loop has a
-// known trip count (no exec-mask loop control, no index division) and the
-// tile layout folds to constants.  The values are the scene compiler's output
-// for cotix/_robocup.py and cotix/_lunar_lander.py; spec_of() admits a scene
-// only when all of them match.
-struct SceneDims {
-  int nb, np, nc, nl, nt, G, W, nmw, poly, rcp_all, rcp_mask, nvt, maxv, pminv;
-};
-enum : int { SPEC_GENERIC = 0, SPEC_ROBOCUP = 1, SPEC_LUNAR = 2 };
-constexpr SceneDims SPEC_DIMS[3] = {{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-                                    {5, 9, 40, 12, 2, 36, 36, 2, 0, 1, 31, 0, 0, 0},
-                                    {4, 10, 25, 7, 2, 84, 84, 1, 1, 0, 14, 42, 6, 4}};
-CX_HD bool dims_match(const SceneHdr& h, const SceneDims& d) {
-  return h.nb == d.nb && h.np == d.np && h.nc == d.nc && h.nl == d.nl && h.nt == d.nt && h.G == d.G && h.W == d.W &&
-         h.nmw == d.nmw && h.poly == d.poly && h.rcp_all == d.rcp_all && (int)h.rcp_mask == d.rcp_mask &&
-         h.nvt == d.nvt && h.maxv == d.maxv && h.pminv == d.pminv;
-}
+// scene (counts, table offsets and parameters in the header); for the two
+// reference scenes, under the default constants in either PRNG layout, the
+// launcher picks an instantiation whose header is a compile-time constant --
+// every per-item loop has a known trip count (no exec-mask loop control, no
+// index division), the tile layout and every table address fold to
+// immediates, the parameters to literals, and no scalar register holds the
+// header.  The constant headers are the scene compiler's output for
+// cotix/_robocup.py and cotix/_lunar_lander.py (cotix_spec_hdrs.h, written by
+// tools/gen_spec_hdrs.py and checked against the compiler by
+// tests/test_emu_cpu.py); spec_of() admits a scene only when its whole header
+// is bit-identical.
+enum : int { SPEC_GENERIC = 0, SPEC_ROBOCUP = 1, SPEC_LUNAR = 2, SPEC_ROBOCUP_PART = 3, SPEC_LUNAR_PART = 4, SPEC_N = 5 };
+}  // namespace cxk
+#include "cotix_spec_hdrs.h"  // cxk::SPEC_HDRS[SPEC_N]
+namespace cxk {
 CX_HD int spec_of(const SceneHdr& h) {
-  if (dims_match(h, SPEC_DIMS[SPEC_ROBOCUP])) return SPEC_ROBOCUP;
-  if (dims_match(h, SPEC_DIMS[SPEC_LUNAR])) return SPEC_LUNAR;
+  for (int s = 1; s < SPEC_N; ++s)
+    if (hdr_equal(h, SPEC_HDRS[s])) return s;
   return SPEC_GENERIC;
 }
-// the header with the specialization's dimensions as constants (SPEC > 0
-// only for a header that spec_of() mapped to SPEC)
+// the header a SPEC instantiation runs with: the specialization's constant
+// (SPEC > 0 only for a header that spec_of() mapped to SPEC)
 template <int SPEC>
-CX_HD SceneHdr spec_hdr(SceneHdr h) {
+CX_HD SceneHdr spec_hdr(const SceneHdr& h) {
   if constexpr (SPEC != SPEC_GENERIC) {
-    constexpr SceneDims d = SPEC_DIMS[SPEC];
-    h.nb = d.nb;
-    h.np = d.np;
-    h.nc = d.nc;
-    h.nl = d.nl;
-    h.nt = d.nt;
-    h.G = d.G;
-    h.W = d.W;
-    h.nmw = d.nmw;
-    h.poly = d.poly;
-    h.rcp_all = d.rcp_all;
-    h.rcp_mask = d.rcp_mask;
-    h.nvt = d.nvt;
-    h.maxv = d.maxv;
-    h.pminv = d.pminv;
+    constexpr SceneHdr k = SPEC_HDRS[SPEC];
+    return k;
+  } else {
+    return h;
   }
-  return h;
 }
 
 // device judge and control of cotix_eval (include/cotix_amd.h: cotix_judge,
@@ -444,46 +455,89 @@ CX_DEV void cumsum_n(const float* x, int n, float* out) {
   }
 }
 
+// Cross-lane primitives.  On the GPU they are the hardware's; the host
+// emulation (tests/emu/cotix_simt.h) runs a wave's 64 lanes as fibers of the
+// same program and resolves each of these as a collective point, so both run
+// one code path.
+#if !defined(__HIP__)
+}  // namespace cxk
+namespace cxk_simt {
+void sync();
+void lockstep();
+uint64_t ballot(bool p);
+uint32_t bpermute(int src, uint32_t v);
+uint32_t pair_swap(uint32_t v);
+}  // namespace cxk_simt
+namespace cxk {
+#define CXK_WAVE_OP static inline __attribute__((always_inline))
+#else
+#define CXK_WAVE_OP CX_DEV
+#endif
 // wave-local ordering between phases: every lane's LDS traffic of the
 // previous phase is complete and visible to the wave before the next starts.
-CX_DEV void wave_sync() {
-#if defined(__HIP__) || defined(__HIPCC__)
+CXK_WAVE_OP void wave_sync() {
+#if defined(__HIP__)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
+  ::cxk_simt::sync();
+#endif
+}
+// an order point inside a phase: every lane's LDS accesses before it precede
+// every lane's after it.  The GPU's lanes run in lockstep and one wave's LDS
+// operations execute in program order, so it emits nothing there; the host
+// emulation, which runs lanes one after another, waits for the wave.
+CXK_WAVE_OP void lockstep() {
+#if !defined(__HIP__)
+  ::cxk_simt::lockstep();
+#endif
+}
+// 64-bit ballot of p over the wave's active lanes
+CXK_WAVE_OP uint64_t ballot(bool p) {
+#if defined(__HIP__)
+  return (uint64_t)__ballot(p);
+#else
+  return cxk_simt::ballot(p);
+#endif
+}
+// the value v of lane src (ds_bpermute)
+CXK_WAVE_OP uint32_t bpermute(int src, uint32_t v) {
+#if defined(__HIP__)
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+#else
+  return cxk_simt::bpermute(src, v);
+#endif
+}
+// the value v of the lane pair's other lane (DPP quad_perm(1,0,3,2); both
+// lanes of the pair active)
+CXK_WAVE_OP uint32_t pair_swap_u32(uint32_t v) {
+#if defined(__HIP__)
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);
+#else
+  return cxk_simt::pair_swap(v);
+#endif
+}
+CXK_WAVE_OP float pair_swap_f32(float x) { return __builtin_bit_cast(float, pair_swap_u32(__builtin_bit_cast(uint32_t, x))); }
+// an LDS word OR-ed by several lanes of a phase
+CXK_WAVE_OP void lds_or(uint32_t& w, uint32_t v) {
+#if defined(__HIP__)
+  atomicOr(&w, v);
+#else
+  w |= v;  // lanes run one at a time between collective points
 #endif
 }
 
-// 64-bit ballot of flags[lane] != 0 over the wave.  Called convergently (all
-// 64 lanes, top level of a phase) after the flags were written by the
-// previous phase; the host emulation rebuilds it from the LDS flags.
-CX_DEV uint64_t wave_ballot(const uint32_t* flags, int lane) {
-#if defined(__HIP__) || defined(__HIPCC__)
-  return (uint64_t)__ballot(flags[lane] != 0u);
-#else
-  (void)lane;
-  uint64_t m = 0;
-  for (int l = 0; l < WAVE; ++l)
-    if (flags[l] != 0u) m |= 1ull << l;
-  return m;
-#endif
-}
+// 64-bit ballot of flags[lane] != 0 over the wave (flags written by an
+// earlier phase); called convergently
+CX_DEV uint64_t wave_ballot(const uint32_t* flags, int lane) { return ballot(flags[lane] != 0u); }
 CX_DEV int popc64(uint64_t m) { return __builtin_popcountll(m); }
-// the number of lanes whose flag is set, after every lane stored its flag
-// (`mine`) at flags[lane] in this phase: lane WAVE-1 gets it (the host
-// emulation runs that lane last); called convergently at the top level
+// the number of lanes whose flag `mine` is set (every lane gets it); called
+// convergently at the top level of a phase
 CX_DEV int wave_count_stored(const uint32_t* flags, int lane, bool mine) {
-#if defined(__HIP__) || defined(__HIPCC__)
   (void)flags;
   (void)lane;
-  return __builtin_popcountll((uint64_t)__ballot(mine));
-#else
-  (void)mine;
-  int n = 0;
-  if (lane == WAVE - 1)
-    for (int l = 0; l < WAVE; ++l) n += flags[l] != 0u ? 1 : 0;
-  return n;
-#endif
+  return popc64(ballot(mine));
 }
 CX_DEV uint64_t lanes_below(int lane) { return lane == 0 ? 0ull : ((1ull << lane) - 1ull); }
 
@@ -601,22 +655,15 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
 
 // split(key, num)[idx] by a pair of adjacent lanes (h = lane & 1, both
 // active): each lane runs the block of one of the key's two words
-// (cx::split_word, the same block), then the pair swaps words with a DPP
-// move -- half the threefry issue of split_at on the chain's critical path.
-// The host emulation runs lanes one by one, so it takes split_at (the same
-// words).
+// (cx::split_word, the same block), then the pair swaps words (pair_swap) --
+// half the threefry issue of split_at on the chain's critical path.
 // The partitionable layout's split is ONE block (both words), which each
 // lane of the pair runs itself (no exchange).
 CX_DEV cx::key2 split_at_pair(cx::key2 k, uint32_t num, uint32_t idx, int h, bool part) {
   if (part) return cx::threefry(k, 0u, idx);
-#if defined(__HIP__)
   const uint32_t mine = cx::split_word(k, num, 2u * idx + (uint32_t)h);
-  const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp((int)mine, (int)mine, 0xB1, 0xF, 0xF, false);
-  return h ? cx::key2{other, mine} : cx::key2{mine, other};  // quad_perm(1,0,3,2): the pair's other lane
-#else
-  (void)h;
-  return cx::split_at(k, num, idx);
-#endif
+  const uint32_t other = pair_swap_u32(mine);
+  return h ? cx::key2{other, mine} : cx::key2{mine, other};
 }
 
 // phase A: Euler (cotix/_physics_solvers.py:16-33) + driver extras + key chain
@@ -1158,18 +1205,10 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
     t.f(co + 2, e) = ct.cp.x;
     t.f(co + 3, e) = ct.cp.y;
     if (!(isn(ct.cp.x) || isn(ct.cp.y))) {
-#if defined(__HIP__) || defined(__HIPCC__)
-      atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
-#else
-      t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
-#endif
+      lds_or(t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
     }
     if (er) {
-#if defined(__HIP__) || defined(__HIPCC__)
-      atomicOr(&t.w(c.L.err, e), er);
-#else
-      t.w(c.L.err, e) |= er;
-#endif
+      lds_or(t.w(c.L.err, e), er);
     }
   }
 }
@@ -1224,18 +1263,10 @@ CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, in
       t.f(co + 2, e) = ct.cp.x;
       t.f(co + 3, e) = ct.cp.y;
       if (!(isn(ct.cp.x) || isn(ct.cp.y))) {
-#if defined(__HIP__) || defined(__HIPCC__)
-        atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
-#else
-        t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
-#endif
+        lds_or(t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
       }
       if (er) {
-#if defined(__HIP__) || defined(__HIPCC__)
-        atomicOr(&t.w(c.L.err, e), er);
-#else
-        t.w(c.L.err, e) |= er;
-#endif
+        lds_or(t.w(c.L.err, e), er);
       }
     }
   }
@@ -1252,7 +1283,10 @@ CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, in
 // The phase's per-lane registers between its three stages (fetch, phase A,
 // contacts): on the GPU they stay in VGPRs (WaveRun::staged runs the stages
 // back to back on the lane); the host emulation keeps one per lane.
-constexpr int ABQ = 4;  // chunks of 64 items prefetched (RoboCup: 160 items, 3 chunks)
+#ifndef COTIX_AB_CHUNKS  // build-time A/B knob of the tooling (tools/gpu_iter.sh); the release uses 4
+#define COTIX_AB_CHUNKS 4
+#endif
+constexpr int ABQ = COTIX_AB_CHUNKS;  // chunks of 64 items prefetched (RoboCup: 160 items, 3 chunks)
 struct ABRegs {
   uint32_t dw[ABQ], bw[ABQ];
   float ga[ABQ][4], gb[ABQ][4], pa[ABQ][4], pb[ABQ][4];  // local geometry; px, py, vx, vy of the bodies
@@ -1335,18 +1369,10 @@ CX_DEV void ab_contacts(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
     t.f(co + 2, e) = ct.cp.x;
     t.f(co + 3, e) = ct.cp.y;
     if (!(isn(ct.cp.x) || isn(ct.cp.y))) {
-#if defined(__HIP__) || defined(__HIPCC__)
-      atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
-#else
-      t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
-#endif
+      lds_or(t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
     }
     if (er) {
-#if defined(__HIP__) || defined(__HIPCC__)
-      atomicOr(&t.w(c.L.err, e), er);
-#else
-      t.w(c.L.err, e) |= er;
-#endif
+      lds_or(t.w(c.L.err, e), er);
     }
   }
 }
@@ -1433,9 +1459,7 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
     t.ws[c.W.bl_mode] = t.ws[c.W.bl_epa];
     t.ws[c.W.bl_epa] = 0u;
   }
-#if defined(__HIP__)
-  uint32_t nlist = 0u;  // GPU: the B list is compacted here (BP1's work, in-register ballots)
-#endif
+  uint32_t nlist = 0u;  // the B list is compacted here (in-register ballots)
   // BQ chunks at a time: every chunk's descriptors, then every box, are read
   // before any is used (the chunks' LDS latencies overlap)
   for (int base = 0; base < c.W.bl_pad; base += BQ * WAVE) {
@@ -1502,29 +1526,15 @@ CX_DEV void ph_BP0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
       t.ws[c.W.bl_flag + w] = keep;
       kq[q] = keep;
     }
-    (void)kq;  // (the host emulation compacts in BP1)
-#if defined(__HIP__)
 #pragma unroll
-    for (int q = 0; q < BQ; ++q) {  // chunk by chunk, in order: the list BP1 would build
+    for (int q = 0; q < BQ; ++q) {  // chunk by chunk, in item order
       if (base + q * WAVE >= c.W.bl_pad) continue;  // uniform
-      const uint64_t mask = (uint64_t)__ballot(kq[q] != 0u);
+      const uint64_t mask = ballot(kq[q] != 0u);
       if (kq[q] != 0u) t.ws[c.W.bl_list + nlist + popc64(mask & lanes_below(lane))] = (uint32_t)(base + q * WAVE + lane);
       nlist += (uint32_t)popc64(mask);
     }
-#endif
   }
-#if defined(__HIP__)
   if (lane == 0) t.ws[c.W.bl_n] = nlist;
-#endif
-}
-// BP1: append chunk `chunk`'s flagged items to the B list
-template <int EW>
-CX_DEV void ph_BP1(const Ctx& c, Tile<EW> t, int lane, int chunk) {
-  const uint64_t mask = wave_ballot(t.ws + c.W.bl_flag + chunk * WAVE, lane);
-  const uint32_t base = chunk == 0 ? 0u : t.ws[c.W.bl_n];
-  if (t.ws[c.W.bl_flag + chunk * WAVE + lane] != 0u)
-    t.ws[c.W.bl_list + base + popc64(mask & lanes_below(lane))] = (uint32_t)(chunk * WAVE + lane);
-  if (lane == WAVE - 1) t.ws[c.W.bl_n] = base + (uint32_t)popc64(mask);
 }
 // ---------------------------------------------------------------------------
 // GJK + EPA of a polygon pair on a PAIR of adjacent lanes (GPU, polygon-only
@@ -1534,18 +1544,15 @@ CX_DEV void ph_BP1(const Ctx& c, Tile<EW> t, int lane, int chunk) {
 // the same difference bits and then run the same GJK / EPA arithmetic in
 // lockstep (identical values: identical control flow).  Half the support
 // work of the one-lane form on the critical path; each lane keeps its own
-// EPA edge column.  The host emulation runs the one-lane form (the same
-// values); the GPU tests pin this path against the C port.
+// EPA edge column.  The host emulation runs the same pair form (its SIMT
+// runtime resolves the pair exchanges).
 // ---------------------------------------------------------------------------
-#if defined(__HIP__)
 #ifdef COTIX_NO_PAIR_GJK  // A/B tooling builds only
 constexpr bool PAIR_GJK = false;
 #else
 constexpr bool PAIR_GJK = true;
 #endif
-CX_DEV float pair_swap(float x) {  // the value of the pair's other lane (quad_perm 1,0,3,2)
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0xB1, 0xF, 0xF, false));
-}
+CX_DEV float pair_swap(float x) { return pair_swap_f32(x); }
 struct PairSide {
   const cx::Shape& mine;  // A on lane 0, B on lane 1
   int h;
@@ -1604,8 +1611,8 @@ CX_DEV cx::v2 epa_pair(const PairSide& ps, int h, const cx::v2* simplex, int ite
       const int k = 2 * j + h;
       nanidx = (k < ne && isn(dh[j])) ? k : nanidx;
     }
-    const int onan = __builtin_amdgcn_update_dpp(nanidx, nanidx, 0xB1, 0xF, 0xF, false);
-    const int ob = __builtin_amdgcn_update_dpp(b, b, 0xB1, 0xF, 0xF, false);
+    const int onan = (int)pair_swap_u32((uint32_t)nanidx);
+    const int ob = (int)pair_swap_u32((uint32_t)b);
     const float obv = pair_swap(bv);
     const int fn = nanidx < onan ? nanidx : onan;
     const bool mine = bv < obv || (!(obv < bv) && b < ob);  // (no NaN among the live entries here)
@@ -1671,10 +1678,7 @@ CX_DEV bool gjk_epa_pair(const cx::Shape& mine, int h, int na, int nb, const cx:
   *pen = iters + 3 <= 14 ? epa_pair<14>(ps, h, simplex, iters, col) : epa_pair<20>(ps, h, simplex, iters, col);
   return true;
 }
-#else
-constexpr bool PAIR_GJK = false;
-#endif
-// the B list items of the polygon-only program run on lane pairs (GPU)
+// the B list items of the polygon-only program run on lane pairs
 template <int FNSET>
 constexpr bool b_pairs() {
   return PAIR_GJK && FNSET == (FNS_ANALYTIC | FNS_CONVEX);
@@ -1682,7 +1686,6 @@ constexpr bool b_pairs() {
 // item w on the lane pair (lane, lane ^ 1); h = lane & 1
 template <int EW, int FNSET>
 CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int w) {
-#if defined(__HIP__)
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int h = lane & 1;
@@ -1717,10 +1720,7 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
   t.f(co + 1, e) = ct.pen.y;
   t.f(co + 2, e) = ct.cp.x;
   t.f(co + 3, e) = ct.cp.y;
-  if (!(isn(ct.cp.x) || isn(ct.cp.y))) atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
-#else
-  (void)a; (void)c; (void)t; (void)env0; (void)lane; (void)w;
-#endif
+  if (!(isn(ct.cp.x) || isn(ct.cp.y))) lds_or(t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
 }
 // BP2: round r of the B list, one item per lane (lane pairs: b_pairs)
 // pairs: the step's mode (lane pairs pay off when EPA runs -- landers on the
@@ -1850,11 +1850,7 @@ CX_DEV void ph_F3(const Ctx& c, Tile<EW> t, int lane, int b) {
   t.f(co + 2, e) = cp.x;
   t.f(co + 3, e) = cp.y;
   if (!(isn(cp.x) || isn(cp.y))) {
-#if defined(__HIP__) || defined(__HIPCC__)
-    atomicOr(&t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
-#else
-    t.w(c.L.vm + (ci >> 5), e) |= 1u << (ci & 31);
-#endif
+    lds_or(t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
   }
 }
 
@@ -1999,33 +1995,6 @@ CX_DEV uint32_t m0_flag(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
   }
   return flag;
 }
-template <int EW>
-CX_DEV void ph_M0(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
-  const SceneHdr& sc = c.sh;
-  const uint32_t flag = m0_flag<EW>(a, c, t, env0, lane);
-  (void)sc;
-#ifdef COTIX_STATS
-  {
-    static unsigned long long wsum = 0;
-    if (lane == 0) wsum = 0;
-    if (flag) {
-      const int e = lane % EW, l = lane / EW;
-      for (int idx = 0; idx < t.ti(sc.o_ccnt + l); ++idx) {
-        const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
-        const int cid = (cd >> 18) & 511u;
-        if (!(cx::isn(t.f(c.L.con + 4 * cid + 2, e)) || cx::isn(t.f(c.L.con + 4 * cid + 3, e)))) ++wsum;
-      }
-    }
-    if (lane == WAVE - 1) {
-      CXK_STAT(valid_cands, wsum);
-      CXK_STAT(fit64, wsum <= 64 ? 1 : 0);
-    }
-  }
-#endif
-  t.ws[WS_KEEP + lane] = flag;
-  const int n = wave_count_stored(t.ws + WS_KEEP, lane, flag != 0u);  // pending items of round 1
-  if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)n;
-}
 // M1 (n > 0 pending items): every lane draws one candidate: G = 64 / n lanes
 // per pending item, in mask order
 template <int EW>
@@ -2057,11 +2026,6 @@ CX_DEV uint32_t m1_pass(const Ctx& c, Tile<EW> t, int lane, uint64_t pend, int k
   }
   return pass;
 }
-template <int EW>
-CX_DEV void ph_M1(const Ctx& c, Tile<EW> t, int lane, int par, int kso) {
-  const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
-  t.ws[WS_FLAG + lane] = m1_pass<EW>(c, t, lane, pend, kso);
-}
 // M2: lane `lane` settles its own item: the first passing draw of its slot
 // writes the cell, else the scan position advances by G
 template <int EW>
@@ -2085,35 +2049,50 @@ CX_DEV uint32_t m2_keep(const Ctx& c, Tile<EW> t, int lane, uint64_t pend, uint6
   }
   return keep;
 }
-template <int EW>
-CX_DEV void ph_M2(const Ctx& c, Tile<EW> t, int lane, int par) {
-  const uint64_t pend = wave_ballot(t.ws + (par ? WS_KEEP2 : WS_KEEP), lane);
-  const uint64_t pm = wave_ballot(t.ws + WS_FLAG, lane);
-  const uint32_t keep = m2_keep<EW>(c, t, lane, pend, pm);
-  t.ws[(par ? WS_KEEP : WS_KEEP2) + lane] = keep;
-  // the next round's pending count (read after the phase: 0 ends the scan)
-  const int n = wave_count_stored(t.ws + (par ? WS_KEEP : WS_KEEP2), lane, keep != 0u);
-  if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)n;
-}
-#if defined(__HIP__)
-// the whole scan as ONE phase on the GPU: every round's pending items and
-// pass bits are in-register ballots (no flag round trips through LDS, no
-// phase syncs between the draw and the settle); the scan positions and the
-// cells stay in LDS, ordered between rounds by a wave fence.  The same
-// per-lane code as M1 / M2 (the host emulation runs those, phase by phase).
+// the whole scan as ONE phase: every round's pending items and pass bits
+// are in-register ballots (no flag round trips through LDS, no phase syncs
+// between the draw and the settle); the scan positions and the cells stay in
+// LDS, ordered between rounds by a wave fence
 template <int EW>
 CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso) {
   // M0: the active items (each lane its own: its scan position is its own word)
-  uint64_t pend = (uint64_t)__ballot(m0_flag<EW>(a, c, t, env0, lane) != 0u);
+  const uint32_t flag = m0_flag<EW>(a, c, t, env0, lane);
+  uint64_t pend = ballot(flag != 0u);
+#ifdef COTIX_STATS
+  {
+    // the valid candidates of the active items (tools/collider_stats.py)
+    uint64_t nv = 0;
+    if (flag) {
+      const int e = lane % EW, l = lane / EW;
+      for (int idx = 0; idx < t.ti(c.sh.o_ccnt + l); ++idx) {
+        const uint32_t cd = t.tb[c.sh.o_cand + t.ti(c.sh.o_cbeg + l) + idx];
+        const int cid = (cd >> 18) & 511u;
+        if (!(cx::isn(t.f(c.L.con + 4 * cid + 2, e)) || cx::isn(t.f(c.L.con + 4 * cid + 3, e)))) ++nv;
+      }
+    }
+    static uint64_t wsum = 0;
+    if (lane == 0) wsum = 0;
+    wsum += nv;
+    if (lane == WAVE - 1) {
+      CXK_STAT(valid_cands, wsum);
+      CXK_STAT(fit64, wsum <= 64 ? 1 : 0);
+      CXK_STAT(wave_steps, 1);
+      CXK_STAT(active_items, popc64(pend));
+    }
+  }
+#endif
   wave_sync();  // the reset scan positions before the draws read them
-  while (pend != 0ull) {
-    const uint64_t pm = (uint64_t)__ballot(m1_pass<EW>(c, t, lane, pend, kso) != 0u);
+  for (int round = 0; pend != 0ull; ++round) {
+    if (lane == 0) {
+      CXK_STAT(rounds, 1);
+      if (round == 1) CXK_STAT(r1_left, popc64(pend));
+    }
+    const uint64_t pm = ballot(m1_pass<EW>(c, t, lane, pend, kso) != 0u);
     const uint32_t keep = m2_keep<EW>(c, t, lane, pend, pm);
     wave_sync();  // the settled scan positions before the next round's draws read them
-    pend = (uint64_t)__ballot(keep != 0u);
+    pend = ballot(keep != 0u);
   }
 }
-#endif
 
 // phase D: choose_random_contact (cotix/_colliders.py:274-295)
 CX_DEV cx::Params load_par(const uint32_t* tb, int o) {
@@ -2810,18 +2789,12 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
     if (FNSET != FNS_ANALYTIC && c.sh.nvt > 0) {
       // the rebuild flags of TV0 and the chunks they make run, wave-uniform:
-      // computed once for TV1-TV4.  On the GPU TV0 runs in TV1's phase (the
-      // flags are ballot from each lane's own word; TV1 reads none of TV0's
-      // other words); the host emulation keeps it a phase of its own
+      // computed once for TV1-TV4.  TV0 runs in TV1's phase (the flags are
+      // ballot from each lane's own word; TV1 reads none of TV0's other words)
       uint64_t redo = 0ull;
       uint32_t runs = 0u;
-#if !defined(__HIP__)
-      run(PH_TV0, [&](int l) { ph_TV0<EW>(a, c, t, env0, l); });
-#endif
       run(PH_TV1, [&](int l) {
-#if defined(__HIP__)
         ph_TV0<EW>(a, c, t, env0, l);
-#endif
         redo = tv_redo_mask<EW>(c, t, l);
         runs = tv_chunks<EW>(c, t, redo);
         ph_TV1<EW>(a, c, t, env0, l, redo, runs);
@@ -2830,9 +2803,10 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_TV3, [&](int l) { ph_TV3<EW>(a, c, t, env0, l, redo, runs); });
       if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !CXK_SKIP(a, 2))
         run(PH_TV3, [&](int l) { ph_TV4<EW>(a, c, t, env0, l, redo, runs); });
-#if !defined(__HIP__)
-      // host emulation (tests): the vertex items die with phase T -- poison
-      // them so that a later step reading stale ones cannot pass by luck
+#ifdef COTIX_EMU_POISON
+      // test instrumentation (the host emulation's build): the vertex items
+      // die with phase T -- poison them so that a later step reading stale
+      // ones cannot pass by luck
       run(PH_TV3, [&](int l) {
         for (int q = l; q < 3 * c.sh.nvt * EW; q += WAVE) t.ws[c.W.vt + q] = 0x7FBADBADu;
       });
@@ -2841,9 +2815,6 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
   }
   if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !CXK_SKIP(a, 2)) {
     run(PH_BP0, [&](int l) { ph_BP0<EW>(a, c, t, env0, l); });
-#if !defined(__HIP__)  // (the GPU's BP0 compacts the list itself)
-    for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_BP1, [&](int l) { ph_BP1<EW>(c, t, l, ch); });
-#endif
     const int n = (int)t.ws[c.W.bl_n];  // uniform: read after the phase barrier
     CXK_STAT(b_items, 0);
     const bool pairs = b_pairs<FNSET>() && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the phase barrier
@@ -2869,19 +2840,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     }
   }
   if (!CXK_SKIP(a, 4) && c.nl > 0 && c.nl * EW <= WAVE) {
-#if defined(__HIP__)
     run(PH_C1, [&](int l) { ph_M_fused<EW>(a, c, t, env0, l, kso); });
-#else
-    run(PH_C0, [&](int l) { ph_M0<EW>(a, c, t, env0, l); });
-    CXK_STAT(wave_steps, 1);
-    for (int par = 0; t.ws[WS_N] != 0u; par ^= 1) {  // uniform: read after the phase barrier
-      CXK_STAT(rounds, 1);
-      if (par == 0) CXK_STAT(active_items, t.ws[WS_N]);
-      if (par == 1) CXK_STAT(r1_left, t.ws[WS_N]);
-      run(PH_C1, [&](int l) { ph_M1<EW>(c, t, l, par, kso); });
-      run(PH_C2, [&](int l) { ph_M2<EW>(c, t, l, par); });
-    }
-#endif
   } else if (!CXK_SKIP(a, 4) && c.nl > 0) {
     for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {
       run(PH_C0, [&](int l) { ph_C0<EW>(a, c, t, env0, l, ch); });

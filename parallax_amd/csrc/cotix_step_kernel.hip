@@ -28,8 +28,9 @@ __device__ unsigned long long g_phase_cycles[cxk::PH_COUNT];
 #endif
 // one phase on this lane, then wave-local ordering before the next phase.
 // staged(ph, fetch, mid, finish): a phase of three stages whose per-lane
-// state S passes from the first to the last in registers (the host emulation
-// runs each stage for all lanes before the next, cxk::ph_AB)
+// state S passes from the first to the last in registers, every lane's
+// stage before every lane's next (lockstep: nothing on the GPU, an order
+// point of the host emulation's fibers); the emulation's HostRun is this
 struct WaveRun {
   int lane;
   template <class S, class F1, class F2, class F3>
@@ -37,7 +38,9 @@ struct WaveRun {
     (*this)(ph, [&](int l) {
       S s;
       fetch(l, s);
+      cxk::lockstep();
       mid(l);
+      cxk::lockstep();
       finish(l, s);
     });
   }
@@ -59,8 +62,11 @@ struct WaveRun {
     asm volatile(";#PHASE_END %0" ::"s"(ph));
   }
 #else
+  // lockstep: the wave-uniform reads between phases precede the phase (a
+  // no-op on the GPU, an order point of the host emulation's fibers)
   template <class F>
   __device__ __forceinline__ void operator()(int, F f) const {
+    cxk::lockstep();
     f(lane);
     cxk::wave_sync();
   }
@@ -73,7 +79,8 @@ template <int EW, int FNSET, int MODE, int SPEC = cxk::SPEC_GENERIC>
 __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   extern __shared__ uint32_t lds[];
   const SceneDev* sc = a.sc;
-  const int nhot = a.sh.nhot;
+  const cxk::SceneHdr sh = cxk::spec_hdr<SPEC>(a.sh);  // a constant for SPEC > 0
+  const int nhot = sh.nhot;
   // the scene tables into LDS: HC reads per thread issued before any store
   // (one global round trip per HC * 256 words, not one per 256)
   constexpr int HC = 16;
@@ -90,7 +97,7 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
       if (i < nhot) lds[i] = r[k];
     }
   }
-  const cxk::Ctx c = cxk::make_ctx<EW>(cxk::spec_hdr<SPEC>(a.sh));
+  const cxk::Ctx c = cxk::make_ctx<EW>(sh);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int env0 = (blockIdx.x * WPB + wave) * EW;
   uint32_t* wbase = lds + nhot + wave * (c.L.S * EW + c.W.words);
@@ -151,6 +158,15 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
   }
   if (spec == cxk::SPEC_LUNAR && mode == 0 && F == F_PP) {
     COTIX_LAUNCH_SPEC(F_PP, 0, cxk::SPEC_LUNAR);
+    return hipGetLastError();
+  }
+  // the partitionable layout's specializations: the step program only
+  if (spec == cxk::SPEC_ROBOCUP_PART && mode == 0 && F == F_AN) {
+    COTIX_LAUNCH_SPEC(F_AN, 0, cxk::SPEC_ROBOCUP_PART);
+    return hipGetLastError();
+  }
+  if (spec == cxk::SPEC_LUNAR_PART && mode == 0 && F == F_PP) {
+    COTIX_LAUNCH_SPEC(F_PP, 0, cxk::SPEC_LUNAR_PART);
     return hipGetLastError();
   }
 #else

@@ -15,6 +15,10 @@ from .params import CotixParams, Params
 from .shapes import AbstractPolygon
 
 
+# the step kernel's scene specializations (cxk::SPEC_*, cotix_kernel.h)
+SPECIALIZATIONS = ("generic", "robocup", "lunar", "robocup_partitionable", "lunar_partitionable")
+
+
 class Scene:
     """cotix_scene_create_ex: the collider's trace-time enumeration
     (cotix/_colliders.py:86-131) compiled once into device tables, with the
@@ -67,13 +71,15 @@ class Scene:
                    "cotix_scene_set_variant")
 
     def variant(self):
-        """What a launch uses: {"envs_per_wave": EW, "specialization": 0
-        generic | 1 RoboCup | 2 LunarLander}."""
+        """What a step launch uses: {"envs_per_wave": EW, "specialization":
+        one of SPECIALIZATIONS} -- the reference scenes under the default
+        constants get a kernel with their whole header folded in, per PRNG
+        layout."""
         import ctypes
         ew, sp = ctypes.c_int(), ctypes.c_int()
         _ffi.check(_ffi.lib.cotix_scene_variant(self.handle, ctypes.byref(ew), ctypes.byref(sp)),
                    "cotix_scene_variant")
-        return {"envs_per_wave": ew.value, "specialization": ["generic", "robocup", "lunar"][sp.value]}
+        return {"envs_per_wave": ew.value, "specialization": SPECIALIZATIONS[sp.value]}
 
     def __del__(self):
         h = getattr(self, "handle", None)

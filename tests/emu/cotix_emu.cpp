@@ -1,11 +1,14 @@
 // TEST INFRASTRUCTURE ONLY -- host emulation of the fused HIP step kernel.
 //
-// Compiles parallax_amd/csrc/cotix_kernel.h (the kernel's phase functions)
-// for the host and runs every phase for all BLK lanes of every workgroup in
-// turn, which is what the __syncthreads() between phases guarantees on the
-// GPU.  Used to (a) check the kernel logic against the oracle on CPU and
-// (b) run it under AddressSanitizer/UBSan (GPU sanitizers are unavailable).
+// Compiles parallax_amd/csrc/cotix_kernel.h (the kernel's phase functions and
+// wave programs) for the host and runs each wave's program on 64 lanes as
+// SIMT fibers (cotix_simt.h): the GPU's own code path, its cross-lane
+// operations (ballots, permutes, pair exchanges) and phase barriers resolved
+// as collective points.  Used to (a) check the kernel logic against the
+// oracle on CPU and (b) run it under AddressSanitizer/UBSan (GPU sanitizers
+// are unavailable).
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -13,6 +16,7 @@
 #include "../../parallax_amd/csrc/cotix_body.h"
 #include "../../parallax_amd/csrc/cotix_kernel.h"
 #include "../../parallax_amd/csrc/cotix_scene.h"
+#include "cotix_simt.h"
 
 namespace {
 std::string g_err;
@@ -21,27 +25,34 @@ struct EmuScene {
   int n_cand = 0, fnset = 0;
 };
 
-// a phase runs for all 64 lanes of the wave before the next starts (what
-// wave_sync() guarantees on the GPU)
+// the lane's phase runner: the GPU's WaveRun (cotix_step_kernel.hip) -- an
+// order point (every lane's wave-uniform reads between phases precede every
+// lane's next phase), the phase on this lane, then the wave barrier; staged
+// phases keep their state in the lane's own frame and order their stages by
+// lockstep points
 struct HostRun {
+  int lane;
   template <class F>
   void operator()(int, F f) const {
-    for (int l = 0; l < cxk::WAVE; ++l) f(l);
+    cxk::lockstep();
+    f(lane);
+    cxk::wave_sync();
   }
-  // a phase of three stages with per-lane state (WaveRun::staged keeps it in
-  // registers): each stage runs for all lanes before the next, as the GPU's
-  // lanes run the stages' instructions in lockstep
   template <class S, class F1, class F2, class F3>
-  void staged(int, F1 fetch, F2 mid, F3 finish) const {
-    std::vector<S> s(cxk::WAVE);
-    for (int l = 0; l < cxk::WAVE; ++l) fetch(l, s[l]);
-    for (int l = 0; l < cxk::WAVE; ++l) mid(l);
-    for (int l = 0; l < cxk::WAVE; ++l) finish(l, s[l]);
+  void staged(int ph, F1 fetch, F2 mid, F3 finish) const {
+    (*this)(ph, [&](int l) {
+      S s;
+      fetch(l, s);
+      cxk::lockstep();
+      mid(l);
+      cxk::lockstep();
+      finish(l, s);
+    });
   }
 };
 
 // one wave at a time (waves are independent), through the kernel's own
-// wave programs (cxk::run_wave / run_wave_backward)
+// wave programs (cxk::run_wave / run_wave_backward) on 64 fiber lanes
 template <int EW>
 void run_blocks(const cxk::KArgs& a, int mode) {
   const cxk::SceneDev& sc = *a.sc;
@@ -54,22 +65,25 @@ void run_blocks(const cxk::KArgs& a, int mode) {
     const cxk::Tile<EW> t{lds.data() + sc.nhot, lds.data(), lds.data() + sc.nhot + (size_t)c.L.S * EW};
     // the kernel instantiation the library launches (cxk::launch_fnset)
     const int F = cxk::launch_fnset(sc.fnset, mode);
-    if (mode == 2)
-      cxk::run_wave_backward<EW, 1>(a, c, t, wv * EW, HostRun{});
-    else if (mode == 1)
-      F == 1 ? cxk::run_wave<EW, 1, true>(a, c, t, wv * EW, HostRun{})
-             : cxk::run_wave<EW, 15, true>(a, c, t, wv * EW, HostRun{});
-    else if (mode == 3)
-      F == 1 ? cxk::run_wave<EW, 1, false, true>(a, c, t, wv * EW, HostRun{})
-             : cxk::run_wave<EW, 15, false, true>(a, c, t, wv * EW, HostRun{});
-    else if (F == 1)
-      cxk::run_wave<EW, 1, false>(a, c, t, wv * EW, HostRun{});
-    else if (F == 3)
-      cxk::run_wave<EW, 3, false>(a, c, t, wv * EW, HostRun{});
-    else if (F == 11)
-      cxk::run_wave<EW, 11, false>(a, c, t, wv * EW, HostRun{});
-    else
-      cxk::run_wave<EW, 15, false>(a, c, t, wv * EW, HostRun{});
+    const int env0 = wv * EW;
+    cxk_simt::run([&](int lane) {
+      const HostRun run{lane};
+      if (mode == 2)
+        cxk::run_wave_backward<EW, 1>(a, c, t, env0, run);
+      else if (mode == 1)
+        F == 1 ? cxk::run_wave<EW, 1, true>(a, c, t, env0, run) : cxk::run_wave<EW, 15, true>(a, c, t, env0, run);
+      else if (mode == 3)
+        F == 1 ? cxk::run_wave<EW, 1, false, true>(a, c, t, env0, run)
+               : cxk::run_wave<EW, 15, false, true>(a, c, t, env0, run);
+      else if (F == 1)
+        cxk::run_wave<EW, 1, false>(a, c, t, env0, run);
+      else if (F == 3)
+        cxk::run_wave<EW, 3, false>(a, c, t, env0, run);
+      else if (F == 11)
+        cxk::run_wave<EW, 11, false>(a, c, t, env0, run);
+      else
+        cxk::run_wave<EW, 15, false>(a, c, t, env0, run);
+    });
   }
 }
 void run_any(const cxk::KArgs& a, int E, int mode) {
@@ -417,6 +431,32 @@ extern "C" int emu_scene_dims(void* scene, int* out) {
 }
 // the step-kernel specialization the launcher picks for the scene (cxk::spec_of)
 extern "C" int emu_scene_spec(void* scene) { return cxk::spec_of(static_cast<EmuScene*>(scene)->s); }
+
+// the scene's header as a C++ initializer in declaration order (floats as
+// exact hex literals): tools/gen_spec_hdrs.py writes the specializations'
+// constant headers (cotix_spec_hdrs.h) from it; returns the length, -1 if
+// buf is too small
+static void hdr_put(std::string& o, const char* name, uint16_t v) { o += std::string("/*") + name + "*/ " + std::to_string(v) + ", "; }
+static void hdr_put(std::string& o, const char* name, uint32_t v) {
+  o += std::string("/*") + name + "*/ " + std::to_string(v) + "u, ";
+}
+static void hdr_put(std::string& o, const char* name, float v) {
+  char b[64];
+  std::snprintf(b, sizeof b, "%af", (double)v);
+  o += std::string("/*") + name + "*/ " + b + ", ";
+}
+extern "C" int emu_scene_hdr_text(void* scene, char* buf, int n) {
+  const cxk::SceneHdr& h = static_cast<EmuScene*>(scene)->s;
+  std::string o = "{";
+#define EMU_HDR_PUT(T, f) hdr_put(o, #f, h.f);
+  CXK_HDR_FIELDS(EMU_HDR_PUT)
+#undef EMU_HDR_PUT
+  o.resize(o.size() - 2);
+  o += "}";
+  if ((int)o.size() + 1 > n) return -1;
+  std::memcpy(buf, o.c_str(), o.size() + 1);
+  return (int)o.size();
+}
 // LDS bytes of the step kernel's workgroup (cxk::lds_bytes, 4 waves) for the scene at `ew` envs per wave
 extern "C" long emu_lds_bytes(void* scene, int ew) {
   return (long)cxk::lds_bytes(static_cast<EmuScene*>(scene)->s, 4, ew);

@@ -118,6 +118,11 @@ def test_scene_variant_api():
     assert s.variant()["envs_per_wave"] == 4
     with pytest.raises(RuntimeError, match="envs_per_wave"):
         s.set_variant(3)
+    # the specializations fold the whole header: the default constants per PRNG layout
+    s = pa.Scene(pa.scenarios.robocup_bodies(), params=pa.Params(prng_layout="partitionable"))
+    assert s.variant()["specialization"] == "robocup_partitionable"
+    s = pa.Scene(pa.scenarios.robocup_bodies(), params=pa.Params(contact_p=0.25))
+    assert s.variant()["specialization"] == "generic"
 
 
 def test_eval_rejects_reset_mode2_without_judge_and_overflow():

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 GOLD = os.path.join(HERE, "golden")
 sys.path.insert(0, os.path.join(HERE, "emu"))
 sys.path.insert(0, GOLD)
@@ -347,16 +348,32 @@ def test_emu_lunar_restarts_move_static_body_vs_cport(emu_lib, EW, bp):
 
 
 def test_reference_scenes_get_their_specializations(emu_lib):
-    """The two reference scenes compile to the dimensions of their step-kernel
-    specializations (cxk::SPEC_DIMS): a scene-compiler change that moved them
-    would silently fall back to the generic kernel."""
+    """The two reference scenes, under the default constants in either PRNG
+    layout, compile to the constant headers of their step-kernel
+    specializations (cxk::SPEC_HDRS): a scene-compiler change that moved them
+    would silently fall back to the generic kernel.  Any other constant set
+    runs the generic kernel."""
     emu, lib = emu_lib
     from cotix_oracle import physics as P
+    from cotix_oracle.params import Params
     lib.emu_scene_spec.argtypes = [ctypes.c_void_p]
-    h, _ = emu.oracle_scene(lib, P.robocup_bodies())
-    assert lib.emu_scene_spec(h) == 1
-    h, _ = emu.oracle_scene(lib, P.lunar_lander_bodies())
-    assert lib.emu_scene_spec(h) == 2
+    for bodies, spec in ((P.robocup_bodies, 1), (P.lunar_lander_bodies, 2)):
+        h, _ = emu.oracle_scene(lib, bodies())
+        assert lib.emu_scene_spec(h) == spec
+        h, _ = emu.oracle_scene(lib, bodies(), Params(prng_layout="partitionable"))
+        assert lib.emu_scene_spec(h) == spec + 2
+        for alt in (dict(contact_p=0.3), dict(gjk_max_steps=31), dict(baumgarte=0.2),
+                    dict(prng_layout="partitionable", epa_max_iters=47)):
+            h, _ = emu.oracle_scene(lib, bodies(), Params(**alt))
+            assert lib.emu_scene_spec(h) == 0, alt
+
+
+def test_specialization_headers_are_current():
+    """parallax_amd/csrc/cotix_spec_hdrs.h is what tools/gen_spec_hdrs.py
+    writes from the current scene compiler (the kernel folds these headers)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_spec_hdrs.py"), "--check"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 def test_reference_scenes_fit_the_lds(emu_lib):

@@ -1283,10 +1283,14 @@ CX_DEV void ph_B_analytic(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, in
 // The phase's per-lane registers between its three stages (fetch, phase A,
 // contacts): on the GPU they stay in VGPRs (WaveRun::staged runs the stages
 // back to back on the lane); the host emulation keeps one per lane.
-#ifndef COTIX_AB_CHUNKS  // build-time A/B knob of the tooling (tools/gpu_iter.sh); the release uses 4
-#define COTIX_AB_CHUNKS 4
+// chunks of 64 items prefetched.  Measured (r04e): with 2 the box world
+// (84 items) runs fused, 1.03x; RoboCup (160 items, 3 chunks) runs A, T, B
+// as phases -- fused it is 0.96x (the fetch holds 3 x 18 words per lane and
+// the contact work no longer overlaps phase A's writes)
+#ifndef COTIX_AB_CHUNKS  // build-time A/B knob of the tooling (tools/gpu_iter.sh)
+#define COTIX_AB_CHUNKS 2
 #endif
-constexpr int ABQ = COTIX_AB_CHUNKS;  // chunks of 64 items prefetched (RoboCup: 160 items, 3 chunks)
+constexpr int ABQ = COTIX_AB_CHUNKS;
 struct ABRegs {
   uint32_t dw[ABQ], bw[ABQ];
   float ga[ABQ][4], gb[ABQ][4], pa[ABQ][4], pb[ABQ][4];  // local geometry; px, py, vx, vy of the bodies
@@ -1959,25 +1963,37 @@ CX_DEV void ph_C3(const Ctx& c, Tile<EW> t, int lane, int par) {
   if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)(kept + (n > WAVE ? n - WAVE : 0));
 }
 
-// Phase C when every (cell, env) item fits one lane (nl * EW <= 64): item
-// id == lane, the pending items are a 64-bit ballot mask (no compaction
-// passes), and each lane updates only its own item's state, so one round is
-// two phases.  Pending flags alternate between WS_KEEP and WS_KEEP2.
-CX_DEV int select_bit(uint64_t m, int k) {  // position of the k-th (0-based) set bit of m
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const uint64_t lo = m & ((1ull << w) - 1ull);
-    const int c = popc64(lo);
-    const bool up = k >= c;
-    k = up ? k - c : k;
-    m = up ? (m >> w) : lo;
-    pos = up ? pos + w : pos;
-  }
-  return pos;
+// Phase C when every (cell, env) item fits one lane (nl * EW <= 64): the
+// whole scan is ONE phase (ph_M_fused).  Item id == lane (its "owner"); the
+// pending items are a 64-bit ballot mask.  Each round gives the n pending
+// items G = 64 / n consecutive lanes ("drawers") in rank order, each drawing
+// the next candidate of its item's scan; the owner then settles its item
+// from the pass ballot: the first passing draw of its G writes the cell
+// (the reference's last passing candidate: the list is in reverse scan
+// order), else its scan position advances by G.  Per-item state (scan
+// position, candidate range, cell address) stays in the owner's registers;
+// the owner publishes its range to its drawers in one LDS word per rank, and
+// the winning candidate word comes back by a lane permute -- per round two
+// dependent LDS round trips before the draws (slot word, candidate word),
+// one permute after, no barrier.
+// (a draw's threefry chain does not wait for the candidate's validity: the
+// contact-point read overlaps it, and a NaN candidate's draw is discarded)
+
+// the uniform lanes-per-item G = 64 / n and the drawer's rank slot = lane / G
+// without integer division: rcp is within 1 ulp, far inside the margins
+// (64 / n is an integer or at least 1/64 from one; (lane + 1/2) / G at least
+// 1/(2G) from one)
+CX_DEV float rcp_approx(float x) {
+#if defined(__HIP__)
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
 }
-// M0: activity (a cell whose distinct contacts are all NaN never writes)
-// the item's activity flag (and its scan position reset when active)
+CX_DEV int lanes_per_item(int n) { return (int)(64.0f * rcp_approx((float)n)); }
+CX_DEV int rank_of_lane(int lane, int G) { return (int)(((float)lane + 0.5f) * rcp_approx((float)G)); }
+
+// M0: the item's activity (a cell whose distinct contacts are all NaN never writes)
 template <int EW>
 CX_DEV uint32_t m0_flag(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   const SceneHdr& sc = c.sh;
@@ -1987,86 +2003,56 @@ CX_DEV uint32_t m0_flag(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
     if (env0 + e < a.B) {
       bool any = false;
       for (int q = 0; q < sc.nmw; ++q) any |= (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
-      if (any) {
-        flag = 1u;
-        t.ws[WS_LIST + 2 * c.nl * EW + lane] = 0u;  // scan position
-      }
+      flag = any ? 1u : 0u;
     }
   }
   return flag;
 }
-// M1 (n > 0 pending items): every lane draws one candidate: G = 64 / n lanes
-// per pending item, in mask order
+// a drawer's candidate: its item's next candidate word (slot word: the
+// item's scan base | end << 13 | id << 26), 0xFFFFFFFF past the item's list;
+// pass: the candidate's bernoulli draw passed and its contact is not NaN
 template <int EW>
-CX_DEV uint32_t m1_pass(const Ctx& c, Tile<EW> t, int lane, uint64_t pend, int kso) {
+CX_DEV uint32_t m_draw(const Ctx& c, Tile<EW> t, uint32_t sw, int q, int kso, bool& pass) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
-  const int n = popc64(pend);
-  uint32_t pass = 0u;
-  if (n > 0) {
-    const int G = WAVE / n, slot = lane / G, q = lane % G;
-    if (slot < n) {
-      const int id = select_bit(pend, slot), e = id % EW, l = id / EW;
-      const int idx = (int)t.ws[WS_LIST + 2 * c.nl * EW + id] + q;
-      if (idx < t.ti(sc.o_ccnt + l)) {
-        const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
-        const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
-        const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
-        CXK_STAT(draws, 1);
-        if (!(isn(cpx) || isn(cpy))) {  // a NaN candidate never writes
-          CXK_STAT(valid_draws, 1);
-          const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
-          const bool part = sc.prng != 0;
-          const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
-          const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
-          pass = bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part) ? 1u : 0u;           // :222-223
-        }
-      }
-    }
-  }
-  return pass;
+  pass = false;
+  const int base = (int)(sw & 8191u), end = (int)((sw >> 13) & 8191u), id = (int)(sw >> 26);
+  const int e = id % EW, idx = base + q;
+  if (idx >= end) return 0xFFFFFFFFu;
+  const uint32_t cd = t.tb[sc.o_cand + idx];
+  const int i1 = cd & 511u, i2 = (cd >> 9) & 511u, cid = (cd >> 18) & 511u, ty = cd >> 27;
+  const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
+  const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
+  const bool part = sc.prng != 0;
+  const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
+  const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
+  const bool valid = !(isn(cpx) || isn(cpy));                                        // a NaN candidate never writes
+  CXK_STAT(draws, 1);
+  CXK_STAT(valid_draws, valid ? 1 : 0);
+  pass = valid && bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part);  // :222-223
+  return cd;
 }
-// M2: lane `lane` settles its own item: the first passing draw of its slot
-// writes the cell, else the scan position advances by G
-template <int EW>
-CX_DEV uint32_t m2_keep(const Ctx& c, Tile<EW> t, int lane, uint64_t pend, uint64_t pm) {
-  const SceneHdr& sc = c.sh;
-  uint32_t keep = 0u;
-  if ((pend >> lane) & 1ull) {
-    const int n = popc64(pend), G = WAVE / n, slot = popc64(pend & lanes_below(lane));
-    const int e = lane % EW, l = lane / EW;
-    const uint64_t gm = G == WAVE ? ~0ull : ((1ull << G) - 1ull);
-    const uint64_t bits = (pm >> (slot * G)) & gm;
-    uint32_t& pos = t.ws[WS_LIST + 2 * c.nl * EW + lane];
-    if (bits != 0ull) {
-      const int idx = (int)pos + __builtin_ctzll(bits);
-      const uint32_t cd = t.tb[sc.o_cand + t.ti(sc.o_cbeg + l) + idx];
-      t.w(c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l), e) = cd;  // the winning candidate word
-    } else {
-      pos = pos + (uint32_t)G;
-      keep = (int)pos < t.ti(sc.o_ccnt + l) ? 1u : 0u;
-    }
-  }
-  return keep;
-}
-// the whole scan as ONE phase: every round's pending items and pass bits
-// are in-register ballots (no flag round trips through LDS, no phase syncs
-// between the draw and the settle); the scan positions and the cells stay in
-// LDS, ordered between rounds by a wave fence
 template <int EW>
 CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso) {
-  // M0: the active items (each lane its own: its scan position is its own word)
+  const SceneHdr& sc = c.sh;
   const uint32_t flag = m0_flag<EW>(a, c, t, env0, lane);
   uint64_t pend = ballot(flag != 0u);
+  // the owner's item: candidate range [cb, ce), scan position, cell word
+  int cb = 0, ce = 0, cell = 0, pos = 0;
+  const int e = lane % EW;
+  if (lane < c.nl * EW) {
+    const int l = lane / EW;
+    cb = t.ti(sc.o_cbeg + l);
+    ce = cb + t.ti(sc.o_ccnt + l);
+    cell = c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l);
+  }
 #ifdef COTIX_STATS
   {
     // the valid candidates of the active items (tools/collider_stats.py)
     uint64_t nv = 0;
     if (flag) {
-      const int e = lane % EW, l = lane / EW;
-      for (int idx = 0; idx < t.ti(c.sh.o_ccnt + l); ++idx) {
-        const uint32_t cd = t.tb[c.sh.o_cand + t.ti(c.sh.o_cbeg + l) + idx];
-        const int cid = (cd >> 18) & 511u;
+      for (int idx = cb; idx < ce; ++idx) {
+        const int cid = (t.tb[sc.o_cand + idx] >> 18) & 511u;
         if (!(cx::isn(t.f(c.L.con + 4 * cid + 2, e)) || cx::isn(t.f(c.L.con + 4 * cid + 3, e)))) ++nv;
       }
     }
@@ -2081,16 +2067,38 @@ CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int l
     }
   }
 #endif
-  wave_sync();  // the reset scan positions before the draws read them
   for (int round = 0; pend != 0ull; ++round) {
+#ifdef COTIX_STATS
     if (lane == 0) {
       CXK_STAT(rounds, 1);
       if (round == 1) CXK_STAT(r1_left, popc64(pend));
     }
-    const uint64_t pm = ballot(m1_pass<EW>(c, t, lane, pend, kso) != 0u);
-    const uint32_t keep = m2_keep<EW>(c, t, lane, pend, pm);
-    wave_sync();  // the settled scan positions before the next round's draws read them
-    pend = ballot(keep != 0u);
+#endif
+    const int n = popc64(pend), G = lanes_per_item(n);
+    const bool mine = ((pend >> lane) & 1ull) != 0ull;
+    const int r = popc64(pend & lanes_below(lane));  // the owner's rank
+    if (mine) t.ws[WS_FLAG + r] = (uint32_t)(cb + pos) | ((uint32_t)ce << 13) | ((uint32_t)lane << 26);
+    lockstep();  // every rank's slot word before the drawers read them
+    const int slot = rank_of_lane(lane, G), q = lane - slot * G;
+    bool pass = false;
+    uint32_t cd = 0xFFFFFFFFu;
+    if (slot < n) cd = m_draw<EW>(c, t, t.ws[WS_FLAG + slot], q, kso, pass);
+    const uint64_t pm = ballot(pass);
+    // the owner: the first passing draw among its drawers r*G .. r*G+G-1
+    const uint64_t gm = G == WAVE ? ~0ull : ((1ull << G) - 1ull);
+    const uint64_t bits = mine ? (pm >> (r * G)) & gm : 0ull;
+    const int win = bits != 0ull ? r * G + __builtin_ctzll(bits) : lane;
+    const uint32_t wcd = bpermute(win, cd);
+    bool keep = false;
+    if (mine) {
+      if (bits != 0ull) {
+        t.w(cell, e) = wcd;  // the winning candidate word
+      } else {
+        pos += G;
+        keep = cb + pos < ce;
+      }
+    }
+    pend = ballot(keep);  // (after every lane's slot read: the next round's slot writes may follow)
   }
 }
 

@@ -1990,7 +1990,23 @@ CX_DEV float rcp_approx(float x) {
   return 1.0f / x;
 #endif
 }
-CX_DEV int lanes_per_item(int n) { return (int)(64.0f * rcp_approx((float)n)); }
+CX_DEV int lanes_per_item(int nd, int n) { return (int)((float)nd * rcp_approx((float)n)); }
+// the even bits of m, packed (bit 2d -> bit d)
+CX_DEV uint64_t even_bits(uint64_t x) {
+  x &= 0x5555555555555555ull;
+  x = (x | (x >> 1)) & 0x3333333333333333ull;
+  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+}
+// rounds with at most this many pending items draw on lane PAIRS (legacy
+// PRNG layout): each split's two threefry blocks run one per lane
+// (split_at_pair), 4 blocks per draw on the chain instead of 7, at half the
+// draws per round
+#ifndef COTIX_SCAN_PAIR_MAX_N
+#define COTIX_SCAN_PAIR_MAX_N 0
+#endif
 CX_DEV int rank_of_lane(int lane, int G) { return (int)(((float)lane + 0.5f) * rcp_approx((float)G)); }
 
 // M0: the item's activity (a cell whose distinct contacts are all NaN never writes)
@@ -2011,8 +2027,8 @@ CX_DEV uint32_t m0_flag(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
 // a drawer's candidate: its item's next candidate word (slot word: the
 // item's scan base | end << 13 | id << 26), 0xFFFFFFFF past the item's list;
 // pass: the candidate's bernoulli draw passed and its contact is not NaN
-template <int EW>
-CX_DEV uint32_t m_draw(const Ctx& c, Tile<EW> t, uint32_t sw, int q, int kso, bool& pass) {
+template <int EW, bool PAIR>
+CX_DEV uint32_t m_draw(const Ctx& c, Tile<EW> t, uint32_t sw, int q, int kso, int h, bool& pass) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   pass = false;
@@ -2024,12 +2040,18 @@ CX_DEV uint32_t m_draw(const Ctx& c, Tile<EW> t, uint32_t sw, int q, int kso, bo
   const float cpx = t.f(c.L.con + 4 * cid + 2, e), cpy = t.f(c.L.con + 4 * cid + 3, e);
   const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
   const bool part = sc.prng != 0;
-  const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
-  const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
-  const bool valid = !(isn(cpx) || isn(cpy));                                        // a NaN candidate never writes
-  CXK_STAT(draws, 1);
-  CXK_STAT(valid_draws, valid ? 1 : 0);
-  pass = valid && bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part);  // :222-223
+  const bool valid = !(isn(cpx) || isn(cpy));  // a NaN candidate never writes
+  if (PAIR) {  // (legacy layout) both lanes of the pair: one block of each split per lane
+    const key2 k2 = split_at_pair(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, h, false);  // :264
+    const key2 k = split_at_pair(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, h, false);   // :254
+    pass = valid && bernoulli_l(split_at_pair(k, 2u, 0u, h, false), sc.pc, false);           // :222-223
+  } else {
+    const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
+    const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
+    pass = valid && bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part);             // :222-223
+  }
+  CXK_STAT(draws, PAIR ? (h == 0 ? 1 : 0) : 1);
+  CXK_STAT(valid_draws, valid && (!PAIR || h == 0) ? 1 : 0);
   return cd;
 }
 template <int EW>
@@ -2074,20 +2096,28 @@ CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int l
       if (round == 1) CXK_STAT(r1_left, popc64(pend));
     }
 #endif
-    const int n = popc64(pend), G = lanes_per_item(n);
+    const int n = popc64(pend);
+    const bool pairs = COTIX_SCAN_PAIR_MAX_N > 0 && n <= COTIX_SCAN_PAIR_MAX_N && sc.prng == 0;  // uniform
+    const int nd = pairs ? WAVE / 2 : WAVE;  // drawers: lanes, or lane pairs
+    const int G = lanes_per_item(nd, n), d = pairs ? lane >> 1 : lane;
     const bool mine = ((pend >> lane) & 1ull) != 0ull;
     const int r = popc64(pend & lanes_below(lane));  // the owner's rank
     if (mine) t.ws[WS_FLAG + r] = (uint32_t)(cb + pos) | ((uint32_t)ce << 13) | ((uint32_t)lane << 26);
     lockstep();  // every rank's slot word before the drawers read them
-    const int slot = rank_of_lane(lane, G), q = lane - slot * G;
+    const int slot = rank_of_lane(d, G), q = d - slot * G;
     bool pass = false;
     uint32_t cd = 0xFFFFFFFFu;
-    if (slot < n) cd = m_draw<EW>(c, t, t.ws[WS_FLAG + slot], q, kso, pass);
-    const uint64_t pm = ballot(pass);
+    if (slot < n) {
+      const uint32_t sw = t.ws[WS_FLAG + slot];
+      cd = pairs ? m_draw<EW, true>(c, t, sw, q, kso, lane & 1, pass) : m_draw<EW, false>(c, t, sw, q, kso, 0, pass);
+    }
+    const uint64_t pl = ballot(pass);
+    const uint64_t pm = pairs ? even_bits(pl) : pl;  // per drawer
     // the owner: the first passing draw among its drawers r*G .. r*G+G-1
     const uint64_t gm = G == WAVE ? ~0ull : ((1ull << G) - 1ull);
     const uint64_t bits = mine ? (pm >> (r * G)) & gm : 0ull;
-    const int win = bits != 0ull ? r * G + __builtin_ctzll(bits) : lane;
+    const int wd = r * G + (bits != 0ull ? __builtin_ctzll(bits) : 0);
+    const int win = bits != 0ull ? (pairs ? 2 * wd : wd) : lane;
     const uint32_t wcd = bpermute(win, cd);
     bool keep = false;
     if (mine) {

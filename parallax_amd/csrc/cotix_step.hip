@@ -292,8 +292,8 @@ int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specializ
 int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec) {
   if (!scene) return fail("null scene");
   if (envs_per_wave) *envs_per_wave = scene->envs_per_wave;
-  // the specialization is instantiated for the default tiling only
-  if (spec) *spec = scene->envs_per_wave == 4 ? scene_spec(scene) : cxk::SPEC_GENERIC;
+  // the step program's specialization: instantiated at 4 and 2 envs per wave
+  if (spec) *spec = (scene->envs_per_wave == 4 || scene->envs_per_wave == 2) ? scene_spec(scene) : cxk::SPEC_GENERIC;
   return 0;
 }
 

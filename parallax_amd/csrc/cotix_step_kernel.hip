@@ -144,8 +144,10 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
   constexpr int F_AN = FNS_ANALYTIC, F_PP = FNS_ANALYTIC | FNS_CONVEX, F_AP = F_PP | cxk::FNS_AABB_POLY,
                 F_ALL = F_AP | FNS_CIRCLE_POLY;
   const int F = cxk::launch_fnset(fs, mode);  // the contact-function program for this scene
-#if COTIX_EW == 4  // the default tiling carries the two reference-scene specializations
-  if (spec == cxk::SPEC_ROBOCUP && F == F_AN) {
+#if COTIX_EW == 4 || COTIX_EW == 2
+  // the reference-scene specializations: every program of RoboCup at the
+  // default tiling, the step programs (mode 0) at 4 and 2 envs per wave
+  if (spec == cxk::SPEC_ROBOCUP && F == F_AN && (mode == 0 || COTIX_EW == 4)) {
     if (mode == 3)
       COTIX_LAUNCH_SPEC(F_AN, 3, cxk::SPEC_ROBOCUP);
     else if (mode == 2)

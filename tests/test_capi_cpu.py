@@ -113,7 +113,9 @@ def test_scene_variant_api():
     s.set_variant(4, False)
     assert s.variant() == {"envs_per_wave": 4, "specialization": "generic"}
     s.set_variant(2)
-    assert s.variant() == {"envs_per_wave": 2, "specialization": "generic"}  # specializations: 4-env tiling only
+    assert s.variant() == {"envs_per_wave": 2, "specialization": "robocup"}  # specializations: 4 and 2 envs per wave
+    s.set_variant(8)
+    assert s.variant() == {"envs_per_wave": 8, "specialization": "generic"}
     s.set_variant(0)
     assert s.variant()["envs_per_wave"] == 4
     with pytest.raises(RuntimeError, match="envs_per_wave"):

@@ -1013,31 +1013,33 @@ def test_regression_hipcc_mixed_kind_transform(torch_cuda, cport_lib, ew):
 
 @pytest.mark.parametrize("scene", ["robocup", "lunar"])
 def test_specialized_kernel_equals_generic(torch_cuda, scene):
-    """The scene-specialized instantiations (compile-time dimensions of the
-    two reference scenes, cxk::SPEC_*) and the generic kernel (specialize=0)
-    give bit-identical state, keys, error bits, restarts and collider traces."""
+    """The scene-specialized instantiations (the two reference scenes' headers
+    as compile-time constants, cxk::SPEC_*, at 4 and 2 envs per wave) and the
+    generic kernel (specialize=0) give bit-identical state, keys, error bits,
+    restarts and collider traces."""
     torch = torch_cuda
     import parallax_amd as pa
     from cotix_oracle import prng
     outs = []
-    for spec in (True, False):
+    for ew, spec in ((4, True), (4, False), (2, True)):
         if scene == "robocup":
             env = pa.BatchedEnv(pa.RoboCupEnv(batch=1000, device="cuda", perturb=True), autoreset=True)
         else:
             tk = torch.tensor(u32_to_i32(prng.split(prng.PRNGKey(0), 1000)), device="cuda")
             env = pa.BatchedEnv(pa.LunarLander(key=tk, batch=1000, device="cuda"), autoreset=True)
             env.scenario.dyn_reset[:3, 1, ::2] -= 6.3  # half of the landers start on the ground
-        env.world.set_variant(4, spec)
-        assert env.world.scene.variant()["specialization"] == (scene if spec else "generic")
+        env.world.set_variant(ew, spec)
+        assert env.world.scene.variant() == {"envs_per_wave": ew, "specialization": scene if spec else "generic"}
         env.reset()
         trc = {}
         env.step(24, trace=trc)
         torch.cuda.synchronize()
         outs.append([env.world.dyn.cpu().numpy(), env.world.keys.cpu().numpy(), env.world.err.cpu().numpy(),
                      env.resets.cpu().numpy(), trc["chosen"].cpu().numpy(), trc["cells"].cpu().numpy()])
-    assert same_f32(outs[0][0], outs[1][0])
-    for g, w in zip(outs[0][1:], outs[1][1:]):
-        assert np.array_equal(g, w)
+    for o in outs[1:]:
+        assert same_f32(outs[0][0], o[0])
+        for g, w in zip(outs[0][1:], o[1:]):
+            assert np.array_equal(g, w)
     assert (outs[0][5] >= 0).any()
 
 

@@ -575,6 +575,14 @@ CX_DEV void ph_geo(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane)
   }
 }
 
+template <int EW>
+CX_DEV void k_one_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, uint32_t k0, uint32_t k1);
+// the key chain of a one-step launch runs in the prologue, on the keys in
+// registers, while the batch of state reads is in flight (ph_load)
+CX_DEV bool keys_on(const KArgs& a) {
+  return (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !CXK_SKIP(a, 16);
+}
+CX_DEV bool k_in_prologue(const KArgs& a) { return keys_on(a) && a.n_steps == 1; }
 template <int EW, bool EVAL = false>
 CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   if (c.sh.poly) {  // phase F's flag array incl. its padding to a multiple of 64
@@ -628,6 +636,7 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
       }
       r[q] = src != nullptr ? *src : 0.0f;
     }
+    if (base == 0 && k_in_prologue(a)) k_one_regs<EW>(a, c, t, lane, k0, k1);  // uniform; the reads in flight
 #pragma unroll
     for (int q = 0; q < LK; ++q) {
       const int w = base + q * WAVE + lane;
@@ -723,19 +732,25 @@ CX_DEV void ph_K2(const Ctx& c, Tile<EW> t, int lane, int n) {
 // a one-step window (K = 1 launches, the RL loop) in ONE pass over (body,
 // env) items: each lane derives its body's choice key through the whole
 // chain (K0 -> K1 -> K2, the same splits), body 0's lane also writes the
-// chain's keys -- no phase syncs or LDS round trips between the three levels
+// chain's keys -- no phase syncs or LDS round trips between the three levels.
+// The env's collider key comes from lane e's registers (lane permutes), so a
+// one-step launch runs this in its prologue (ph_load) while the state reads
+// are in flight.  Items ((body, env), half) on lane pairs (split_at_pair),
+// in uniform rounds of 64 (the permutes are wave-wide).
 template <int EW>
-CX_DEV void ph_K_one(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) {
+CX_DEV void k_one_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, uint32_t k0, uint32_t k1) {
   using namespace cx;
   const Lay& L = c.L;
   const int nb = c.nb;
   const bool coll = (a.stages & COTIX_STAGE_COLLIDER) != 0;
-  // items ((body, env), half): every split on a lane pair (split_at_pair)
-  for (int w = lane; w < 2 * (coll ? nb : 1) * EW; w += WAVE) {
-    const int p = w >> 1, h = w & 1, e = p % EW, i = p / EW, o = L.kw;
+  const bool part = c.sh.prng != 0;
+  const int ni = 2 * (coll ? nb : 1) * EW;
+  for (int base = 0; base < ni; base += WAVE) {
+    const int w = base + lane, p = w >> 1, h = w & 1, e = p % EW, i = p / EW, o = L.kw;
+    const key2 kin = key2{bpermute(e, k0), bpermute(e, k1)};  // env e's collider key (lane e)
+    if (w >= ni) continue;
     const bool wr = i == 0 && h == 0;
-    const bool part = c.sh.prng != 0;
-    key2 k = split_at_pair(key2{t.w(L.key, e), t.w(L.key + 1, e)}, 2u, 0u, h, part);  // K0
+    key2 k = split_at_pair(kin, 2u, 0u, h, part);  // K0
     if (wr) {
       t.w(o, e) = k.a;
       t.w(o + 1, e) = k.b;
@@ -2911,7 +2926,7 @@ template <int EW, int FNSET, bool ROLL, bool EVAL = false, class R = void>
 CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, bool loaded = false) {
   static_assert(!(ROLL && EVAL), "the rollout has no judge");
   if (!loaded) run(PH_LOAD, [&](int l) { ph_load_fwd<EW, ROLL, EVAL>(a, c, t, env0, l); });
-  const bool keys = (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !CXK_SKIP(a, 16);
+  const bool keys = keys_on(a);
   if (EVAL && a.judge.on) {  // the first NFE's start
     run(PH_J, [&](int l) { ph_JB<EW>(a, c, t, env0, l); });
     run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });
@@ -2920,10 +2935,13 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
-    if (keys && slot == 0) {
+    if (keys && slot == 0 && !(step == 0 && k_in_prologue(a))) {
       const int n = a.n_steps - step < KWIN ? a.n_steps - step : KWIN;
-      if (n == 1) {
-        run(PH_K, [&](int l) { ph_K_one<EW>(a, c, t, l); });
+      if (n == 1) {  // (a launch's last window: the keys from the tile)
+        run(PH_K, [&](int l) {
+          const uint32_t k0 = l < EW ? t.w(c.L.key, l) : 0u, k1 = l < EW ? t.w(c.L.key + 1, l) : 0u;
+          k_one_regs<EW>(a, c, t, l, k0, k1);
+        });
       } else {
         run(PH_K, [&](int l) { ph_K0<EW>(a, c, t, l, n); });
         run(PH_K, [&](int l) { ph_K1<EW>(c, t, l, n); });

@@ -234,6 +234,19 @@ class World:
         launch.  judge / control: ctypes cotix_judge / cotix_control (or None);
         action f32 [B, 2] held over the env-steps; reward f32 [B] and finished
         i32 [B] in/out; obs f32 [B, n_bodies, 6] out (nullable)."""
+        self.eval_launcher(dyn, keys, err, n_nfe, wfe, dt, stages, judge, control, reward, finished, action,
+                           action_body, reset_mode, dyn_reset, resets, obs)()
+
+    def eval_launcher(self, dyn, keys, err, n_nfe, wfe, dt, stages, judge=None, control=None, reward=None,
+                      finished=None, action=None, action_body=0, reset_mode=0, dyn_reset=None, resets=None,
+                      obs=None):
+        """eval_state's launch prepared once: checks every tensor and converts
+        every argument now, and returns launch(action=None, stream=None), which
+        calls cotix_eval with them on the current stream (or `stream`, a raw
+        stream handle) -- the per-step host cost of an RL loop that steps the
+        same buffers over and over (BatchedEnv.step).  launch(action=t) swaps
+        in another f32 [B, 2] action tensor (shape/dtype/device checked, then
+        only its pointer); the returned launcher keeps every tensor alive."""
         for t, shape in ((dyn, tuple(self.dyn.shape)), (keys, (self.B, 2)), (err, (self.B,))):
             if tuple(t.shape) != shape or not t.is_contiguous() or t.device != self.dyn.device:
                 raise ValueError("state tensor shape/device/layout mismatch")
@@ -247,12 +260,32 @@ class World:
             if t is not None and t.dtype != dt_:  # the kernel reads f32 / 32-bit words
                 raise ValueError("eval tensor dtype %s, expected %s" % (t.dtype, dt_))
         import ctypes
-        _ffi.check(_ffi.lib.cotix_eval(
-            self.scene.handle, _ffi.ptr(dyn), _ffi.ptr(keys), _ffi.ptr(err), _ffi.ptr(self.geom), self.geom_stride,
-            self.B, int(n_nfe), int(wfe), float(dt), int(self._stages(stages)),
-            None if judge is None else ctypes.byref(judge), None if control is None else ctypes.byref(control),
-            _ffi.ptr(action), int(action_body), _ffi.ptr(reward), _ffi.ptr(finished), int(reset_mode),
-            _ffi.ptr(dyn_reset), _ffi.ptr(resets), _ffi.ptr(obs), _ffi.stream_ptr(self.device)), "cotix_eval")
+        args = [ctypes.c_void_p(self.scene.handle), _ffi.ptr(dyn), _ffi.ptr(keys), _ffi.ptr(err), _ffi.ptr(self.geom),
+                ctypes.c_int(self.geom_stride), ctypes.c_int(self.B), ctypes.c_int(int(n_nfe)), ctypes.c_int(int(wfe)),
+                ctypes.c_float(float(dt)), ctypes.c_int(int(self._stages(stages))),
+                None if judge is None else ctypes.pointer(judge), None if control is None else ctypes.pointer(control),
+                _ffi.ptr(action), ctypes.c_int(int(action_body)), _ffi.ptr(reward), _ffi.ptr(finished),
+                ctypes.c_int(int(reset_mode)), _ffi.ptr(dyn_reset), _ffi.ptr(resets), _ffi.ptr(obs)]
+        keep = (dyn, keys, err, self.geom, judge, control, action, reward, finished, dyn_reset, resets, obs)
+        fn, dev_index = _ffi.lib.cotix_eval, self.dyn.device.index
+        raw_stream = torch.cuda.current_stream  # (the stream at each launch, as every other op)
+        act_shape, act_dev = (self.B, 2), self.dyn.device
+
+        def launch(action=None, stream=None):
+            a = args
+            if action is not None:
+                if tuple(action.shape) != act_shape or action.dtype != torch.float32 or action.device != act_dev \
+                        or not action.is_contiguous():
+                    raise ValueError("action must be a contiguous f32 [B, 2] tensor on the world's device")
+                a = list(args)
+                a[13] = ctypes.c_void_p(action.data_ptr())
+            st = raw_stream(dev_index).cuda_stream if stream is None else stream
+            rc = fn(*a, ctypes.c_void_p(st))
+            if rc != 0:
+                _ffi.check(rc, "cotix_eval")
+            return keep  # (the launch reads them asynchronously)
+
+        return launch
 
     # -- body-level operators (UniversalShape, cotix/_universal_shape.py:87-132) --
     def penetrates_with(self, i, j):

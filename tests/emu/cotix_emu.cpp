@@ -445,6 +445,12 @@ static void hdr_put(std::string& o, const char* name, float v) {
   std::snprintf(b, sizeof b, "%af", (double)v);
   o += std::string("/*") + name + "*/ " + b + ", ";
 }
+// the scene's hot tables (tooling: table inspection); returns nhot
+extern "C" int emu_scene_hot(void* scene, uint32_t* out, int n) {
+  const cxk::SceneDev& s = static_cast<EmuScene*>(scene)->s;
+  for (int q = 0; q < s.nhot && q < n; ++q) out[q] = s.hot[q];
+  return s.nhot;
+}
 extern "C" int emu_scene_hdr_text(void* scene, char* buf, int n) {
   const cxk::SceneHdr& h = static_cast<EmuScene*>(scene)->s;
   std::string o = "{";

@@ -32,6 +32,25 @@ def main():
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         out[name] = {"env_steps_per_s": 4096 * n / wall, "us_per_call": wall / n * 1e6}
+    # the kernel alone: HIP events around each launch (a separate pass)
+    n = 500
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for e0, e1 in evs:
+        e0.record()
+        env.step(1)
+        e1.record()
+    torch.cuda.synchronize()
+    out["kernel_us_events"] = sum(a.elapsed_time(b) for a, b in evs) / n * 1e3
+    # the host side alone: the same Python path with the library call stubbed
+    real = pa._ffi.lib.cotix_eval
+    pa._ffi.lib.cotix_eval = lambda *a: 0
+    try:
+        t0 = time.perf_counter()
+        for _ in range(n):
+            env.step(1)
+        out["python_us_per_call_no_launch"] = (time.perf_counter() - t0) / n * 1e6
+    finally:
+        pa._ffi.lib.cotix_eval = real
     print(json.dumps(out))
 
 

@@ -44,18 +44,18 @@ CX_DEV bool isn(float x) { return x != x; }
 CX_DEV float qnan() { return __builtin_nanf(""); }
 CX_DEV float finf() { return __builtin_inff(); }
 
-// lax.max / lax.min: NaN-propagating, ties keep the first operand.
-// (written as three flat selects: the nested-ternary form compiles to
-// divergent branches on gfx950)
+// lax.max / lax.min: NaN-propagating (the first NaN operand), ties keep the
+// first operand.  Two flat selects: a >= b is false when either is NaN, so
+// m is already b when b is NaN, and only a NaN a needs its own test (the two
+// compares are independent: their select hazards overlap).  The
+// nested-ternary form compiles to divergent branches on gfx950.
 CX_DEV float fmax_(float a, float b) {
   const float m = (a >= b) ? a : b;
-  const float n = isn(b) ? b : m;
-  return isn(a) ? a : n;
+  return isn(a) ? a : m;
 }
 CX_DEV float fmin_(float a, float b) {
   const float m = (a <= b) ? a : b;
-  const float n = isn(b) ? b : m;
-  return isn(a) ? a : n;
+  return isn(a) ? a : m;
 }
 // jnp.clip (jax 0.4.x): minimum(hi, maximum(lo, x))
 CX_DEV float clip_(float x, float lo, float hi) { return fmin_(hi, fmax_(lo, x)); }

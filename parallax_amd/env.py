@@ -71,7 +71,7 @@ class BatchedEnv:
         observation into instead of this env's buffer (e.g. an all-gather
         send buffer)."""
         w = self.world
-        if not isinstance(n_steps, numbers.Integral) or isinstance(n_steps, bool):
+        if type(n_steps) is not int and (not isinstance(n_steps, numbers.Integral) or isinstance(n_steps, bool)):
             raise TypeError("n_steps must be an int (pass the action as action=...)")
         if trace is not None and self.judge is not None:
             raise ValueError("trace= is not available with a judge (the judge runs the cotix_eval program)")

@@ -268,7 +268,9 @@ class World:
                 ctypes.c_int(int(reset_mode)), _ffi.ptr(dyn_reset), _ffi.ptr(resets), _ffi.ptr(obs)]
         keep = (dyn, keys, err, self.geom, judge, control, action, reward, finished, dyn_reset, resets, obs)
         fn, dev_index = _ffi.lib.cotix_eval, self.dyn.device.index
-        raw_stream = torch.cuda.current_stream  # (the stream at each launch, as every other op)
+        # the current stream at each launch, as every other op (the raw handle without a Stream object)
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        cur_stream = raw if raw is not None else (lambda i: torch.cuda.current_stream(i).cuda_stream)
         act_shape, act_dev = (self.B, 2), self.dyn.device
 
         def launch(action=None, stream=None):
@@ -279,7 +281,7 @@ class World:
                     raise ValueError("action must be a contiguous f32 [B, 2] tensor on the world's device")
                 a = list(args)
                 a[13] = ctypes.c_void_p(action.data_ptr())
-            st = raw_stream(dev_index).cuda_stream if stream is None else stream
+            st = cur_stream(dev_index) if stream is None else stream
             rc = fn(*a, ctypes.c_void_p(st))
             if rc != 0:
                 _ffi.check(rc, "cotix_eval")

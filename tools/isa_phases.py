@@ -11,6 +11,7 @@ NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E",
          "adj", "F", "K", "E1", "R", "trace", "B0", "B1", "F0", "F1", "F2", "F3",
          "TV0", "TV1", "TV2", "TV3"]
 src, pat = sys.argv[1], sys.argv[2]
+DUMP = sys.argv[3] if len(sys.argv) > 3 else None  # optional: print this phase's instructions
 lines = open(src).read().split("\n")
 body, cur = [], False
 for ln in lines:
@@ -43,6 +44,8 @@ for ln in body:
     op = t.split()[0]
     ph = stack[-1] if stack else "-"
     cnt[ph][op] += 1
+    if DUMP is not None and ph == DUMP:
+        print(t)
 for ph, c in sorted(cnt.items(), key=lambda kv: -sum(kv[1].values())):
     tot = sum(c.values())
     v = sum(n for k, n in c.items() if k.startswith("v_"))

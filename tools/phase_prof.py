@@ -1,7 +1,9 @@
 """Per-phase cycle profile of the fused step kernel (perf tooling, not the
 product).  Needs the profiling build of the library:
     hipcc ... -DCOTIX_PHASE_PROF -> parallax_amd/_lib/libcotix_amd_prof.so   (tools/phase_prof.py --build)
-and runs the bench workload with it:  python tools/phase_prof.py [--scenario robocup|lunar] [--launches N]"""
+and runs the bench workload with it:  python tools/phase_prof.py [--scenario robocup|lunar|box] [--launches N]
+--mode grad: the config-5 rollout (cotix_rollout forward + cotix_rollout_backward,
+--substeps steps), the forward's and the backward's phases reported apart."""
 import argparse
 import ctypes
 import json
@@ -32,6 +34,7 @@ def main():
     ap.add_argument("--lib", default=LIB)
     ap.add_argument("--no-broadphase", action="store_true", help="lunar: without COTIX_STAGE_BROADPHASE")
     ap.add_argument("--drop", type=float, default=0.0, help="lunar: lower lander and legs by this much (in contact)")
+    ap.add_argument("--mode", default="step", choices=["step", "grad"])
     a = ap.parse_args()
     if a.build:
         return build()
@@ -46,6 +49,8 @@ def main():
     if a.scenario == "robocup":
         keys = pa.random.split(pa.random.PRNGKey(3, dev), B).contiguous()
         scen = pa.RoboCupEnv(batch=B, device=dev, keys=keys, perturb=True)
+    elif a.scenario == "box":
+        scen = pa.BoxWorld(batch=B, device=dev)
     else:
         tk = pa.random.split(pa.random.PRNGKey(0, dev), B).contiguous()
         ck = pa.random.split(pa.random.PRNGKey(1, dev), B).contiguous()
@@ -56,25 +61,54 @@ def main():
             for i in range(3):
                 scen.dyn_reset[i, 1] -= a.drop
                 scen.dyn_reset[i, 3] = -0.3
+    ew = 4  # the profiling build carries the default tiling only (COTIX_EW4_ONLY)
+    waves = (B + ew - 1) // ew
+    buf = (ctypes.c_ulonglong * 40)()
+
+    def phases(steps):
+        n = f(buf, 40)
+        nph = NAMES.index("sub0")
+        tot = sum(buf[q] for q in range(min(n, nph)))  # the sub-phase timers (nph..) overlap the phases
+        return {"cycles_per_wave_step_total": tot / waves / steps,
+                "phases": {NAMES[q]: {"cycles_per_wave_step": buf[q] / waves / steps, "share": buf[q] / tot}
+                           for q in range(n) if buf[q]}}
+
+    if a.mode == "grad":
+        world = scen.world
+        nb = len(world.bodies)
+        dyn0, keys0 = world.dyn.clone(), world.keys.clone()
+        gen = torch.Generator(device="cpu").manual_seed(1234)
+        actions = (torch.randn(a.substeps, B, 2, generator=gen) * 0.1).to(dev)
+        w = pa.rollout.ball_x_weights(nb, nb - 1)
+        fwd, bwd = [], []
+        for it in range(a.warmup + a.launches):
+            world.dyn.copy_(dyn0)
+            world.keys.copy_(keys0)
+            world.err.zero_()
+            torch.cuda.synchronize()
+            f(buf, 40)
+            _, saved = pa.rollout_forward(world, actions, nb - 1, w)
+            torch.cuda.synchronize()
+            pf = phases(a.substeps)
+            pa.rollout_backward(world, saved)
+            torch.cuda.synchronize()
+            pb = phases(a.substeps)
+            if it >= a.warmup:
+                fwd.append(pf)
+                bwd.append(pb)
+        print(json.dumps({"scenario": a.scenario, "mode": "grad", "envs": B, "envs_per_wave": ew,
+                          "steps_per_launch": a.substeps, "forward": fwd[-1], "backward": bwd[-1]}, indent=1))
+        return
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
     for _ in range(a.warmup):
         env.step(a.substeps)
-    buf = (ctypes.c_ulonglong * 40)()
     f(buf, 40)  # reset after warm-up
     for _ in range(a.launches):
         env.step(a.substeps)
     torch.cuda.synchronize()
-    n = f(buf, 40)
-    ew = 4  # the profiling build carries the default tiling only (COTIX_EW4_ONLY)
-    waves = (B + ew - 1) // ew
-    steps = a.launches * a.substeps
-    nph = NAMES.index("sub0")
-    tot = sum(buf[q] for q in range(min(n, nph)))  # the sub-phase timers (nph..) overlap the phases
-    out = {NAMES[q]: {"cycles_per_wave_step": buf[q] / waves / steps, "share": buf[q] / tot} for q in range(n)
-           if buf[q]}
-    print(json.dumps({"scenario": a.scenario, "envs": B, "envs_per_wave": ew, "cycles_per_wave_step_total": tot / waves / steps,
-                      "phases": out}, indent=1))
+    p = phases(a.launches * a.substeps)
+    print(json.dumps({"scenario": a.scenario, "envs": B, "envs_per_wave": ew, **p}, indent=1))
 
 
 if __name__ == "__main__":

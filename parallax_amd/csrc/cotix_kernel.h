@@ -1992,7 +1992,8 @@ CX_DEV void ph_C3(const Ctx& c, Tile<EW> t, int lane, int par) {
 // dependent LDS round trips before the draws (slot word, candidate word),
 // one permute after, no barrier.
 // (a draw's threefry chain does not wait for the candidate's validity: the
-// contact-point read overlaps it, and a NaN candidate's draw is discarded)
+// contact-point read overlaps it, and a NaN candidate's draw is discarded --
+// a bitwise AND, which the compiler cannot turn into a branch on the read)
 
 // the uniform lanes-per-item G = 64 / n and the drawer's rank slot = lane / G
 // without integer division: rcp is within 1 ulp, far inside the margins
@@ -2059,11 +2060,11 @@ CX_DEV uint32_t m_draw(const Ctx& c, Tile<EW> t, uint32_t sw, int q, int kso, in
   if (PAIR) {  // (legacy layout) both lanes of the pair: one block of each split per lane
     const key2 k2 = split_at_pair(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, h, false);  // :264
     const key2 k = split_at_pair(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, h, false);   // :254
-    pass = valid && bernoulli_l(split_at_pair(k, 2u, 0u, h, false), sc.pc, false);           // :222-223
+    pass = bernoulli_l(split_at_pair(k, 2u, 0u, h, false), sc.pc, false) & valid;            // :222-223
   } else {
     const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
     const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
-    pass = valid && bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part);             // :222-223
+    pass = bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part) & valid;              // :222-223
   }
   CXK_STAT(draws, PAIR ? (h == 0 ? 1 : 0) : 1);
   CXK_STAT(valid_draws, valid && (!PAIR || h == 0) ? 1 : 0);

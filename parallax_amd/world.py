@@ -260,7 +260,7 @@ class World:
             if t is not None and t.dtype != dt_:  # the kernel reads f32 / 32-bit words
                 raise ValueError("eval tensor dtype %s, expected %s" % (t.dtype, dt_))
         import ctypes
-        args = [ctypes.c_void_p(self.scene.handle), _ffi.ptr(dyn), _ffi.ptr(keys), _ffi.ptr(err), _ffi.ptr(self.geom),
+        args = [self.scene.handle, _ffi.ptr(dyn), _ffi.ptr(keys), _ffi.ptr(err), _ffi.ptr(self.geom),
                 ctypes.c_int(self.geom_stride), ctypes.c_int(self.B), ctypes.c_int(int(n_nfe)), ctypes.c_int(int(wfe)),
                 ctypes.c_float(float(dt)), ctypes.c_int(int(self._stages(stages))),
                 None if judge is None else ctypes.pointer(judge), None if control is None else ctypes.pointer(control),

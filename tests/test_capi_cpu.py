@@ -170,3 +170,45 @@ def test_env_step_argument_checks():
     envj = pa.BatchedEnv(Scen(), judge=E.LinearJudge(rate_w={24: 1.0}))
     with pytest.raises(ValueError, match="trace"):
         envj.step(1, trace={})
+
+
+def test_prepared_eval_launch_marshals_every_argument(monkeypatch):
+    """World.eval_launcher / BatchedEnv.step's prepared launch: every argument
+    converts through cotix_eval's declared ctypes signature (checked with the
+    real argtypes; the call itself is stubbed -- no GPU here), the action slot
+    is swapped per launch, and the launch is reused for the same buffers."""
+    import ctypes
+    import parallax_amd as pa
+    from parallax_amd import envs as E
+    real = pa._ffi.lib.cotix_eval
+    calls = []
+
+    def checked(*args):
+        assert len(args) == len(real.argtypes)
+        for t, v in zip(real.argtypes, args):
+            if v is not None:
+                t.from_param(v)  # raises on a mismatch
+        calls.append(args)
+        return 0
+
+    monkeypatch.setattr(pa._ffi.lib, "cotix_eval", checked)
+    monkeypatch.setattr(torch._C, "_cuda_getCurrentRawStream", lambda i: 0, raising=False)
+
+    class Scen:
+        world = _robocup_world_cpu()
+        dyn_reset = world.dyn.clone()
+        stages = pa._ffi.STAGES_ROBOCUP
+
+    for judge in (None, E.LinearJudge(rate_w={24: 1.0})):
+        env = pa.BatchedEnv(Scen(), autoreset=True, judge=judge)
+        env.step(1)
+        env.step(1)
+        assert len(env._launchers) == 1  # one prepared launch for the same configuration
+        act = torch.ones(Scen.world.B, 2)
+        env.step(1, action=act)
+        assert calls[-1][13].value == act.data_ptr() and calls[-2][13] is None
+        env.step(4)
+        assert len(env._launchers) == 2
+        with pytest.raises(ValueError, match="action"):
+            env.step(1, action=torch.ones(Scen.world.B, 3))
+    assert isinstance(calls[0][-1], ctypes.c_void_p)

@@ -163,7 +163,8 @@ int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, in
  * compile-time constant, 0 forces the generic kernel.
  * cotix_scene_variant reports what a step launch uses: the tiling and the
  * specialization id (0 generic, 1 RoboCup, 2 LunarLander, 3 RoboCup and 4
- * LunarLander in the partitionable PRNG layout). */
+ * LunarLander in the partitionable PRNG layout, 5 the box world's structure:
+ * 3 AABB walls and 4 circles, legacy layout). */
 int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specialize);
 int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec);
 

@@ -141,8 +141,9 @@ struct SceneDev : SceneHdr {
 
 // Scene specializations of the step kernel.  The phases are generic over the
 // scene (counts, table offsets and parameters in the header); for the two
-// reference scenes, under the default constants in either PRNG layout, the
-// launcher picks an instantiation whose header is a compile-time constant --
+// reference scenes, under the default constants in either PRNG layout (and
+// the box world's structure, legacy layout), the launcher picks an
+// instantiation whose header is a compile-time constant --
 // every per-item loop has a known trip count (no exec-mask loop control, no
 // index division), the tile layout and every table address fold to
 // immediates, the parameters to literals, and no scalar register holds the
@@ -151,7 +152,15 @@ struct SceneDev : SceneHdr {
 // tools/gen_spec_hdrs.py and checked against the compiler by
 // tests/test_emu_cpu.py); spec_of() admits a scene only when its whole header
 // is bit-identical.
-enum : int { SPEC_GENERIC = 0, SPEC_ROBOCUP = 1, SPEC_LUNAR = 2, SPEC_ROBOCUP_PART = 3, SPEC_LUNAR_PART = 4, SPEC_N = 5 };
+enum : int {
+  SPEC_GENERIC = 0,
+  SPEC_ROBOCUP = 1,
+  SPEC_LUNAR = 2,
+  SPEC_ROBOCUP_PART = 3,
+  SPEC_LUNAR_PART = 4,
+  SPEC_BOX = 5,  // the box world's structure (3 AABB walls, 4 circles): the finite scene of the secondary figures
+  SPEC_N = 6
+};
 }  // namespace cxk
 #include "cotix_spec_hdrs.h"  // cxk::SPEC_HDRS[SPEC_N]
 namespace cxk {

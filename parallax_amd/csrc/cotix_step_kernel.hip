@@ -162,6 +162,18 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
     COTIX_LAUNCH_SPEC(F_PP, 0, cxk::SPEC_LUNAR);
     return hipGetLastError();
   }
+#if COTIX_EW == 4
+  // the box world's structure: the step and rollout programs (finite_scene, grad_box)
+  if (spec == cxk::SPEC_BOX && F == F_AN && mode <= 2) {
+    if (mode == 2)
+      COTIX_LAUNCH_SPEC(F_AN, 2, cxk::SPEC_BOX);
+    else if (mode == 1)
+      COTIX_LAUNCH_SPEC(F_AN, 1, cxk::SPEC_BOX);
+    else
+      COTIX_LAUNCH_SPEC(F_AN, 0, cxk::SPEC_BOX);
+    return hipGetLastError();
+  }
+#endif
   // the partitionable layout's specializations: the step program only
   if (spec == cxk::SPEC_ROBOCUP_PART && mode == 0 && F == F_AN) {
     COTIX_LAUNCH_SPEC(F_AN, 0, cxk::SPEC_ROBOCUP_PART);

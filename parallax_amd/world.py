@@ -16,7 +16,7 @@ from .shapes import AbstractPolygon
 
 
 # the step kernel's scene specializations (cxk::SPEC_*, cotix_kernel.h)
-SPECIALIZATIONS = ("generic", "robocup", "lunar", "robocup_partitionable", "lunar_partitionable")
+SPECIALIZATIONS = ("generic", "robocup", "lunar", "robocup_partitionable", "lunar_partitionable", "box")
 
 
 class Scene:

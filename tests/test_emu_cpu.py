@@ -366,6 +366,13 @@ def test_reference_scenes_get_their_specializations(emu_lib):
                     dict(prng_layout="partitionable", epa_max_iters=47)):
             h, _ = emu.oracle_scene(lib, bodies(), Params(**alt))
             assert lib.emu_scene_spec(h) == 0, alt
+    # the box world's structure (any parameter values of 3 AABB walls + 4 circles)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_spec_hdrs
+    h, _ = emu.oracle_scene(lib, gen_spec_hdrs.box_bodies())
+    assert lib.emu_scene_spec(h) == 5
+    h, _ = emu.oracle_scene(lib, gen_spec_hdrs.box_bodies(), Params(prng_layout="partitionable"))
+    assert lib.emu_scene_spec(h) == 0
 
 
 def test_specialization_headers_are_current():

@@ -1011,7 +1011,7 @@ def test_regression_hipcc_mixed_kind_transform(torch_cuda, cport_lib, ew):
     _robocup_vs_cport(torch, pa, cport, lib, env, dyn, keys, 1, 6)
 
 
-@pytest.mark.parametrize("scene", ["robocup", "lunar"])
+@pytest.mark.parametrize("scene", ["robocup", "lunar", "box"])
 def test_specialized_kernel_equals_generic(torch_cuda, scene):
     """The scene-specialized instantiations (the two reference scenes' headers
     as compile-time constants, cxk::SPEC_*, at 4 and 2 envs per wave) and the
@@ -1024,6 +1024,10 @@ def test_specialized_kernel_equals_generic(torch_cuda, scene):
     for ew, spec in ((4, True), (4, False), (2, True)):
         if scene == "robocup":
             env = pa.BatchedEnv(pa.RoboCupEnv(batch=1000, device="cuda", perturb=True), autoreset=True)
+        elif scene == "box":
+            if ew == 2:
+                continue  # (the box world's specialization: the 4-env tiling)
+            env = pa.BatchedEnv(pa.BoxWorld(batch=1000, device="cuda"), autoreset=True)
         else:
             tk = torch.tensor(u32_to_i32(prng.split(prng.PRNGKey(0), 1000)), device="cuda")
             env = pa.BatchedEnv(pa.LunarLander(key=tk, batch=1000, device="cuda"), autoreset=True)

@@ -1987,19 +1987,22 @@ CX_DEV void ph_C3(const Ctx& c, Tile<EW> t, int lane, int par) {
   if (lane == WAVE - 1) t.ws[WS_N] = (uint32_t)(kept + (n > WAVE ? n - WAVE : 0));
 }
 
-// Phase C when every (cell, env) item fits one lane (nl * EW <= 64): the
-// whole scan is ONE phase (ph_M_fused).  Item id == lane (its "owner"); the
-// pending items are a 64-bit ballot mask.  Each round gives the n pending
-// items G = 64 / n consecutive lanes ("drawers") in rank order, each drawing
-// the next candidate of its item's scan; the owner then settles its item
-// from the pass ballot: the first passing draw of its G writes the cell
-// (the reference's last passing candidate: the list is in reverse scan
-// order), else its scan position advances by G.  Per-item state (scan
-// position, candidate range, cell address) stays in the owner's registers;
-// the owner publishes its range to its drawers in one LDS word per rank, and
-// the winning candidate word comes back by a lane permute -- per round two
-// dependent LDS round trips before the draws (slot word, candidate word),
-// one permute after, no barrier.
+// Phase C when the (cell, env) items fit two per lane (nl * EW <= 128): the
+// whole scan is ONE phase (ph_M_fused).  Items id and id + 64 belong to lane
+// id (their "owner"); the pending items are two 64-bit ballot masks.  Each
+// round gives the first min(n, 64) pending items (in id order) G = 64 / min(n, 64)
+// consecutive lanes ("drawers", at least one) in rank order, each drawing
+// the next candidate of its item's scan; an owner then settles each of its
+// items that drew from the pass ballot: the first passing draw of its G
+// writes the cell (the reference's last passing candidate: the list is in
+// reverse scan order), else its scan position advances by G; an item past
+// rank 64 waits for a later round (its draws are the same candidates then).  Per-item state (scan position, candidate
+// range, cell address) stays in the owner's registers; the owner publishes
+// its range to its drawers in one LDS word per rank, and the winning
+// candidate word comes back by a lane permute -- per round two dependent LDS
+// round trips before the draws (slot word, candidate word), one permute
+// after, no barrier.  (Draws on lane pairs -- two threefry blocks of a split
+// per lane -- measured no gain, r04j: half the draws per round cost rounds.)
 // (a draw's threefry chain does not wait for the candidate's validity: the
 // contact-point read overlaps it, and a NaN candidate's draw is discarded --
 // a bitwise AND, which the compiler cannot turn into a branch on the read)
@@ -2015,49 +2018,35 @@ CX_DEV float rcp_approx(float x) {
   return 1.0f / x;
 #endif
 }
-CX_DEV int lanes_per_item(int nd, int n) { return (int)((float)nd * rcp_approx((float)n)); }
-// the even bits of m, packed (bit 2d -> bit d)
-CX_DEV uint64_t even_bits(uint64_t x) {
-  x &= 0x5555555555555555ull;
-  x = (x | (x >> 1)) & 0x3333333333333333ull;
-  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
-  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
-  return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
-}
-// rounds with at most this many pending items draw on lane PAIRS (legacy
-// PRNG layout): each split's two threefry blocks run one per lane
-// (split_at_pair), 4 blocks per draw on the chain instead of 7, at half the
-// draws per round
-#ifndef COTIX_SCAN_PAIR_MAX_N
-#define COTIX_SCAN_PAIR_MAX_N 0
+CX_DEV int lanes_per_item(int n) { return n >= WAVE ? 1 : (int)((float)WAVE * rcp_approx((float)n)); }
+// the most items that draw in one round (64: one lane each at least); a
+// smaller value is a test build's knob (tests/test_emu_cpu.py: the
+// items-past-the-last-rank path with few items)
+#ifndef COTIX_SCAN_RANKS
+#define COTIX_SCAN_RANKS 64
 #endif
 CX_DEV int rank_of_lane(int lane, int G) { return (int)(((float)lane + 0.5f) * rcp_approx((float)G)); }
 
 // M0: the item's activity (a cell whose distinct contacts are all NaN never writes)
 template <int EW>
-CX_DEV uint32_t m0_flag(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV bool m0_active(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int id) {
   const SceneHdr& sc = c.sh;
-  uint32_t flag = 0u;
-  if (lane < c.nl * EW) {
-    const int e = lane % EW, l = lane / EW;
-    if (env0 + e < a.B) {
-      bool any = false;
-      for (int q = 0; q < sc.nmw; ++q) any |= (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
-      flag = any ? 1u : 0u;
-    }
-  }
-  return flag;
+  if (id >= c.nl * EW) return false;
+  const int e = id % EW, l = id / EW;
+  if (env0 + e >= a.B) return false;
+  bool any = false;
+  for (int q = 0; q < sc.nmw; ++q) any |= (t.tb[sc.o_cmask + l * sc.nmw + q] & t.w(c.L.vm + q, e)) != 0u;
+  return any;
 }
-// a drawer's candidate: its item's next candidate word (slot word: the
-// item's scan base | end << 13 | id << 26), 0xFFFFFFFF past the item's list;
-// pass: the candidate's bernoulli draw passed and its contact is not NaN
-template <int EW, bool PAIR>
-CX_DEV uint32_t m_draw(const Ctx& c, Tile<EW> t, uint32_t sw, int q, int kso, int h, bool& pass) {
+// a drawer's candidate: its item's next candidate word (slot word: the item's
+// scan base | end << 12 | id << 25), 0xFFFFFFFF past the item's list; pass:
+// the candidate's bernoulli draw passed and its contact is not NaN
+template <int EW>
+CX_DEV uint32_t m_draw(const Ctx& c, Tile<EW> t, uint32_t sw, int q, int kso, bool& pass) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   pass = false;
-  const int base = (int)(sw & 8191u), end = (int)((sw >> 13) & 8191u), id = (int)(sw >> 26);
+  const int base = (int)(sw & 4095u), end = (int)((sw >> 12) & 8191u), id = (int)(sw >> 25);
   const int e = id % EW, idx = base + q;
   if (idx >= end) return 0xFFFFFFFFu;
   const uint32_t cd = t.tb[sc.o_cand + idx];
@@ -2066,41 +2055,63 @@ CX_DEV uint32_t m_draw(const Ctx& c, Tile<EW> t, uint32_t sw, int q, int kso, in
   const key2 sk = key2{t.w(kso + 2 + 2 * ty, e), t.w(kso + 3 + 2 * ty, e)};
   const bool part = sc.prng != 0;
   const bool valid = !(isn(cpx) || isn(cpy));  // a NaN candidate never writes
-  if (PAIR) {  // (legacy layout) both lanes of the pair: one block of each split per lane
-    const key2 k2 = split_at_pair(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, h, false);  // :264
-    const key2 k = split_at_pair(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, h, false);   // :254
-    pass = bernoulli_l(split_at_pair(k, 2u, 0u, h, false), sc.pc, false) & valid;            // :222-223
-  } else {
-    const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
-    const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
-    pass = bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part) & valid;              // :222-223
-  }
-  CXK_STAT(draws, PAIR ? (h == 0 ? 1 : 0) : 1);
-  CXK_STAT(valid_draws, valid && (!PAIR || h == 0) ? 1 : 0);
+  const key2 k2 = split_at_l(sk, (uint32_t)t.ti(sc.o_tn2 + ty), (uint32_t)i2, part);  // :264
+  const key2 k = split_at_l(k2, (uint32_t)t.ti(sc.o_tn1 + ty), (uint32_t)i1, part);   // :254
+  pass = bernoulli_l(split_at_l(k, 2u, 0u, part), sc.pc, part) & valid;              // :222-223
+  CXK_STAT(draws, 1);
+  CXK_STAT(valid_draws, valid ? 1 : 0);
   return cd;
+}
+// an owner's item (owner slot s of lane l: item id = l + 64 s)
+struct MItem {
+  int cb = 0, ce = 0, cell = 0, pos = 0, e = 0;
+};
+template <int EW>
+CX_DEV MItem m_item(const Ctx& c, Tile<EW> t, int id) {
+  const SceneHdr& sc = c.sh;
+  MItem it;
+  if (id < c.nl * EW) {
+    const int l = id / EW;
+    it.e = id % EW;
+    it.cb = t.ti(sc.o_cbeg + l);
+    it.ce = it.cb + t.ti(sc.o_ccnt + l);
+    it.cell = c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l);
+  }
+  return it;
+}
+// an owner's item after a round's pass ballot pm: the cell word from the
+// winning drawer (wcd, permuted), or the scan advances; returns "still pending"
+template <int EW>
+CX_DEV bool m_settle(Tile<EW> t, MItem& it, bool drew, uint64_t bits, uint32_t wcd, int G) {
+  if (!drew) return true;  // (past the last rank: waits for a later round)
+  if (bits != 0ull) {
+    t.w(it.cell, it.e) = wcd;  // the winning candidate word
+    return false;
+  }
+  it.pos += G;
+  return it.cb + it.pos < it.ce;
 }
 template <int EW>
 CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso) {
-  const SceneHdr& sc = c.sh;
-  const uint32_t flag = m0_flag<EW>(a, c, t, env0, lane);
-  uint64_t pend = ballot(flag != 0u);
-  // the owner's item: candidate range [cb, ce), scan position, cell word
-  int cb = 0, ce = 0, cell = 0, pos = 0;
-  const int e = lane % EW;
-  if (lane < c.nl * EW) {
-    const int l = lane / EW;
-    cb = t.ti(sc.o_cbeg + l);
-    ce = cb + t.ti(sc.o_ccnt + l);
-    cell = c.L.m + t.ti(sc.o_ci + l) * c.nb + t.ti(sc.o_cj + l);
+  const bool two = c.nl * EW > WAVE;  // uniform (a constant in the specialized kernels)
+  MItem it0 = m_item<EW>(c, t, lane), it1;
+  const bool f0 = m0_active<EW>(a, c, t, env0, lane);
+  bool f1 = false;
+  if (two) {
+    it1 = m_item<EW>(c, t, lane + WAVE);
+    f1 = m0_active<EW>(a, c, t, env0, lane + WAVE);
   }
+  uint64_t pend0 = ballot(f0), pend1 = two ? ballot(f1) : 0ull;
 #ifdef COTIX_STATS
   {
     // the valid candidates of the active items (tools/collider_stats.py)
     uint64_t nv = 0;
-    if (flag) {
-      for (int idx = cb; idx < ce; ++idx) {
-        const int cid = (t.tb[sc.o_cand + idx] >> 18) & 511u;
-        if (!(cx::isn(t.f(c.L.con + 4 * cid + 2, e)) || cx::isn(t.f(c.L.con + 4 * cid + 3, e)))) ++nv;
+    for (int s = 0; s < 2; ++s) {
+      const MItem& it = s ? it1 : it0;
+      if (!(s ? f1 : f0)) continue;
+      for (int idx = it.cb; idx < it.ce; ++idx) {
+        const int cid = (t.tb[c.sh.o_cand + idx] >> 18) & 511u;
+        if (!(cx::isn(t.f(c.L.con + 4 * cid + 2, it.e)) || cx::isn(t.f(c.L.con + 4 * cid + 3, it.e)))) ++nv;
       }
     }
     static uint64_t wsum = 0;
@@ -2110,50 +2121,44 @@ CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int l
       CXK_STAT(valid_cands, wsum);
       CXK_STAT(fit64, wsum <= 64 ? 1 : 0);
       CXK_STAT(wave_steps, 1);
-      CXK_STAT(active_items, popc64(pend));
+      CXK_STAT(active_items, popc64(pend0) + popc64(pend1));
     }
   }
 #endif
-  for (int round = 0; pend != 0ull; ++round) {
+  for (int round = 0; (pend0 | pend1) != 0ull; ++round) {
 #ifdef COTIX_STATS
     if (lane == 0) {
       CXK_STAT(rounds, 1);
-      if (round == 1) CXK_STAT(r1_left, popc64(pend));
+      if (round == 1) CXK_STAT(r1_left, popc64(pend0) + popc64(pend1));
     }
 #endif
-    const int n = popc64(pend);
-    const bool pairs = COTIX_SCAN_PAIR_MAX_N > 0 && n <= COTIX_SCAN_PAIR_MAX_N && sc.prng == 0;  // uniform
-    const int nd = pairs ? WAVE / 2 : WAVE;  // drawers: lanes, or lane pairs
-    const int G = lanes_per_item(nd, n), d = pairs ? lane >> 1 : lane;
-    const bool mine = ((pend >> lane) & 1ull) != 0ull;
-    const int r = popc64(pend & lanes_below(lane));  // the owner's rank
-    if (mine) t.ws[WS_FLAG + r] = (uint32_t)(cb + pos) | ((uint32_t)ce << 13) | ((uint32_t)lane << 26);
+    const int n0 = popc64(pend0), n = n0 + popc64(pend1);
+    const int ns = n < COTIX_SCAN_RANKS ? n : COTIX_SCAN_RANKS, G = lanes_per_item(ns);  // items that draw, lanes each
+    const bool m0 = ((pend0 >> lane) & 1ull) != 0ull, m1 = ((pend1 >> lane) & 1ull) != 0ull;
+    const int r0 = popc64(pend0 & lanes_below(lane)), r1 = n0 + popc64(pend1 & lanes_below(lane));  // ranks
+    const bool d0 = m0 && r0 < ns, d1 = m1 && r1 < ns;
+    if (d0) t.ws[WS_FLAG + r0] = (uint32_t)(it0.cb + it0.pos) | ((uint32_t)it0.ce << 12) | ((uint32_t)lane << 25);
+    if (d1)
+      t.ws[WS_FLAG + r1] =
+          (uint32_t)(it1.cb + it1.pos) | ((uint32_t)it1.ce << 12) | ((uint32_t)(lane + WAVE) << 25);
     lockstep();  // every rank's slot word before the drawers read them
-    const int slot = rank_of_lane(d, G), q = d - slot * G;
+    const int slot = rank_of_lane(lane, G), q = lane - slot * G;
     bool pass = false;
     uint32_t cd = 0xFFFFFFFFu;
-    if (slot < n) {
-      const uint32_t sw = t.ws[WS_FLAG + slot];
-      cd = pairs ? m_draw<EW, true>(c, t, sw, q, kso, lane & 1, pass) : m_draw<EW, false>(c, t, sw, q, kso, 0, pass);
-    }
-    const uint64_t pl = ballot(pass);
-    const uint64_t pm = pairs ? even_bits(pl) : pl;  // per drawer
-    // the owner: the first passing draw among its drawers r*G .. r*G+G-1
+    if (slot < ns) cd = m_draw<EW>(c, t, t.ws[WS_FLAG + slot], q, kso, pass);
+    const uint64_t pm = ballot(pass);
+    // an owner's item: the first passing draw among its drawers r*G .. r*G+G-1
     const uint64_t gm = G == WAVE ? ~0ull : ((1ull << G) - 1ull);
-    const uint64_t bits = mine ? (pm >> (r * G)) & gm : 0ull;
-    const int wd = r * G + (bits != 0ull ? __builtin_ctzll(bits) : 0);
-    const int win = bits != 0ull ? (pairs ? 2 * wd : wd) : lane;
-    const uint32_t wcd = bpermute(win, cd);
-    bool keep = false;
-    if (mine) {
-      if (bits != 0ull) {
-        t.w(cell, e) = wcd;  // the winning candidate word
-      } else {
-        pos += G;
-        keep = cb + pos < ce;
-      }
+    const uint64_t b0 = d0 ? (pm >> (r0 * G)) & gm : 0ull;
+    const uint32_t w0 = bpermute(b0 != 0ull ? r0 * G + __builtin_ctzll(b0) : lane, cd);
+    const bool k0 = m0 && m_settle<EW>(t, it0, d0, b0, w0, G);
+    pend0 = ballot(k0);  // (after every lane's slot read: the next round's slot writes may follow)
+    if (two) {
+      const uint64_t b1 = d1 ? (pm >> (r1 * G)) & gm : 0ull;
+      const uint32_t w1 = bpermute(b1 != 0ull ? r1 * G + __builtin_ctzll(b1) : lane, cd);
+      const bool k1 = m1 && m_settle<EW>(t, it1, d1, b1, w1, G);
+      pend1 = ballot(k1);
     }
-    pend = ballot(keep);  // (after every lane's slot read: the next round's slot writes may follow)
   }
 }
 
@@ -2902,7 +2907,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_F3, [&](int l) { ph_F3<EW>(c, t, l, b); });
     }
   }
-  if (!CXK_SKIP(a, 4) && c.nl > 0 && c.nl * EW <= WAVE) {
+  if (!CXK_SKIP(a, 4) && c.nl > 0 && c.nl * EW <= 2 * WAVE) {
     run(PH_C1, [&](int l) { ph_M_fused<EW>(a, c, t, env0, l, kso); });
   } else if (!CXK_SKIP(a, 4) && c.nl > 0) {
     for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {

@@ -84,13 +84,17 @@ def test_emu_lunar_trace(emu_lib, EW, bp):
     run_trace(emu, lib, P.lunar_lander_bodies(tr["terrain_keys"][0]), rows, tr, 1 | 2 | 4 | 8 | 16 | bp, EW, True)
 
 
-def test_emu_box_world_trace(emu_lib):
+@pytest.mark.parametrize("EW", [2, 4, 8])
+def test_emu_box_world_trace(emu_lib, EW):
+    """The box world's 24 cells: 48 (cell, env) items at 2 envs per wave (one
+    per lane), 96 at 4 (two per lane: the fused scan's second owner slot and
+    its rank > 64 rounds), 192 at 8 (the list-compaction scan)."""
     emu, lib = emu_lib
     import make_golden as mg
     tr = np.load(os.path.join(GOLD, "box_world_trace.npz"))
     for e in range(tr["dyn"].shape[1]):
         sub = {k: tr[k][:, e:e + 1] for k in ("dyn", "keys", "err", "chosen", "cells")}
-        run_trace(emu, lib, mg.box_world_bodies(e), None, sub, 1 | 4 | 16, 2, False)
+        run_trace(emu, lib, mg.box_world_bodies(e), None, sub, 1 | 4 | 16, EW, False)
 
 
 def test_emu_order_clockwise_ties_nan_zero(emu_lib):
@@ -514,3 +518,38 @@ def test_emu_mixed_kinds_step_vs_cport(emu_lib, EW, circle):
     assert same_f32(got[0], want[0])
     for g, w in zip(got[1:], want[1:]):
         assert np.array_equal(g, w)
+
+
+def test_scan_items_past_the_last_rank(emu_lib):
+    """The fused scan draws for at most COTIX_SCAN_RANKS pending items per
+    round (64 in the library); the others wait for a later round.  A build
+    with 3 ranks runs that path on every step: the traces stay bit-exact
+    (RoboCup at 4 and 8 envs per wave -- one and two items per lane --, the
+    box world at 4, LunarLander at 4)."""
+    import ctypes
+    emu, real = emu_lib
+    out = os.path.join(HERE, "emu", "build", "libcotix_emu_ranks3.so")
+    src = os.path.join(HERE, "emu", "cotix_emu.cpp")
+    deps = [src] + [os.path.join(ROOT, "parallax_amd", "csrc", f) for f in os.listdir(
+        os.path.join(ROOT, "parallax_amd", "csrc")) if f.endswith(".h")]
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(f) for f in deps):
+        tmp = "%s.%d.tmp" % (out, os.getpid())
+        subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-w",
+                        "-DCOTIX_SCAN_RANKS=3", src, "-o", tmp], check=True)
+        os.replace(tmp, out)
+    lib = ctypes.CDLL(out)
+    for fn in ("emu_scene_create", "emu_scene_create_ex", "emu_step", "emu_step_ex"):
+        getattr(lib, fn).argtypes = getattr(real, fn).argtypes
+    lib.emu_last_error.restype = ctypes.c_char_p
+    from cotix_oracle import physics as P
+    import make_golden as mg
+    tr = np.load(os.path.join(GOLD, "robocup_trace.npz"))
+    for EW in (4, 8):
+        run_trace(emu, lib, P.robocup_bodies(), None, tr, 1 | 4 | 16, EW, False)
+    tb = np.load(os.path.join(GOLD, "box_world_trace.npz"))
+    for e in range(tb["dyn"].shape[1]):
+        sub = {k: tb[k][:, e:e + 1] for k in ("dyn", "keys", "err", "chosen", "cells")}
+        run_trace(emu, lib, mg.box_world_bodies(e), None, sub, 1 | 4 | 16, 4, False)
+    tl = np.load(os.path.join(GOLD, "lunar_trace.npz"))
+    rows = [emu.oracle_scene(real, P.lunar_lander_bodies(k))[1] for k in tl["terrain_keys"]]
+    run_trace(emu, lib, P.lunar_lander_bodies(tl["terrain_keys"][0]), rows, tl, 1 | 2 | 4 | 8 | 16, 4, True)

@@ -1351,11 +1351,45 @@ CX_DEV void ab_fetch(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, ABRegs&
     }
   }
 }
-// stage 3: the contacts from the fetched words
+// one analytic contact item from its descriptor, its parts' local geometry
+// and its bodies' post-Euler positions: the translate-only transforms of
+// phase T (circle: (r, cx + px, cy + py); AABB: lo + p, up + p), the contact,
+// its words and valid bit
+template <int EW>
+CX_DEV void ab_item(const KArgs& a, const Ctx& c, Tile<EW> t, int e, int ci, uint32_t dw, const float* ga,
+                    const float* gb, float pxa, float pya, float pxb, float pyb) {
+  using namespace cx;
+  CXK_STAT(b_items, 1);
+  Shape A, Bs;
+  A.kind = (int)((dw >> 23) & 3u);
+  Bs.kind = (int)((dw >> 25) & 3u);
+  A.n = Bs.n = 0;
+  const bool ca = A.kind == KIND_CIRCLE, cb = Bs.kind == KIND_CIRCLE;
+#pragma unroll
+  for (int k = 0; k < 2 * MAXV; ++k) A.w[k] = Bs.w[k] = 0.0f;
+  A.w[0] = ca ? ga[0] : ga[0] + pxa;
+  A.w[1] = ca ? ga[1] + pxa : ga[1] + pya;
+  A.w[2] = ca ? ga[2] + pya : ga[2] + pxa;
+  A.w[3] = ca ? ga[3] : ga[3] + pya;
+  Bs.w[0] = cb ? gb[0] : gb[0] + pxb;
+  Bs.w[1] = cb ? gb[1] + pxb : gb[1] + pyb;
+  Bs.w[2] = cb ? gb[2] + pyb : gb[2] + pxb;
+  Bs.w[3] = cb ? gb[3] : gb[3] + pyb;
+  uint32_t er = 0u;
+  const Contact ct = run_contact_set<FNS_ANALYTIC>((int)((dw >> 20) & 7u), A, Bs, narrow_of(c.sh), &er,
+                                                   ((dw >> 27) & 1u) != 0u);
+  const int co = c.L.con + 4 * ci;
+  t.f(co + 0, e) = ct.pen.x;
+  t.f(co + 1, e) = ct.pen.y;
+  t.f(co + 2, e) = ct.cp.x;
+  t.f(co + 3, e) = ct.cp.y;
+  if (!(isn(ct.cp.x) || isn(ct.cp.y))) lds_or(t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
+  if (er) lds_or(t.w(c.L.err, e), er);
+}
+// stage 3: the contacts from the fetched words (post-Euler positions p + v dt,
+// euler_item's expression on the same operands)
 template <int EW>
 CX_DEV void ab_contacts(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, const ABRegs& r) {
-  using namespace cx;
-  const SceneHdr& sc = c.sh;
   const int ni = c.nc * EW, nch = ab_chunks<EW>(a, c);
   const bool eul = (a.stages & COTIX_STAGE_EULER) != 0;
 #pragma unroll
@@ -1363,45 +1397,74 @@ CX_DEV void ab_contacts(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
     if (q >= nch) continue;
     const int w = q * WAVE + lane, e = w % EW, ci = w / EW;
     if (w >= ni || env0 + e >= a.B) continue;
-    CXK_STAT(b_items, 1);
-    const uint32_t dw = r.dw[q];
-    Shape A, Bs;
-    A.kind = (int)((dw >> 23) & 3u);
-    Bs.kind = (int)((dw >> 25) & 3u);
-    A.n = Bs.n = 0;
-    // post-Euler positions (euler_item: p + v * dt) and the translate-only
-    // transforms of phase T (circle: (r, cx + px, cy + py); AABB: lo + p, up + p)
     const float* pa = r.pa[q];
     const float* pb = r.pb[q];
-    const float* ga = r.ga[q];
-    const float* gb = r.gb[q];
-    const float pxa = eul ? pa[0] + pa[2] * a.dt : pa[0], pya = eul ? pa[1] + pa[3] * a.dt : pa[1];
-    const float pxb = eul ? pb[0] + pb[2] * a.dt : pb[0], pyb = eul ? pb[1] + pb[3] * a.dt : pb[1];
-    const bool ca = A.kind == KIND_CIRCLE, cb = Bs.kind == KIND_CIRCLE;
+    ab_item<EW>(a, c, t, e, ci, r.dw[q], r.ga[q], r.gb[q], eul ? pa[0] + pa[2] * a.dt : pa[0],
+                eul ? pa[1] + pa[3] * a.dt : pa[1], eul ? pb[0] + pb[2] * a.dt : pb[0],
+                eul ? pb[1] + pb[3] * a.dt : pb[1]);
+  }
+}
+// Phase B of the analytic forward programs with more chunks than the fused
+// form takes (RoboCup: 160 items, 3 chunks): every launch-constant word of an
+// item -- its descriptor, its bodies, both parts' local geometry -- is read
+// ONCE per launch into the lane's registers (BConst, before the step loop);
+// a step's phase B then reads only its bodies' post-Euler positions (one LDS
+// round trip) and builds the world parts itself, so phase T (whose world
+// parts no forward phase of these scenes reads otherwise) does not run.
+constexpr int HQ = 4;  // chunks of 64 items held in registers
+struct BConst {
+  uint32_t dw[HQ], bw[HQ];
+  float ga[HQ][4], gb[HQ][4];
+};
+template <int EW>
+CX_DEV int bc_chunks(const Ctx& c) {
+  return (c.nc * EW + WAVE - 1) / WAVE;
+}
+template <int EW>
+CX_DEV void bc_fetch(const Ctx& c, Tile<EW> t, int lane, BConst& r) {
+  const SceneHdr& sc = c.sh;
+  const int ni = c.nc * EW, nch = bc_chunks<EW>(c);
 #pragma unroll
-    for (int k = 0; k < 2 * MAXV; ++k) A.w[k] = Bs.w[k] = 0.0f;
-    A.w[0] = ca ? ga[0] : ga[0] + pxa;
-    A.w[1] = ca ? ga[1] + pxa : ga[1] + pya;
-    A.w[2] = ca ? ga[2] + pya : ga[2] + pxa;
-    A.w[3] = ca ? ga[3] : ga[3] + pya;
-    Bs.w[0] = cb ? gb[0] : gb[0] + pxb;
-    Bs.w[1] = cb ? gb[1] + pxb : gb[1] + pyb;
-    Bs.w[2] = cb ? gb[2] + pyb : gb[2] + pxb;
-    Bs.w[3] = cb ? gb[3] : gb[3] + pyb;
-    uint32_t er = 0u;
-    const Contact ct = run_contact_set<FNS_ANALYTIC>((int)((dw >> 20) & 7u), A, Bs, narrow_of(sc), &er,
-                                                     ((dw >> 27) & 1u) != 0u);
-    const int co = c.L.con + 4 * ci;
-    t.f(co + 0, e) = ct.pen.x;
-    t.f(co + 1, e) = ct.pen.y;
-    t.f(co + 2, e) = ct.cp.x;
-    t.f(co + 3, e) = ct.cp.y;
-    if (!(isn(ct.cp.x) || isn(ct.cp.y))) {
-      lds_or(t.w(c.L.vm + (ci >> 5), e), 1u << (ci & 31));
+  for (int q = 0; q < HQ; ++q) {
+    r.dw[q] = r.bw[q] = 0u;
+    if (q >= nch) continue;  // uniform
+    const int w0 = q * WAVE + lane, w = w0 < ni ? w0 : ni - 1;  // clamped: every read in range
+    r.dw[q] = t.tb[sc.o_cdesc + 2 * (w / EW)];
+    r.bw[q] = t.tb[sc.o_cbody + w / EW];
+  }
+#pragma unroll
+  for (int q = 0; q < HQ; ++q) {
+    if (q >= nch) continue;
+    const int w0 = q * WAVE + lane, w = w0 < ni ? w0 : ni - 1, e = w % EW;
+    // analytic scenes: a part's world offset is its local-geometry offset (4 words per part)
+    const int la = c.L.geo + (int)(r.dw[q] & 1023u), lb = c.L.geo + (int)((r.dw[q] >> 10) & 1023u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r.ga[q][k] = t.f(la + k, e);
+      r.gb[q][k] = t.f(lb + k, e);
     }
-    if (er) {
-      lds_or(t.w(c.L.err, e), er);
-    }
+  }
+}
+template <int EW>
+CX_DEV void ph_B_const(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, const BConst& r) {
+  const int ni = c.nc * EW, nch = bc_chunks<EW>(c);
+  float px[HQ][2][2];  // every chunk's positions read before any is used (one round trip)
+#pragma unroll
+  for (int q = 0; q < HQ; ++q) {
+    if (q >= nch) continue;
+    const int w0 = q * WAVE + lane, w = w0 < ni ? w0 : ni - 1, e = w % EW;
+    const int oa = c.L.dyn + 6 * (int)(r.bw[q] & 255u), ob = c.L.dyn + 6 * (int)((r.bw[q] >> 8) & 255u);
+    px[q][0][0] = t.f(oa, e);
+    px[q][0][1] = t.f(oa + 1, e);
+    px[q][1][0] = t.f(ob, e);
+    px[q][1][1] = t.f(ob + 1, e);
+  }
+#pragma unroll
+  for (int q = 0; q < HQ; ++q) {
+    if (q >= nch) continue;
+    const int w = q * WAVE + lane, e = w % EW, ci = w / EW;
+    if (w >= ni || env0 + e >= a.B) continue;
+    ab_item<EW>(a, c, t, e, ci, r.dw[q], r.ga[q], r.gb[q], px[q][0][0], px[q][0][1], px[q][1][0], px[q][1][1]);
   }
 }
 template <int EW, int FNSET>
@@ -2947,6 +3010,12 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });
   }
 
+  // analytic scenes beyond the fused form's chunks: phase B's launch-constant
+  // item words in registers for the whole launch (ph_B_const)
+  const bool bconst = FNSET == FNS_ANALYTIC && c.nc * EW > ABQ * WAVE && c.nc * EW <= HQ * WAVE &&
+                      (a.stages & COTIX_STAGE_COLLIDER) != 0 && !CXK_SKIP(a, 2);
+  BConst bc;
+  if (bconst) run(PH_B, [&](int l) { bc_fetch<EW>(c, t, l, bc); });
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
@@ -2966,7 +3035,13 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     const int kso = c.L.kw + slot * c.L.kww;  // this step's sk0, skt in the key window
     // phases A, T, B as one (circle / AABB scenes whose contact items fit the
     // phase's ABQ prefetched chunks; uniform)
-    if (FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE) {
+    if (bconst) {  // phase A, then B from the launch-constant item words (no phase T)
+      run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
+      if (a.stages & COTIX_STAGE_COLLIDER) {
+        run(PH_B, [&](int l) { ph_B_const<EW>(a, c, t, env0, l, bc); });
+        collider_phases<EW, FNSET, true, R, true>(a, c, t, env0, run, slot, kso);
+      }
+    } else if (FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE) {
       // stage 1 reads the pre-Euler state: every read is issued before phase
       // A's writes (stage 2); stage 3 computes the contacts
       run.template staged<ABRegs>(

@@ -854,17 +854,24 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
       if (env0 + e < a.B) euler_item<EW, EVAL>(a, c, t, env0, e, b, step);
     }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
-    for (int e = lane; e < EW; e += WAVE) {
-      if (!PRE && !CXK_SKIP(a, 16)) {
-        const bool part = c.sh.prng != 0;
+    if (!PRE && !CXK_SKIP(a, 16)) {
+      // (the backward re-play: the step's keys from its saved key) on a lane
+      // pair per env (split_at_pair: each lane one block of each split)
+      const bool part = c.sh.prng != 0;
+      for (int w = lane; w < 2 * EW; w += WAVE) {
+        const int e = w >> 1, h = w & 1;
         key2 k = key2{t.w(L.key, e), t.w(L.key + 1, e)};
-        key2 s = split_at_l(k, 2u, 0u, part);  // cotix/_colliders.py:142 == next driver key
-        t.w(L.sk0, e) = s.a;
-        t.w(L.sk0 + 1, e) = s.b;
+        key2 s = split_at_pair(k, 2u, 0u, h, part);  // cotix/_colliders.py:142 == next driver key
+        if (h == 0) {
+          t.w(L.sk0, e) = s.a;
+          t.w(L.sk0 + 1, e) = s.b;
+        }
         for (int q = 0; q < c.nt; ++q) {  // :175, one split per type key
-          s = split_at_l(s, 2u, 0u, part);
-          t.w(L.skt + 2 * q, e) = s.a;
-          t.w(L.skt + 2 * q + 1, e) = s.b;
+          s = split_at_pair(s, 2u, 0u, h, part);
+          if (h == 0) {
+            t.w(L.skt + 2 * q, e) = s.a;
+            t.w(L.skt + 2 * q + 1, e) = s.b;
+          }
         }
       }
     }
@@ -2766,31 +2773,64 @@ CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
   }
 }
 
+// the return weights, staged once per launch into the tile's restart-state
+// words (the rollout programs never restart): a step reads them from LDS,
+// not per term from the kernel arguments (a dynamic index there is a memory
+// load per term and step)
+template <int EW>
+CX_DEV void stage_ret_w(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) {
+  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) t.f(c.L.rst + w / EW, w % EW) = a.ret_w[w / EW];
+}
 // return accumulation after a step: ret += sum_k w_k * state_k (w_k != 0)
 template <int EW>
 CX_DEV void ph_ret(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int e = lane; e < EW; e += WAVE) {
     if (env0 + e >= a.B) continue;
     float acc = t.f(c.L.ret, e);
-    for (int k = 0; k < c.nb * 6; ++k)
-      if (a.ret_w[k] != 0.0f) acc = acc + a.ret_w[k] * t.f(c.L.dyn + k, e);
+    for (int k = 0; k < c.nb * 6; ++k) {
+      const float w = t.f(c.L.rst + k, e);
+      acc = w != 0.0f ? acc + w * t.f(c.L.dyn + k, e) : acc;  // (terms with w == 0 skipped)
+    }
     t.f(c.L.ret, e) = acc;
   }
 }
 
-// backward: state before step `step` from the saved trajectory
+// backward: the saved state of step `step`, read into registers one step
+// ahead (restore_fetch in the previous step's restore phase), so the global
+// reads are in flight while that step re-plays and differentiates
+constexpr int RQ = (MAXB * 6 * 8 + 63) / 64;  // words per lane: nb * 6 * EW over 64 lanes (EW <= 8)
+struct RestoreRegs {
+  float d[RQ];
+  uint32_t k0 = 0u, k1 = 0u;
+};
 template <int EW>
-CX_DEV void ph_restore(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+CX_DEV void restore_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step, RestoreRegs& r) {
   const size_t base = (size_t)step * c.nb * 6 * a.B;
-  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
-    int e = w % EW, off = w / EW, g = env0 + e;
-    t.f(c.L.dyn + off, e) = (g < a.B) ? a.save_dyn[base + (size_t)off * a.B + g] : 0.0f;
+  const int nd = c.nb * 6 * EW;
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    const int w = q * WAVE + lane, e = w % EW, off = w / EW, g = env0 + e;
+    if (q * WAVE >= nd) break;  // uniform
+    r.d[q] = (w < nd && g < a.B) ? a.save_dyn[base + (size_t)off * a.B + g] : 0.0f;
   }
-  for (int e = lane; e < EW; e += WAVE) {
-    int g = env0 + e;
-    t.w(c.L.key, e) = (g < a.B) ? a.save_keys[2 * ((size_t)step * a.B + g)] : 0u;
-    t.w(c.L.key + 1, e) = (g < a.B) ? a.save_keys[2 * ((size_t)step * a.B + g) + 1] : 0u;
-    t.w(c.L.err, e) = 0u;
+  const int g = env0 + lane;
+  const bool le = lane < EW && g < a.B;
+  r.k0 = le ? a.save_keys[2 * ((size_t)step * a.B + g)] : 0u;
+  r.k1 = le ? a.save_keys[2 * ((size_t)step * a.B + g) + 1] : 0u;
+}
+template <int EW>
+CX_DEV void restore_apply(const Ctx& c, Tile<EW> t, int lane, const RestoreRegs& r) {
+  const int nd = c.nb * 6 * EW;
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    const int w = q * WAVE + lane;
+    if (q * WAVE >= nd) break;  // uniform
+    if (w < nd) t.f(c.L.dyn + w / EW, w % EW) = r.d[q];
+  }
+  if (lane < EW) {
+    t.w(c.L.key, lane) = r.k0;
+    t.w(c.L.key + 1, lane) = r.k1;
+    t.w(c.L.err, lane) = 0u;
   }
 }
 
@@ -2888,7 +2928,7 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         t.f(o + 5, e) = t.f(o + 5, e) + t.f(o + 4, e) * a.dt;
       }
       if (step > 0)
-        for (int k = 0; k < 6; ++k) t.f(o + k, e) = t.f(o + k, e) + a.ret_w[6 * b + k];
+        for (int k = 0; k < 6; ++k) t.f(o + k, e) = t.f(o + k, e) + t.f(L.rst + 6 * b + k, e);  // ret_w (staged)
     }
   }
 }
@@ -2997,8 +3037,10 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
 template <int EW, bool ROLL, bool EVAL = false>
 CX_DEV void ph_load_fwd(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int l) {
   ph_load<EW, EVAL>(a, c, t, env0, l);
-  if (ROLL)
+  if (ROLL) {
     for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
+    stage_ret_w<EW>(a, c, t, l);
+  }
 }
 template <int EW, int FNSET, bool ROLL, bool EVAL = false, class R = void>
 CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, bool loaded = false) {
@@ -3083,10 +3125,16 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
   run(PH_ADJ, [&](int l) {
     ph_geo<EW>(a, c, t, env0, l);
     ph_adj_init<EW>(a, c, t, env0, l);
+    stage_ret_w<EW>(a, c, t, l);
     for (int e = l; e < EW; e += WAVE) t.w(c.L.pcv, e) = 0u;  // phase T's pose entries
   });
+  RestoreRegs rr;
+  if (a.n_steps > 0) run(PH_RESTORE, [&](int l) { restore_fetch<EW>(a, c, env0, l, a.n_steps - 1, rr); });
   for (int step = a.n_steps - 1; step >= 0; --step) {
-    run(PH_RESTORE, [&](int l) { ph_restore<EW>(a, c, t, env0, l, step); });
+    run(PH_RESTORE, [&](int l) {
+      restore_apply<EW>(c, t, l, rr);
+      if (step > 0) restore_fetch<EW>(a, c, env0, l, step - 1, rr);  // the next (earlier) step, in flight
+    });
     run(PH_A, [&](int l) { ph_A<EW, false>(a, c, t, env0, l, step); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0, c.L.sk0);
     run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });

@@ -218,6 +218,8 @@ def valu_roofline(scenario, B, substeps, launch_ms, warmup=None, layout="legacy"
                 "traffic": pmc["hbm_bytes_per_launch_corrected"],
                 "source": "profiles/%s_%s_summary.json" % (pmc["tag"], scenario),
                 "valu_active_frac_of_wave_cycles": pmc["valu_active_frac_of_wave_cycles"],
+                "wait_frac_of_wave_cycles": pmc.get("wait_frac_of_wave_cycles"),
+                "stall": pmc.get("stall"),
                 "pmc_avg_launch_ms": pmc["avg_launch_ns"] * 1e-6}
     except (OSError, KeyError, ValueError):
         return None
@@ -249,6 +251,7 @@ def roofline(scenario, B, substeps, launch_ms, nb, layout="legacy"):
         ach = v["valu_instr_per_launch"] / (launch_ms * 1e-3)
         out.update(achieved=ach / 1e9, frac=ach / VALU_PEAK_WAVE_INSTR_S, traffic=v["traffic"],
                    traffic_source=v["source"], valu_active_frac_of_wave_cycles=v["valu_active_frac_of_wave_cycles"],
+                   wait_frac_of_wave_cycles=v["wait_frac_of_wave_cycles"], stall=v["stall"],
                    pmc_avg_launch_ms=v["pmc_avg_launch_ms"])
     return out
 

@@ -25,6 +25,9 @@ for wl in "robocup:--scenario robocup --warmup 2" "lunar:--scenario lunar --warm
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $P/pmc_fetch -o run --output-format csv -- $B > /dev/null 2> $P/pmc1.err || { tail $P/pmc1.err; exit 3; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $P/pmc_write -o run --output-format csv -- $B > /dev/null 2> $P/pmc2.err || { tail $P/pmc2.err; exit 4; }
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU -d $P/pmc_sq -o run --output-format csv -- $B > /dev/null 2> $P/pmc3.err || { tail $P/pmc3.err; exit 5; }
+  # the stall attribution: wave cycles = issuing (ACTIVE_INST_ANY) + parked on
+  # waitcnt / barrier (WAIT_ANY) + issue-stalled (WAIT_INST_ANY, of it LDS)
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT -d $P/pmc_stall -o run --output-format csv -- $B > /dev/null 2> $P/pmc4.err || { tail $P/pmc4.err; exit 6; }
   echo "profile $sc ok"
 done
 timeout -k 10 200 python tools/phase_prof.py > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --scenario lunar > $O/phase_lunar.json && echo "phase ok"

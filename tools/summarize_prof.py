@@ -28,6 +28,21 @@ def last_dispatches(rows, n):
     return [r for r in rows if int(r["Dispatch_Id"]) in keep]
 
 
+def stall_fracs(s):
+    """The stall pass's buckets as fractions of its own wave cycles."""
+    if not s:
+        return None
+    w = s["SQ_WAVE_CYCLES"]
+    return {"active_any": s["SQ_ACTIVE_INST_ANY"] / w, "active_valu": s["SQ_ACTIVE_INST_VALU"] / w,
+            "active_lds": s["SQ_ACTIVE_INST_LDS"] / w, "wait_any": s["SQ_WAIT_ANY"] / w,
+            "wait_inst_any": s["SQ_WAIT_INST_ANY"] / w, "wait_inst_lds": s["SQ_WAIT_INST_LDS"] / w,
+            "lds_bank_conflict_cycles_per_lds_active": s["SQ_LDS_BANK_CONFLICT"] / max(s["SQ_ACTIVE_INST_LDS"], 1.0)}
+
+
+def have(d):
+    return os.path.exists(os.path.join(src, d, "run_counter_collection.csv"))
+
+
 def pmc(d, n=None):
     rows = [r for r in csv.DictReader(open(os.path.join(src, d, "run_counter_collection.csv"))) if K in r["Kernel_Name"]]
     if n:
@@ -67,7 +82,8 @@ if scen.startswith("grad"):
                          "hbm_bytes_per_launch_raw": (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024,
                          "hbm_bytes_per_launch_corrected": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024,
                          "valu_active_frac_of_wave_cycles": c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"],
-                         "wait_frac_of_wave_cycles": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]}
+                         "wait_frac_of_wave_cycles": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
+                         "stall": stall_fracs(pmc_k("pmc_stall", row["Name"]) if have("pmc_stall") else None)}
     summary = {"tag": tag, "scenario": scen, "config": bench["config"], "library": bench["config"]["library"],
                "bench_value": bench["value"], "warmup": bench["warmup"], "steps": bench["steps"], "kernels": kernels}
     os.makedirs(out, exist_ok=True)
@@ -109,13 +125,15 @@ summary = {
     "counters_per_launch": c,
     "valu_active_frac_of_wave_cycles": c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"],
     "wait_frac_of_wave_cycles": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
+    "stall": stall_fracs(pmc("pmc_stall", nt) if have("pmc_stall") else None),
 }
 os.makedirs(out, exist_ok=True)
 json.dump(summary, open(os.path.join(out, "%s_%s_summary.json" % (tag, scen)), "w"), indent=1)
 json.dump(summary, open(os.path.join(out, "latest_pmc_%s.json" % scen), "w"), indent=1)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, "%s_%s_kernel_stats.csv" % (tag, scen)))
-for d in ("pmc_fetch", "pmc_write", "pmc_sq"):
-    shutil.copy(os.path.join(src, d, "run_counter_collection.csv"), os.path.join(out, "%s_%s_%s.csv" % (tag, scen, d)))
+for d in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_stall"):
+    if have(d):
+        shutil.copy(os.path.join(src, d, "run_counter_collection.csv"), os.path.join(out, "%s_%s_%s.csv" % (tag, scen, d)))
 print(json.dumps({k: summary[k] for k in ("avg_launch_ns", "bench_event_launch_ms", "hbm_bytes_per_launch_raw",
                                           "hbm_bytes_per_launch_corrected", "valu_active_frac_of_wave_cycles",
-                                          "wait_frac_of_wave_cycles")}, indent=1))
+                                          "wait_frac_of_wave_cycles", "stall")}, indent=1))

@@ -476,7 +476,6 @@ void lockstep();
 uint64_t ballot(bool p);
 uint32_t bpermute(int src, uint32_t v);
 uint32_t pair_swap(uint32_t v);
-uint32_t quad_perm(uint32_t v, int src);
 }  // namespace cxk_simt
 namespace cxk {
 #define CXK_WAVE_OP static inline __attribute__((always_inline))
@@ -529,17 +528,6 @@ CXK_WAVE_OP uint32_t pair_swap_u32(uint32_t v) {
 #endif
 }
 CXK_WAVE_OP float pair_swap_f32(float x) { return __builtin_bit_cast(float, pair_swap_u32(__builtin_bit_cast(uint32_t, x))); }
-// the value v of lane S of this lane's quad (DPP quad_perm(S,S,S,S); the
-// quad's four lanes active)
-template <int S>
-CXK_WAVE_OP float quad_bcast_f32(float x) {
-#if defined(__HIP__)
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), S | (S << 2) | (S << 4) | (S << 6),
-                                                    0xF, 0xF, false));
-#else
-  return __builtin_bit_cast(float, ::cxk_simt::quad_perm(__builtin_bit_cast(uint32_t, x), S));
-#endif
-}
 // an LDS word OR-ed by several lanes of a phase
 CXK_WAVE_OP void lds_or(uint32_t& w, uint32_t v) {
 #if defined(__HIP__)
@@ -2393,55 +2381,10 @@ CX_DEV cx::ResPre load_rp(Tile<EW> t, int ro, int e) {
   return p;
 }
 
-// cx::resolve_seq on a QUAD of lanes (one env): the four divisions of the
-// impulse -- ni = nim / den, vdu = vd / |vd| (two), idr = -|vd| / den --
-// one per lane (q = lane & 3) and broadcast to the quad (DPP), instead of
-// four in a row on one lane; every other expression is the same, on every
-// lane of the quad, so the quad holds identical values throughout.
-template <bool RCP>
-CX_DEV bool resolve_seq_quad(float& vx1, float& vy1, float& w1, const cx::Params& m1, cx::Rcp q1, float& vx2,
-                             float& vy2, float& w2, const cx::Params& m2, cx::Rcp q2, const cx::ResPre& p, int q) {
-  using namespace cx;
-  const v2 v1 = v2{vx1 + (-p.r1.y) * w1, vy1 + p.r1.x * w1};  // velocity_at(b1, cp)
-  const v2 v2_ = v2{vx2 + (-p.r2.y) * w2, vy2 + p.r2.x * w2};
-  const v2 relv = sub(v2_, v1);
-  if (dot(p.pen, relv) < 0.0f) return false;  // (moving apart: the quad's four lanes alike)
-  const float vn = dot(relv, p.n);
-  const float nim = p.ne * vn - p.pterm;
-  const v2 vd = v2{relv.x + vn * p.n.x, relv.y + vn * p.n.y};
-  const float vdn = nrm(vd);
-  const float num = q == 0 ? nim : (q == 1 ? vd.x : (q == 2 ? vd.y : -vdn));
-  const float dnm = (q == 0 || q == 3) ? p.den : vdn;
-  const float r = num / dnm;
-  const float ni = quad_bcast_f32<0>(r);
-  const v2 vdu = v2{quad_bcast_f32<1>(r), quad_bcast_f32<2>(r)};
-  float idr = quad_bcast_f32<3>(r);
-  v2 imp = scl(p.n, ni);
-  idr = clip_(idr, 0.0f, ni * p.mu);
-  imp = add(imp, scl(vdu, idr));
-  // apply_impulse(b1, -imp, cp), apply_impulse(b2, imp, cp)  (:68-73)
-  const v2 i1 = neg(imp);
-  const float t1 = crs(p.r1, i1), t2 = crs(p.r2, imp);
-  vx1 = vx1 + div_r<RCP>(i1.x, m1.mass, q1.m);
-  vy1 = vy1 + div_r<RCP>(i1.y, m1.mass, q1.m);
-  w1 = w1 + div_r<RCP>(t1, m1.inertia, q1.i);
-  vx2 = vx2 + div_r<RCP>(imp.x, m2.mass, q2.m);
-  vy2 = vy2 + div_r<RCP>(imp.y, m2.mass, q2.m);
-  w2 = w2 + div_r<RCP>(t2, m2.inertia, q2.i);
-  return true;
-}
-// the resolution of one env, on one lane (q < 0) or on a quad (q = lane & 3)
-template <bool RCP>
-CX_DEV bool resolve_any(float& vx1, float& vy1, float& w1, const cx::Params& m1, cx::Rcp q1, float& vx2, float& vy2,
-                        float& w2, const cx::Params& m2, cx::Rcp q2, const cx::ResPre& p, int q) {
-  return q < 0 ? cx::resolve_seq<RCP>(vx1, vy1, w1, m1, q1, vx2, vy2, w2, m2, q2, p)
-               : resolve_seq_quad<RCP>(vx1, vy1, w1, m1, q1, vx2, vy2, w2, m2, q2, p, q);
-}
-
 // E1 sequential pass, NB (== nb) bodies' velocities in registers; body j is
 // picked and written back by unrolled selects (no scratch)
 template <int EW, bool REC, int NB, bool RCP>
-CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e, int q) {
+CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
@@ -2495,7 +2438,7 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e, int q) {
       t.f(rc + 5, e) = jy;
       t.f(rc + 6, e) = jw;
     }
-    const bool applied = resolve_any<RCP>(vx[i], vy[i], vw[i], pi[i], qi[i], jx, jy, jw, pj[i], qj[i], pr[i], q);
+    const bool applied = resolve_seq<RCP>(vx[i], vy[i], vw[i], pi[i], qi[i], jx, jy, jw, pj[i], qj[i], pr[i]);
     if (REC) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
 #pragma unroll
     for (int b = 0; b < NB; ++b)
@@ -2514,7 +2457,7 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e, int q) {
 }
 // E1 for any body count: the same pass on the LDS tile
 template <int EW, bool REC, bool RCP>
-CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e, int q) {
+CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
@@ -2538,8 +2481,8 @@ CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e, int q) {
     const Params pi = load_par(t.tb, sc.o_par + 4 * i);
     const Params pj = Params{t.f(ro + RP_MJ, e), t.f(ro + RP_IJ, e), 0.0f, 0.0f};
     const Rcp qj = Rcp{t.f(ro + RP_QMJ, e), t.f(ro + RP_QIJ, e)};
-    const bool applied = resolve_any<RCP>(ix, iy, iw, pi, load_rcp(t.tb, sc.o_rcp + 2 * i), jx, jy, jw, pj, qj,
-                                          load_rp<EW>(t, ro, e), q);
+    const bool applied = resolve_seq<RCP>(ix, iy, iw, pi, load_rcp(t.tb, sc.o_rcp + 2 * i), jx, jy, jw, pj, qj,
+                                     load_rp<EW>(t, ro, e));
     if (REC) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
     t.f(oi + 2, e) = ix;
     t.f(oi + 3, e) = iy;
@@ -2561,29 +2504,6 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   const SceneHdr& sc = c.sh;
   const int nb = c.nb;
   const Lay& L = c.L;
-  // the sequential resolutions of env e on the quad of lanes 4e .. 4e+3
-  // (resolve_seq_quad); the rest of the phase on the quad's first lane
-  for (int w = lane; w < 4 * EW; w += WAVE) {
-    const int e = w >> 2, q = w & 3;
-    int g = env0 + e;
-    if (g >= a.B) continue;  // (the whole quad)
-    if (a.stages & COTIX_STAGE_COLLIDER) {
-      if (sc.rcp_all) {
-        switch (nb) {
-          case 4: e1_regs<EW, REC, 4, true>(c, t, e, q); break;
-          case 5: e1_regs<EW, REC, 5, true>(c, t, e, q); break;
-          default: e1_tile<EW, REC, true>(c, t, e, q); break;
-        }
-      } else {
-        switch (nb) {
-          case 4: e1_regs<EW, REC, 4, false>(c, t, e, q); break;
-          case 5: e1_regs<EW, REC, 5, false>(c, t, e, q); break;
-          default: e1_tile<EW, REC, false>(c, t, e, q); break;
-        }
-      }
-    }
-  }
-  lockstep();  // every quad's velocities before the per-env tail reads them
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g >= a.B) continue;
@@ -2607,6 +2527,21 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
       (void)wslots;
     }
 #endif
+    if (a.stages & COTIX_STAGE_COLLIDER) {
+      if (sc.rcp_all) {
+        switch (nb) {
+          case 4: e1_regs<EW, REC, 4, true>(c, t, e); break;
+          case 5: e1_regs<EW, REC, 5, true>(c, t, e); break;
+          default: e1_tile<EW, REC, true>(c, t, e); break;
+        }
+      } else {
+        switch (nb) {
+          case 4: e1_regs<EW, REC, 4, false>(c, t, e); break;
+          case 5: e1_regs<EW, REC, 5, false>(c, t, e); break;
+          default: e1_tile<EW, REC, false>(c, t, e); break;
+        }
+      }
+    }
     if ((a.stages & COTIX_STAGE_LUNAR) && nb >= 3) {
       Dyn d[3];
 #pragma unroll

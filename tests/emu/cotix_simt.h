@@ -11,8 +11,7 @@
 // Resolution rules (cxk_simt:: primitives, cotix_kernel.h):
 //  * pair operations (pair_swap: quad_perm(1,0,3,2)) resolve per lane pair,
 //    as soon as both lanes wait at one -- their n-th each (the two lanes of
-//    a pair run their exchanges in lockstep; a count mismatch aborts); quad
-//    permutes (quad_perm(S,S,S,S) broadcasts) likewise per quad of lanes;
+//    a pair run their exchanges in lockstep; a count mismatch aborts);
 //  * wave operations (sync, lockstep, ballot, bpermute) are convergent: they
 //    resolve when every live lane waits at its n-th wave operation, the same
 //    operation on every lane (anything else aborts as a divergent collective
@@ -78,7 +77,7 @@ constexpr size_t STACK = 4u << 20;
 constexpr size_t STACK = 1u << 20;
 #endif
 
-enum Op : int { OP_NONE = 0, OP_SYNC, OP_LOCKSTEP, OP_BALLOT, OP_BPERMUTE, OP_PAIR_SWAP, OP_QUAD_PERM };
+enum Op : int { OP_NONE = 0, OP_SYNC, OP_LOCKSTEP, OP_BALLOT, OP_BPERMUTE, OP_PAIR_SWAP };
 enum State : int { RUN = 0, WAIT, DONE };
 
 struct Fiber {
@@ -88,7 +87,7 @@ struct Fiber {
   int op = OP_NONE;
   const void* site = nullptr;
   uint64_t in = 0, out = 0;
-  uint64_t npair = 0, nquad = 0, nwave = 0;  // pair / quad / wave operations resolved so far
+  uint64_t npair = 0, nwave = 0;  // pair / wave operations resolved so far
 #if CXS_ASAN
   void* fake = nullptr;
 #endif
@@ -211,24 +210,6 @@ inline void run(const std::function<void(int)>& body) {
         resolved = true;
       }
     }
-    // quad permutes (quad_perm: each lane names the quad lane it reads)
-    for (int l = 0; l < NL; l += 4) {
-      bool all = true;
-      for (int k = 0; k < 4; ++k) all = all && w.f[l + k].state == WAIT && w.f[l + k].op == OP_QUAD_PERM;
-      if (!all) continue;
-      for (int k = 1; k < 4; ++k)
-        if (w.f[l + k].nquad != w.f[l].nquad) fail("quad permute out of step (the lanes' counts differ)", l + k);
-      for (int k = 0; k < 4; ++k) {
-        Fiber& f = w.f[l + k];
-        const int src = (int)(f.in >> 32) & 3;
-        f.out = w.f[l + src].in & 0xFFFFFFFFull;
-      }
-      for (int k = 0; k < 4; ++k) {
-        ++w.f[l + k].nquad;
-        w.f[l + k].state = RUN;
-      }
-      resolved = true;
-    }
     if (resolved) continue;
     // then one wave operation, with every live lane
     int lead = -1;
@@ -237,7 +218,6 @@ inline void run(const std::function<void(int)>& body) {
       const Fiber& f = w.f[l];
       if (f.state == DONE) continue;
       if (f.op == OP_PAIR_SWAP) fail("pair exchange whose partner waits elsewhere or has left", l);
-      if (f.op == OP_QUAD_PERM) fail("quad permute whose quad waits elsewhere or has left", l);
       if (lead < 0) lead = l;
       const Fiber& g = w.f[lead];
       if (f.op != g.op || f.nwave != g.nwave) {
@@ -278,9 +258,6 @@ __attribute__((noinline)) uint32_t bpermute(int src, uint32_t v) {
 }
 __attribute__((noinline)) uint32_t pair_swap(uint32_t v) {
   return (uint32_t)wait(OP_PAIR_SWAP, __builtin_return_address(0), v);
-}
-__attribute__((noinline)) uint32_t quad_perm(uint32_t v, int src) {
-  return (uint32_t)wait(OP_QUAD_PERM, __builtin_return_address(0), ((uint64_t)(uint32_t)src << 32) | v);
 }
 
 }  // namespace cxk_simt

@@ -1419,6 +1419,9 @@ CX_DEV void ab_contacts(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
 // round trip) and builds the world parts itself, so phase T (whose world
 // parts no forward phase of these scenes reads otherwise) does not run.
 constexpr int HQ = 4;  // chunks of 64 items held in registers
+#ifndef COTIX_BCONST_MIN_STEPS  // build-time A/B knob of the tooling: the fewest steps per launch that use it
+#define COTIX_BCONST_MIN_STEPS 1
+#endif
 struct BConst {
   uint32_t dw[HQ], bw[HQ];
   float ga[HQ][4], gb[HQ][4];
@@ -2773,23 +2776,65 @@ CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
   }
 }
 
-// the return weights, staged once per launch into the tile's restart-state
-// words (the rollout programs never restart): a step reads them from LDS,
-// not per term from the kernel arguments (a dynamic index there is a memory
-// load per term and step)
+// The return weights, staged once per launch into the tile's restart-state
+// words (the rollout programs never restart), so that no step reads them from
+// the kernel arguments (a dynamic index there is a memory load per term and
+// step).  The backward (G3) reads them dense: word k of body-state word k.
+// The forward's return sums only the nonzero terms, compacted in k order
+// (ballots): word 0 the count n, then (k, w) pairs -- two LDS round trips per
+// step for up to RT terms (the return of config 5 has one).
+constexpr int RT = 8;
 template <int EW>
 CX_DEV void stage_ret_w(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) {
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) t.f(c.L.rst + w / EW, w % EW) = a.ret_w[w / EW];
 }
-// return accumulation after a step: ret += sum_k w_k * state_k (w_k != 0)
+CX_DEV int ret_terms_cap(const Ctx& c) {
+  const int cap = (c.nb * 6 - 1) / 2;
+  return cap < RT ? cap : RT;
+}
+template <int EW>
+CX_DEV void stage_ret_terms(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) {
+  const int nk = c.nb * 6;  // <= MAXB * 6 = 96
+  const float w0 = lane < nk ? a.ret_w[lane] : 0.0f, w1 = lane + WAVE < nk ? a.ret_w[lane + WAVE] : 0.0f;
+  const uint64_t m0 = ballot(w0 != 0.0f), m1 = ballot(w1 != 0.0f);
+  const int n0 = popc64(m0), n = n0 + popc64(m1), cap = ret_terms_cap(c);
+  const int r0 = popc64(m0 & lanes_below(lane)), r1 = n0 + popc64(m1 & lanes_below(lane));
+  if (n <= cap) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float w = h ? w1 : w0;
+      const int r = h ? r1 : r0;
+      if (w != 0.0f)
+        for (int e = 0; e < EW; ++e) {
+          t.w(c.L.rst + 1 + 2 * r, e) = (uint32_t)(lane + h * WAVE);
+          t.f(c.L.rst + 2 + 2 * r, e) = w;
+        }
+    }
+  }
+  if (lane < EW) t.w(c.L.rst, lane) = (uint32_t)n;
+}
+// return accumulation after a step: ret += sum_k w_k * state_k (w_k != 0), k ascending
 template <int EW>
 CX_DEV void ph_ret(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int e = lane; e < EW; e += WAVE) {
     if (env0 + e >= a.B) continue;
     float acc = t.f(c.L.ret, e);
-    for (int k = 0; k < c.nb * 6; ++k) {
-      const float w = t.f(c.L.rst + k, e);
-      acc = w != 0.0f ? acc + w * t.f(c.L.dyn + k, e) : acc;  // (terms with w == 0 skipped)
+    const int n = (int)t.w(c.L.rst, e);
+    if (n <= ret_terms_cap(c)) {
+      int kk[RT];
+      float ww[RT], sv[RT];
+#pragma unroll
+      for (int j = 0; j < RT; ++j) {
+        kk[j] = j < n ? (int)t.w(c.L.rst + 1 + 2 * j, e) : 0;
+        ww[j] = j < n ? t.f(c.L.rst + 2 + 2 * j, e) : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < RT; ++j) sv[j] = t.f(c.L.dyn + kk[j], e);
+#pragma unroll
+      for (int j = 0; j < RT; ++j) acc = j < n ? acc + ww[j] * sv[j] : acc;
+    } else {  // more terms than the list holds: every weight from the kernel arguments
+      for (int k = 0; k < c.nb * 6; ++k)
+        if (a.ret_w[k] != 0.0f) acc = acc + a.ret_w[k] * t.f(c.L.dyn + k, e);
     }
     t.f(c.L.ret, e) = acc;
   }
@@ -3080,7 +3125,7 @@ CX_DEV void ph_load_fwd(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
   ph_load<EW, EVAL>(a, c, t, env0, l);
   if (ROLL) {
     for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
-    stage_ret_w<EW>(a, c, t, l);
+    stage_ret_terms<EW>(a, c, t, l);
   }
 }
 template <int EW, int FNSET, bool ROLL, bool EVAL = false, class R = void>
@@ -3096,7 +3141,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   // analytic scenes beyond the fused form's chunks: phase B's launch-constant
   // item words in registers for the whole launch (ph_B_const)
   const bool bconst = FNSET == FNS_ANALYTIC && c.nc * EW > ABQ * WAVE && c.nc * EW <= HQ * WAVE &&
-                      (a.stages & COTIX_STAGE_COLLIDER) != 0 && !CXK_SKIP(a, 2);
+                      (a.stages & COTIX_STAGE_COLLIDER) != 0 && !CXK_SKIP(a, 2) &&
+                      a.n_steps >= COTIX_BCONST_MIN_STEPS;
   BConst bc;
   if (bconst) run(PH_B, [&](int l) { bc_fetch<EW>(c, t, l, bc); });
   for (int step = 0; step < a.n_steps; ++step) {

@@ -106,3 +106,25 @@ def test_backward_rejects_polygon_scenes(emu_lib):
     with pytest.raises(RuntimeError, match="circle/AABB"):
         emu.rollout_backward(lib, h, sd, sk, geom, 0, 1 | 4 | 16, np.zeros((1, 1, 2), np.float32), 0,
                              np.zeros(24, np.float32))
+
+
+@pytest.mark.parametrize("nterms", [8, 42])
+def test_emu_rollout_return_terms(emu_lib, nterms):
+    """The forward's return over more nonzero weights: 8 terms (the compact
+    list's capacity) and all 42 (past it: the weights from the kernel
+    arguments), bit-exact returns and the gradients vs the VJP oracle."""
+    emu, lib = emu_lib
+    B, T = 3, 8
+    case = GC.box_case(B, T, seed=2)
+    rng = np.random.default_rng(5)
+    w = np.zeros(7 * 6, np.float32)
+    idx = np.sort(rng.choice(42, nterms, replace=False))
+    w[idx] = rng.uniform(-1, 1, nterms).astype(np.float32)
+    case["w"] = w
+    ret, ga, gd, _ = _emu_run(emu, lib, case)
+    orc = GC.oracle(case)
+    for e in range(B):
+        r, oga, ogS = orc[e]
+        assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)
+        ok, msg = GC.close(ga[:, e], oga)
+        assert ok, "env %d grad_action: %s" % (e, msg)

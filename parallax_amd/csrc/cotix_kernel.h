@@ -2891,96 +2891,9 @@ CX_DEV void ph_adj_init(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
 // d state_{step+1}; the tile holds the re-played step (post-Euler positions,
 // contacts, choices, recorded pre-resolution velocities).  Exit: adj = d ret
 // / d state_step, grad_action[step] written.
-// Phase G in three parts.  G1 (one lane per env, the resolutions in reverse
-// order): resolve_vjp on the adjoint chain; each resolution's contact
-// cotangents (gpen, gcp) replace its recorded velocities (rec words 1-4,
-// read just before).  G2 (one (resolution, env) item per lane, in parallel):
-// the contact's VJP on its world parts -> the position cotangents of the two
-// parts' bodies, into rec words 1-4.  G3 (one lane per env): those added to
-// the adjoint in reverse resolution order, then the action gradient, Euler's
-// reverse and the return weights.  The contact VJPs depend on the chain only
-// through (gpen, gcp), so they leave its critical path; the position
-// adjoints are the same sums re-associated (the contact terms added after the
-// chain's own position terms instead of interleaved).
 template <int EW>
-CX_DEV void ph_G1(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   using namespace cx;
-  const SceneHdr& sc = c.sh;
-  const int nb = c.nb;
-  const Lay& L = c.L;
-  for (int e = lane; e < EW; e += WAVE) {
-    if (env0 + e >= a.B) continue;
-    for (int i = nb - 1; i >= 0; --i) {  // resolutions in reverse order
-      const int ro = L.rec + REC_W * i;
-      if (t.w(ro, e) == 0u) continue;
-      const int j = (int)t.w(L.ch + i, e);
-      const int cid = (int)((t.w(L.m + i * nb + j, e) >> 18) & 511u);
-      const int co = L.con + 4 * cid, oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
-      const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), t.f(ro + 1, e), t.f(ro + 2, e), t.f(oi + 4, e), t.f(ro + 3, e)};
-      const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), t.f(ro + 4, e), t.f(ro + 5, e), t.f(oj + 4, e), t.f(ro + 6, e)};
-      const int ai = L.adj + 6 * i, aj = L.adj + 6 * j;
-      Dyn gi = Dyn{t.f(ai, e), t.f(ai + 1, e), t.f(ai + 2, e), t.f(ai + 3, e), t.f(ai + 4, e), t.f(ai + 5, e)};
-      Dyn gj = Dyn{t.f(aj, e), t.f(aj + 1, e), t.f(aj + 2, e), t.f(aj + 3, e), t.f(aj + 4, e), t.f(aj + 5, e)};
-      v2 gpen = v2{0.0f, 0.0f}, gcp = v2{0.0f, 0.0f};
-      resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
-                  v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp,
-                  baum_of(sc));
-      t.f(ai, e) = gi.px;
-      t.f(ai + 1, e) = gi.py;
-      t.f(ai + 2, e) = gi.vx;
-      t.f(ai + 3, e) = gi.vy;
-      t.f(ai + 4, e) = gi.a;
-      t.f(ai + 5, e) = gi.w;
-      t.f(aj, e) = gj.px;
-      t.f(aj + 1, e) = gj.py;
-      t.f(aj + 2, e) = gj.vx;
-      t.f(aj + 3, e) = gj.vy;
-      t.f(aj + 4, e) = gj.a;
-      t.f(aj + 5, e) = gj.w;
-      t.f(ro + 1, e) = gpen.x;  // (the recorded velocities are read above, for this resolution only)
-      t.f(ro + 2, e) = gpen.y;
-      t.f(ro + 3, e) = gcp.x;
-      t.f(ro + 4, e) = gcp.y;
-    }
-  }
-}
-template <int EW>
-CX_DEV void ph_G2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
-  using namespace cx;
-  const SceneHdr& sc = c.sh;
-  const int nb = c.nb;
-  const Lay& L = c.L;
-  for (int w = lane; w < nb * EW; w += WAVE) {
-    const int e = w % EW, i = w / EW;
-    if (env0 + e >= a.B) continue;
-    const int ro = L.rec + REC_W * i;
-    if (t.w(ro, e) == 0u) continue;
-    const int j = (int)t.w(L.ch + i, e);
-    const int cid = (int)((t.w(L.m + i * nb + j, e) >> 18) & 511u);
-    // the contact: fn(world(part pa), world(part pb)); world = local + body position
-    const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
-    const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
-    const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
-    Shape SA, SB;
-    SA.kind = ka;
-    SB.kind = kb;
-    SA.n = SB.n = 0;
-    for (int k = 0; k < 2 * MAXV; ++k) SA.w[k] = SB.w[k] = 0.0f;
-    for (int k = 0; k < 4; ++k) {
-      SA.w[k] = t.f(wa + k, e);
-      SB.w[k] = t.f(wb + k, e);
-    }
-    float ga[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    contact_vjp(fn, SA, SB, v2{t.f(ro + 1, e), t.f(ro + 2, e)}, v2{t.f(ro + 3, e), t.f(ro + 4, e)}, ga, gb);
-    // the position cotangents of the parts' bodies (circle: (r, cx, cy); AABB: lo, up)
-    t.f(ro + 1, e) = ka == KIND_CIRCLE ? ga[1] : ga[0] + ga[2];
-    t.f(ro + 2, e) = ka == KIND_CIRCLE ? ga[2] : ga[1] + ga[3];
-    t.f(ro + 3, e) = kb == KIND_CIRCLE ? gb[1] : gb[0] + gb[2];
-    t.f(ro + 4, e) = kb == KIND_CIRCLE ? gb[2] : gb[1] + gb[3];
-  }
-}
-template <int EW>
-CX_DEV void ph_G3(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   const SceneHdr& sc = c.sh;
   const int nb = c.nb;
   const Lay& L = c.L;
@@ -2988,17 +2901,63 @@ CX_DEV void ph_G3(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, 
     const int g = env0 + e;
     if (g >= a.B) continue;
     if (a.stages & COTIX_STAGE_COLLIDER) {
-      for (int i = nb - 1; i >= 0; --i) {  // the contact terms, in reverse resolution order
+      for (int i = nb - 1; i >= 0; --i) {  // resolutions in reverse order
         const int ro = L.rec + REC_W * i;
         if (t.w(ro, e) == 0u) continue;
         const int j = (int)t.w(L.ch + i, e);
         const int cid = (int)((t.w(L.m + i * nb + j, e) >> 18) & 511u);
-        const int qa = L.adj + 6 * t.ti(sc.o_pbody + t.ti(sc.o_cpa + cid));
-        const int qb = L.adj + 6 * t.ti(sc.o_pbody + t.ti(sc.o_cpb + cid));
-        t.f(qa, e) = t.f(qa, e) + t.f(ro + 1, e);
-        t.f(qa + 1, e) = t.f(qa + 1, e) + t.f(ro + 2, e);
-        t.f(qb, e) = t.f(qb, e) + t.f(ro + 3, e);
-        t.f(qb + 1, e) = t.f(qb + 1, e) + t.f(ro + 4, e);
+        const int co = L.con + 4 * cid, oi = L.dyn + 6 * i, oj = L.dyn + 6 * j;
+        const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), t.f(ro + 1, e), t.f(ro + 2, e), t.f(oi + 4, e), t.f(ro + 3, e)};
+        const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), t.f(ro + 4, e), t.f(ro + 5, e), t.f(oj + 4, e), t.f(ro + 6, e)};
+        const int ai = L.adj + 6 * i, aj = L.adj + 6 * j;
+        Dyn gi = Dyn{t.f(ai, e), t.f(ai + 1, e), t.f(ai + 2, e), t.f(ai + 3, e), t.f(ai + 4, e), t.f(ai + 5, e)};
+        Dyn gj = Dyn{t.f(aj, e), t.f(aj + 1, e), t.f(aj + 2, e), t.f(aj + 3, e), t.f(aj + 4, e), t.f(aj + 5, e)};
+        v2 gpen = v2{0.0f, 0.0f}, gcp = v2{0.0f, 0.0f};
+        resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
+                    v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp,
+                    baum_of(sc));
+        // the contact: fn(world(part pa), world(part pb)); world = local + body position
+        const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
+        const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
+        const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
+        Shape SA, SB;
+        SA.kind = ka;
+        SB.kind = kb;
+        SA.n = SB.n = 0;
+        for (int k = 0; k < 2 * MAXV; ++k) SA.w[k] = SB.w[k] = 0.0f;
+        for (int k = 0; k < 4; ++k) {
+          SA.w[k] = t.f(wa + k, e);
+          SB.w[k] = t.f(wb + k, e);
+        }
+        float ga[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        contact_vjp(fn, SA, SB, gpen, gcp, ga, gb);
+        t.f(ai, e) = gi.px;
+        t.f(ai + 1, e) = gi.py;
+        t.f(ai + 2, e) = gi.vx;
+        t.f(ai + 3, e) = gi.vy;
+        t.f(ai + 4, e) = gi.a;
+        t.f(ai + 5, e) = gi.w;
+        t.f(aj, e) = gj.px;
+        t.f(aj + 1, e) = gj.py;
+        t.f(aj + 2, e) = gj.vx;
+        t.f(aj + 3, e) = gj.vy;
+        t.f(aj + 4, e) = gj.a;
+        t.f(aj + 5, e) = gj.w;
+        const int qa = L.adj + 6 * t.ti(sc.o_pbody + pa), qb = L.adj + 6 * t.ti(sc.o_pbody + pb);
+        if (ka == KIND_CIRCLE) {
+          t.f(qa, e) = t.f(qa, e) + ga[1];
+          t.f(qa + 1, e) = t.f(qa + 1, e) + ga[2];
+        } else {
+          t.f(qa, e) = t.f(qa, e) + (ga[0] + ga[2]);
+          t.f(qa + 1, e) = t.f(qa + 1, e) + (ga[1] + ga[3]);
+        }
+        if (kb == KIND_CIRCLE) {
+          t.f(qb, e) = t.f(qb, e) + gb[1];
+          t.f(qb + 1, e) = t.f(qb + 1, e) + gb[2];
+        } else {
+          t.f(qb, e) = t.f(qb, e) + (gb[0] + gb[2]);
+          t.f(qb + 1, e) = t.f(qb + 1, e) + (gb[1] + gb[3]);
+        }
       }
     }
     if (a.action != nullptr && a.grad_action != nullptr) {  // v[action_body] += action[step]
@@ -3225,11 +3184,7 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
     run(PH_A, [&](int l) { ph_A<EW, false>(a, c, t, env0, l, step); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0, c.L.sk0);
     run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
-    if (a.stages & COTIX_STAGE_COLLIDER) {
-      run(PH_G, [&](int l) { ph_G1<EW>(a, c, t, env0, l); });
-      run(PH_G, [&](int l) { ph_G2<EW>(a, c, t, env0, l); });
-    }
-    run(PH_G, [&](int l) { ph_G3<EW>(a, c, t, env0, l, step); });
+    run(PH_G, [&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
   }
   run(PH_ADJ, [&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });
 }

@@ -2152,6 +2152,37 @@ CX_DEV MItem m_item(const Ctx& c, Tile<EW> t, int id) {
   }
   return it;
 }
+// an owner's launch-constant words, in registers for the whole launch
+// (mc_fetch once, before the step loop): both owner items and the first two
+// words of their cells' contact masks (every reference scene: nmw <= 2)
+struct MConst {
+  MItem it[2];
+  uint32_t cm[2][2] = {{0u, 0u}, {0u, 0u}};
+};
+template <int EW>
+CX_DEV void mc_fetch(const Ctx& c, Tile<EW> t, int lane, MConst& m) {
+  const SceneHdr& sc = c.sh;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int id = lane + s * WAVE;
+    if (s == 1 && c.nl * EW <= WAVE) continue;  // uniform
+    m.it[s] = m_item<EW>(c, t, id);
+    if (id < c.nl * EW)
+      for (int q = 0; q < 2 && q < sc.nmw; ++q) m.cm[s][q] = t.tb[sc.o_cmask + (id / EW) * sc.nmw + q];
+  }
+}
+// the item's activity from the held mask words (nmw <= 2) or the tables
+template <int EW>
+CX_DEV bool m0_active_c(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int id, const uint32_t* cm) {
+  const SceneHdr& sc = c.sh;
+  if (sc.nmw > 2) return m0_active<EW>(a, c, t, env0, id);
+  if (id >= c.nl * EW) return false;
+  const int e = id % EW;
+  if (env0 + e >= a.B) return false;
+  bool any = false;
+  for (int q = 0; q < 2 && q < sc.nmw; ++q) any |= (cm[q] & t.w(c.L.vm + q, e)) != 0u;
+  return any;
+}
 // an owner's item after a round's pass ballot pm: the cell word from the
 // winning drawer (wcd, permuted), or the scan advances; returns "still pending"
 template <int EW>
@@ -2165,15 +2196,11 @@ CX_DEV bool m_settle(Tile<EW> t, MItem& it, bool drew, uint64_t bits, uint32_t w
   return it.cb + it.pos < it.ce;
 }
 template <int EW>
-CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso) {
+CX_DEV void ph_M_fused(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso, const MConst& mc) {
   const bool two = c.nl * EW > WAVE;  // uniform (a constant in the specialized kernels)
-  MItem it0 = m_item<EW>(c, t, lane), it1;
-  const bool f0 = m0_active<EW>(a, c, t, env0, lane);
-  bool f1 = false;
-  if (two) {
-    it1 = m_item<EW>(c, t, lane + WAVE);
-    f1 = m0_active<EW>(a, c, t, env0, lane + WAVE);
-  }
+  MItem it0 = mc.it[0], it1 = mc.it[1];
+  const bool f0 = m0_active_c<EW>(a, c, t, env0, lane, mc.cm[0]);
+  const bool f1 = two && m0_active_c<EW>(a, c, t, env0, lane + WAVE, mc.cm[1]);
   uint64_t pend0 = ballot(f0), pend1 = two ? ballot(f1) : 0ull;
 #ifdef COTIX_STATS
   {
@@ -3000,7 +3027,8 @@ enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH
 // L.sk0 where phase A splits the keys (backward re-play)
 // AB: phases A, T and B ran as one (ab_fetch / ph_A / ab_contacts, analytic forward programs)
 template <int EW, int FNSET, bool PRE, class R, bool AB = false>
-CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso) {
+CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso,
+                            const MConst& mc) {
   if (!AB && !CXK_SKIP(a, 1)) {
     run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
     if (FNSET != FNS_ANALYTIC && c.sh.nvt > 0) {
@@ -3056,7 +3084,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     }
   }
   if (!CXK_SKIP(a, 4) && c.nl > 0 && c.nl * EW <= 2 * WAVE) {
-    run(PH_C1, [&](int l) { ph_M_fused<EW>(a, c, t, env0, l, kso); });
+    run(PH_C1, [&](int l) { ph_M_fused<EW>(a, c, t, env0, l, kso, mc); });
   } else if (!CXK_SKIP(a, 4) && c.nl > 0) {
     for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {
       run(PH_C0, [&](int l) { ph_C0<EW>(a, c, t, env0, l, ch); });
@@ -3104,6 +3132,9 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
                       a.n_steps >= COTIX_BCONST_MIN_STEPS;
   BConst bc;
   if (bconst) run(PH_B, [&](int l) { bc_fetch<EW>(c, t, l, bc); });
+  MConst mc;  // the fused scan's launch-constant owner words
+  if ((a.stages & COTIX_STAGE_COLLIDER) && c.nl > 0 && c.nl * EW <= 2 * WAVE)
+    run(PH_C1, [&](int l) { mc_fetch<EW>(c, t, l, mc); });
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
@@ -3127,7 +3158,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
       if (a.stages & COTIX_STAGE_COLLIDER) {
         run(PH_B, [&](int l) { ph_B_const<EW>(a, c, t, env0, l, bc); });
-        collider_phases<EW, FNSET, true, R, true>(a, c, t, env0, run, slot, kso);
+        collider_phases<EW, FNSET, true, R, true>(a, c, t, env0, run, slot, kso, mc);
       }
     } else if (FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE) {
       // stage 1 reads the pre-Euler state: every read is issued before phase
@@ -3137,10 +3168,10 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
           [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); },
           [&](int l, const ABRegs& r) { ab_contacts<EW>(a, c, t, env0, l, r); });
       if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true, R, FNSET == FNS_ANALYTIC>(
-          a, c, t, env0, run, slot, kso);
+          a, c, t, env0, run, slot, kso, mc);
     } else {
       run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
-      if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso);
+      if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso, mc);
     }
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
@@ -3176,13 +3207,16 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
   });
   RestoreRegs rr;
   if (a.n_steps > 0) run(PH_RESTORE, [&](int l) { restore_fetch<EW>(a, c, env0, l, a.n_steps - 1, rr); });
+  MConst mc;  // the fused scan's launch-constant owner words
+  if ((a.stages & COTIX_STAGE_COLLIDER) && c.nl > 0 && c.nl * EW <= 2 * WAVE)
+    run(PH_C1, [&](int l) { mc_fetch<EW>(c, t, l, mc); });
   for (int step = a.n_steps - 1; step >= 0; --step) {
     run(PH_RESTORE, [&](int l) {
       restore_apply<EW>(c, t, l, rr);
       if (step > 0) restore_fetch<EW>(a, c, env0, l, step - 1, rr);  // the next (earlier) step, in flight
     });
     run(PH_A, [&](int l) { ph_A<EW, false>(a, c, t, env0, l, step); });
-    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0, c.L.sk0);
+    if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0, c.L.sk0, mc);
     run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
     run(PH_G, [&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
   }

@@ -6,6 +6,7 @@ set -o pipefail
 export TMPDIR=/tmp
 TAG=${TAG:-round}
 O=gpurun_out/$TAG; mkdir -p $O
+if [ "${HEAD:-1}" = 1 ]; then  # HEAD=0: the profiles only (a second call)
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
@@ -13,11 +14,15 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 rc=$?; echo "smoke rc=$rc"; [ $rc -eq 0 ] || { tail -20 $O/smoke.log; exit $rc; }
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc"; cut -c1-200 $O/bench.json; [ $rc -eq 0 ] || { tail $O/bench.err; exit $rc; }
+fi
 # workload key : bench arguments (lunar_contact: the landers on the terrain,
 # driver steps 2560-3200, the stretch of the bench line's lunar_contact figure)
-for wl in "robocup:--scenario robocup --warmup 2" "lunar:--scenario lunar --warmup 2" \
-          "lunar_contact:--scenario lunar --warmup 40" "box:--scenario box --warmup 2" \
-          "grad:--mode grad --scenario robocup --warmup 1" "grad_box:--mode grad --scenario box --warmup 1"; do
+ALL=("robocup:--scenario robocup --warmup 2" "lunar:--scenario lunar --warmup 2" \
+     "lunar_contact:--scenario lunar --warmup 40" "box:--scenario box --warmup 2" \
+     "grad:--mode grad --scenario robocup --warmup 1" "grad_box:--mode grad --scenario box --warmup 1")
+for wl in "${ALL[@]}"; do
+  sc=${wl%%:*}
+  [ -n "$WLS" ] && [[ " $WLS " != *" $sc "* ]] && continue  # WLS: a subset of the workloads
   sc=${wl%%:*}; args=${wl#*:}
   P=$O/prof_$sc; mkdir -p $P
   B="python bench.py $args --steps 10 --cpu-baseline off --extras off"
@@ -30,4 +35,6 @@ for wl in "robocup:--scenario robocup --warmup 2" "lunar:--scenario lunar --warm
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT -d $P/pmc_stall -o run --output-format csv -- $B > /dev/null 2> $P/pmc4.err || { tail $P/pmc4.err; exit 6; }
   echo "profile $sc ok"
 done
-timeout -k 10 200 python tools/phase_prof.py > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --scenario lunar > $O/phase_lunar.json && echo "phase ok"
+if [ "${PHASES:-1}" = 1 ]; then
+timeout -k 10 200 python tools/phase_prof.py > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --scenario lunar > $O/phase_lunar.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario box --launches 3 > $O/phase_grad_box.json && echo "phase ok"
+fi

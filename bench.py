@@ -25,7 +25,9 @@ The JSON line also carries, measured in the same process after the headline
   lunar           BASELINE config 2 (LunarLander, 4096 envs, GJK/EPA) while the
                   landers fall; lunar_contact: settled on the terrain
   grad            BASELINE config 5 (64-step differentiable rollout, fwd + bwd);
-                  grad_box: the same on the box world (finite gradients)
+                  grad_box: the same on the box world (finite gradients);
+                  grad_lunar: LunarLander settled on its terrain (gradients
+                  through GJK/EPA polygon contacts and the joints)
   eval            AbstractEnvironment.eval with a device judge and control,
                   4 NFEs x 16 env-steps in one cotix_eval launch
   config1         BASELINE config 1 (one LunarLander env, 10,000 steps): GPU
@@ -351,12 +353,15 @@ def sub_step(pa, dev, name, B, substeps, steps, warmup, key=None):
 
 def sub_grad(pa, dev, B, T, steps, warmup, scenario="robocup"):
     r = run_grad(pa, dev, B, T, steps, warmup, rank=0, world_size=1, scenario=scenario)
-    out = {"workload": ("BoxWorld %d envs, %d-step differentiable rollout, fwd + bwd (config 5 on a finite scene)"
-                        if scenario == "box" else
-                        "RoboCup %d envs, %d-step differentiable rollout, fwd + bwd (BASELINE config 5)") % (B, T),
+    out = {"workload": {"box": "BoxWorld %d envs, %d-step differentiable rollout, fwd + bwd (config 5 on a finite "
+                                "scene)",
+                        "lunar": "LunarLander %d envs settled on the terrain (after 2560 steps), %d-step "
+                                 "differentiable rollout, fwd + bwd: gradients through GJK/EPA polygon contacts and "
+                                 "the joints (lander x w.r.t. the lander's per-step dv)"}.get(
+                scenario, "RoboCup %d envs, %d-step differentiable rollout, fwd + bwd (BASELINE config 5)") % (B, T),
            "value": r["value"], "unit": "env-steps/s with d(return)/d(action)", "fwd_ms": r["fwd_ms"],
            "bwd_ms": r["bwd_ms"], "finite_grad_env_fraction": r["finite"]}
-    v = grad_valu("grad_box" if scenario == "box" else "grad", B, T, r["fwd_ms"], r["bwd_ms"])
+    v = grad_valu({"box": "grad_box", "lunar": "grad_lunar"}.get(scenario, "grad"), B, T, r["fwd_ms"], r["bwd_ms"])
     if v is not None:
         out["valu"] = v
     return out
@@ -564,6 +569,7 @@ def main():
         out["lunar_contact"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 40, key="lunar_contact")
         out["grad"] = sub_grad(pa, dev, B, 64, 5, 1)
         out["grad_box"] = sub_grad(pa, dev, B, 64, 5, 1, scenario="box")
+        out["grad_lunar"] = sub_grad(pa, dev, B, 64, 5, 1, scenario="lunar")
         out["eval"] = sub_eval(pa, dev, B)
         out["config1"] = sub_config1(pa, dev)
     # the CPU baseline last: its OpenMP threads must not compete with the
@@ -586,17 +592,26 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario
     scenario "box": the same on the box world (finite dynamics), whose
     gradients are finite -- RoboCup's degenerate reference scene makes most
     of its envs' gradients NaN."""
+    stages, ab = pa._ffi.STAGES_ROBOCUP, None
     if scenario == "box":
         scen = pa.BoxWorld(batch=B, device=dev, env_offset=rank * B, total_envs=world_size * B)
+    elif scenario == "lunar":
+        # LunarLander settled on its terrain (driver steps 2560+, the lunar_contact
+        # regime): GJK/EPA polygon contacts and the joints every step
+        scen = pa.LunarLander(batch=B, device=dev)
+        stages, ab = pa._ffi.STAGES_LUNAR | pa._ffi.STAGE_BROADPHASE, 0
+        for _ in range(40):
+            scen.world.step(64, 1e-2, stages)
     else:
         scen = pa.RoboCupEnv(batch=B, device=dev, perturb=True, env_offset=rank * B, total_envs=world_size * B)
     world = scen.world
     nb = len(world.bodies)
+    ab = nb - 1 if ab is None else ab
     variant = world.scene.variant()
     dyn0, keys0 = world.dyn.clone(), world.keys.clone()
     gen = torch.Generator(device="cpu").manual_seed(1234 + rank)
     actions = (torch.randn(T, B, 2, generator=gen) * 0.1).to(dev)  # SURVEY 8(d): ball dv ~ N(0, 0.1^2)
-    w = pa.rollout.ball_x_weights(nb, nb - 1)  # RoboCup: the ball (body 4); box world: the last ball
+    w = pa.rollout.ball_x_weights(nb, ab)  # RoboCup: the ball (body 4); box world: the last ball; LL: the lander
     evf = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     evb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     state = {}
@@ -607,7 +622,7 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario
         world.err.zero_()
         if i is not None:
             evf[i][0].record()
-        ret, saved = pa.rollout_forward(world, actions, nb - 1, w)
+        ret, saved = pa.rollout_forward(world, actions, ab, w, stages=stages)
         if i is not None:
             evf[i][1].record()
             evb[i][0].record()

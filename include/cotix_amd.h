@@ -293,7 +293,15 @@ int cotix_eval(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, co
  * semantics through the reference's lax.cond branches, balanced ties for
  * max/min/clip).  grad_action device f32 [n_steps][B][2] (nullable),
  * grad_dyn0 device f32 [n_bodies][6][B] (nullable) = d ret / d initial state.
- * Scenes with polygon parts (GJK/EPA) and the LunarLander stage are rejected. */
+ * Polygon contacts (polygon_vs_polygon, aabb_vs_polygon) are differentiated
+ * through EPA's final edge (its supports -- polygon vertices, AABB corners --
+ * are argmax choices, i.e. constants) and the included contact_from_edges
+ * terms, the polygons' world vertices through the body angle
+ * (cotix/_collisions.py:115-273, cotix/_contacts.py:205-315); the LunarLander
+ * joint stage through its four impulse pairs (cotix/_lunar_lander.py:176-212).
+ * Rejected: scenes with circle x polygon contacts (EPA's circle supports
+ * chain through every iteration) and the joint stage on a polygon-free scene.
+ * The re-play runs without COTIX_STAGE_BROADPHASE (an exact filter). */
 int cotix_rollout(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
                   int B, int n_steps, float dt, int stages, const float* action, int action_body,
                   const float* ret_weights, float* ret, float* saved_dyn, uint32_t* saved_keys,

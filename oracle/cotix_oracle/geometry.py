@@ -224,7 +224,7 @@ def _sort_key(v):
     return (0, float(v) + 0.0)
 
 
-def order_clockwise(verts):
+def order_clockwise_idx(verts):
     """cotix/_geometry_utils.py:60-67: subtract the (sequentially summed) mean,
     atan2, stable argsort."""
     n = len(verts)
@@ -236,8 +236,11 @@ def order_clockwise(verts):
     mx = sx / F(n)
     my = sy / F(n)
     ang = [atan2_32(v[1] - my, v[0] - mx) for v in verts]
-    idx = sorted(range(n), key=lambda k: _sort_key(ang[k]))  # Python sort is stable
-    return [verts[k] for k in idx]
+    return sorted(range(n), key=lambda k: _sort_key(ang[k]))  # Python sort is stable
+
+
+def order_clockwise(verts):
+    return [verts[k] for k in order_clockwise_idx(verts)]
 
 
 def rotate(vec, angle):
@@ -473,7 +476,13 @@ def _closest_edge(edges):  # :171-175
 
 
 def epa(a, b, simplex, iters):
-    """_get_closest_minkowski_diff (cotix/_collisions.py:115-273).  The scan of
+    """_get_closest_minkowski_diff (cotix/_collisions.py:115-273)."""
+    best = epa_best_edge(a, b, simplex, iters)
+    return _closest_point_on_edge_to_point(best[0], best[1], (ZERO, ZERO))
+
+
+def epa_best_edge(a, b, simplex, iters):
+    """EPA's final closest polytope edge (two Minkowski points).  The scan of
     ``iters`` conditional bodies stops at the first false condition: the state
     is a fixed point afterwards (value-identical early exit)."""
     z = (ZERO, ZERO)
@@ -506,7 +515,7 @@ def epa(a, b, simplex, iters):
         best, bei = _closest_edge(edges)
         i += 1
     best, _ = _closest_edge(edges)
-    return _closest_point_on_edge_to_point(best[0], best[1], (ZERO, ZERO))
+    return best
 
 
 # ----------------------------------------------------------------------------

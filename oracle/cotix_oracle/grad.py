@@ -23,6 +23,7 @@ import warnings
 import numpy as np
 import torch
 
+from . import geometry as G
 from . import params as _params
 from . import physics as P
 
@@ -201,18 +202,186 @@ def resolve(b1, b2, pen, cp):
     return True
 
 
-def _world_part(part, p):
+class _SinCos(torch.autograd.Function):
+    """The build's f32 (sin, cos) (geometry.sincos32); JAX's JVP rules
+    d sin = cos, d cos = -sin, on those values."""
+
+    @staticmethod
+    def forward(ctx, x):
+        s, c = G.sincos32(np.float32(x.item()))
+        st, ct = torch.tensor(float(s), dtype=F32), torch.tensor(float(c), dtype=F32)
+        ctx.save_for_backward(st, ct)
+        return st, ct
+
+    @staticmethod
+    def backward(ctx, gs, gc):
+        s, c = ctx.saved_tensors
+        return gs * c - gc * s
+
+
+def _rot(v, s, c):  # rotate (cotix/_geometry_utils.py:81-88): [[c,-s],[s,c]] @ v
+    return (c * v[0] + (-s) * v[1], s * v[0] + c * v[1])
+
+
+class _Poly:
+    """A world polygon: torch vertices in Polygon.__init__'s clockwise order
+    (the permutation is a constant), plus the oracle shape of their values."""
+
+    def __init__(self, verts):
+        self.v = verts
+        self.np = G.Polygon([(np.float32(x.item()), np.float32(y.item())) for x, y in verts], sort=False)
+
+    def verts(self):
+        return self.v
+
+    def edges(self):  # Polygon.edges: (v_k, v_{k-1})
+        return [(self.v[k], self.v[k - 1]) for k in range(len(self.v))]
+
+
+class _Box:
+    """A world AABB (lower, upper) with AABB.vertices / edges' corner order."""
+
+    def __init__(self, lo, up):
+        self.lo, self.up = lo, up
+        self.np = G.AABB((np.float32(lo[0].item()), np.float32(lo[1].item())),
+                         (np.float32(up[0].item()), np.float32(up[1].item())))
+
+    def verts(self):
+        u, lo = self.up, self.lo
+        return [u, (u[0], lo[1]), lo, (lo[0], u[1])]
+
+    def edges(self):
+        vs = self.verts()
+        return [(vs[k], vs[(k + 1) % 4]) for k in range(4)]
+
+
+def _world_part(part, p, ang):
     if part.kind == "Circle":
         return (_t(part.radius), (_t(part.position[0]) + p[0], _t(part.position[1]) + p[1]))
     if part.kind == "AABB":
-        return ((_t(part.lower[0]) + p[0], _t(part.lower[1]) + p[1]),
-                (_t(part.upper[0]) + p[0], _t(part.upper[1]) + p[1]))
-    raise NotImplementedError("polygon contacts are not differentiated")
+        return _Box((_t(part.lower[0]) + p[0], _t(part.lower[1]) + p[1]),
+                    (_t(part.upper[0]) + p[0], _t(part.upper[1]) + p[1]))
+    # Polygon.transform: HomogenuousTransformer.forward_vector (t2 == 1), then re-sorted
+    s, c = _SinCos.apply(ang)
+    ws = [((c * _t(x0) + (-s) * _t(x1)) + p[0] * 1.0, (s * _t(x0) + c * _t(x1)) + p[1] * 1.0)
+          for x0, x1 in part.vertices_]
+    idx = G.order_clockwise_idx([(np.float32(x.item()), np.float32(y.item())) for x, y in ws])
+    return _Poly([ws[k] for k in idx])
 
 
-def step_torch(S, a, bodies, trace, dt, action_body, gravity=False):
+# ---- GJK / EPA contacts (cotix/_collisions.py:115-273, cotix/_contacts.py:205-315) ----
+def _closest_to_origin(a, b):  # _closest_point_on_edge_to_point(a, b, 0) :156-166
+    z = _t(0.0)
+    d = _sub(a, b)
+    length = d[0] * d[0] + d[1] * d[1]
+    if float(length) == 0.0:
+        return (z - a[0], z - a[1])
+    pb = (z - b[0], z - b[1])
+    t = _clip(_dot(pb, d) / length, _t(0.0), _t(1.0))
+    proj = (b[0] + d[0] * t, b[1] + d[1] * t)
+    return (z - proj[0], z - proj[1])
+
+
+def _minkowski_point(A, B, pt):
+    """The Minkowski point a_i - b_j equal to `pt` (EPA's supports are vertices
+    of a polygon or corners of an AABB, chosen by argmax: constants).  Rule,
+    shared with the kernel's VJP (cotix_grad.h): the first (i, j), A-major,
+    whose difference equals pt."""
+    va, vb = A.np.vertices(), B.np.vertices()
+    for i, a in enumerate(va):
+        for j, b in enumerate(vb):
+            if a[0] - b[0] == pt[0] and a[1] - b[1] == pt[1]:
+                ta, tb = A.verts()[i], B.verts()[j]
+                return (ta[0] - tb[0], ta[1] - tb[1])
+    raise AssertionError("EPA edge point is not a Minkowski vertex pair")
+
+
+def _edge_vs_edge(ea, eb):  # :206-225, the intersecting branch
+    p, r = ea[0], _sub(ea[1], ea[0])
+    q, s = eb[0], _sub(eb[1], eb[0])
+    c = r[0] * s[1] - s[0] * r[1]
+    qp = _sub(q, p)
+    t = (qp[0] * s[1] - s[0] * qp[1]) / c
+    return (p[0] + r[0] * t, p[1] + r[1] * t)
+
+
+def _contact_from_edges(A, B):
+    """:205-267 with the inclusion of each term (vertex containment, edge
+    intersection) decided by the oracle on the forward values: constants."""
+    acc = (_t(0.0), _t(0.0))
+    n = np.float32(0.0)
+    for v, vn in zip(A.verts(), A.np.vertices()):
+        if B.np.contains(vn):
+            acc, n = _add(acc, v), n + np.float32(1.0)
+    for v, vn in zip(B.verts(), B.np.vertices()):
+        if A.np.contains(vn):
+            acc, n = _add(acc, v), n + np.float32(1.0)
+    ea_np, eb_np = A.np.edges(), B.np.edges()
+    ea_t, eb_t = A.edges(), B.edges()
+    for jb in range(len(eb_np)):
+        for ia in range(len(ea_np)):
+            if not G.vnan(G._edge_vs_edge(ea_np[ia], eb_np[jb])):
+                acc, n = _add(acc, _edge_vs_edge(ea_t[ia], eb_t[jb])), n + np.float32(1.0)
+    assert n > 0, "contact without a contact point"
+    return (acc[0] / float(n), acc[1] / float(n))
+
+
+def _convex_contact(fname, A, B, d0):
+    """polygon_vs_polygon :294-315 / aabb_vs_polygon :270-291, contact branch."""
+    nb_ = len(B.np.vertices())
+    na_ = 4 if isinstance(A, _Box) else len(A.np.vertices())
+    cap = _params.current().epa_max_iters
+    iters = min(cap, (4 if isinstance(A, _Box) else na_) + nb_ + 1)
+    hit, simplex = G.check_for_collision_convex(A.np, B.np, d0)
+    assert hit, "not a contact"
+    best = G.epa_best_edge(A.np, B.np, simplex, iters)
+    pen = _closest_to_origin(_minkowski_point(A, B, best[0]), _minkowski_point(A, B, best[1]))
+    return pen, _contact_from_edges(A, B)
+
+
+# ---- LunarLander joints (cotix/_lunar_lander.py:145-218) ----
+def _lunar_joints(st):
+    f05 = np.float32(0.05)
+    lander, rleg, lleg = st[0], st[1], st[2]
+    sl, cl = _SinCos.apply(lander.ang)
+    sr, cr = _SinCos.apply(rleg.ang)
+    sll, cll = _SinCos.apply(lleg.ang)
+
+    def k(x, y):
+        return (_t(np.float32(x) * f05), _t(np.float32(y) * f05))
+
+    llj1 = _add(_rot(k(P.LEG_AWAY, -P.LEG_DOWN), sl, cl), lander.p)
+    llj2 = _add(_rot(k(P.LEG_AWAY, -P.LEG_DOWN + 8), sl, cl), lander.p)
+    lj1 = lleg.p
+    lj2 = _add(lleg.p, _rot((_t(0.0), _t(0.4)), sll, cll))
+    lrj1 = _add(_rot(k(-P.LEG_AWAY, -P.LEG_DOWN), sl, cl), lander.p)
+    lrj2 = _add(_rot(k(-P.LEG_AWAY, -P.LEG_DOWN + 8), sl, cl), lander.p)
+    rj1 = rleg.p
+    rj2 = _add(rleg.p, _rot((_t(0.0), _t(0.4)), sr, cr))
+
+    def fixed(b1, c1, b2, c2):
+        dp = _sub(c1, c2)
+        dv = _sub(b1.vel_at(c1), b2.vel_at(c2))
+        kk = _norm(dv) + float(np.float32(0.1))
+        imp = (dp[0] * 1.0 + (dv[0] * kk) * float(f05), dp[1] * 1.0 + (dv[1] * kk) * float(f05))
+        _apply(b1, (-imp[0], -imp[1]), c1)
+        _apply(b2, imp, c2)
+
+    fixed(lander, llj1, lleg, lj1)
+    fixed(lander, llj2, lleg, lj2)
+    fixed(lander, lrj1, rleg, rj1)
+    fixed(lander, lrj2, rleg, rj2)
+    rleg.w = rleg.w * float(np.float32(0.95))
+    lleg.w = lleg.w * float(np.float32(0.95))
+
+
+CONVEX = ("polygon_vs_polygon", "aabb_vs_polygon")
+
+
+def step_torch(S, a, bodies, trace, dt, action_body, gravity=False, d0=None, joints=False):
     """One step's continuous map S_t [nb,6] -> S_{t+1} given the oracle's
-    discrete choices (trace of the same step)."""
+    discrete choices (trace of the same step).  gravity / joints: the
+    LunarLander step (examples/test_viz.py:24-44)."""
     nb = S.shape[0]
     dt = float(np.float32(dt))
     st = []
@@ -229,10 +398,19 @@ def step_torch(S, a, bodies, trace, dt, action_body, gravity=False):
         if j == i:
             continue
         fname, (o1b, o1p), (o2b, o2p) = src[i][j]
-        s1 = _world_part(bodies[o1b].parts[o1p], st[o1b].p)
-        s2 = _world_part(bodies[o2b].parts[o2p], st[o2b].p)
-        pen, cp = CONTACTS[fname](s1, s2)
+        s1 = _world_part(bodies[o1b].parts[o1p], st[o1b].p, st[o1b].ang)
+        s2 = _world_part(bodies[o2b].parts[o2p], st[o2b].p, st[o2b].ang)
+        if fname in CONTACTS:
+            s1 = (s1.lo, s1.up) if isinstance(s1, _Box) else s1
+            s2 = (s2.lo, s2.up) if isinstance(s2, _Box) else s2
+            pen, cp = CONTACTS[fname](s1, s2)
+        elif fname in CONVEX:
+            pen, cp = _convex_contact(fname, s1, s2, d0)
+        else:
+            raise NotImplementedError("%s is not differentiated (circle support chain through EPA)" % fname)
         resolve(st[i], st[j], pen, cp)
+    if joints:
+        _lunar_joints(st)
     rows = [torch.stack([b.p[0], b.p[1], b.v[0], b.v[1], b.ang, b.w]) for b in st]
     return torch.stack(rows)
 
@@ -263,7 +441,8 @@ def rollout_grad(make_bodies, S0, key0, actions, w, action_body, d0, dt=P.DT, st
     for t in range(T - 1, -1, -1):
         S = torch.tensor(states[t], dtype=F32, requires_grad=True)
         a = torch.tensor(actions[t], dtype=F32, requires_grad=True)
-        out = step_torch(S, a, meta, traces[t], dt, action_body, gravity=step is P.lunar_lander_step)
+        ll = step is P.lunar_lander_step
+        out = step_torch(S, a, meta, traces[t], dt, action_body, gravity=ll, d0=d0, joints=ll)
         o = out.detach().numpy()
         same = (o.view(np.uint32) == states[t + 1].view(np.uint32)) | (np.isnan(o) & np.isnan(states[t + 1]))
         assert same.all(), "torch restatement diverged from the oracle at step %d: %s vs %s" % (

@@ -750,8 +750,11 @@ struct EdgeCol {  // edge k, component c at p[(4k + c) * st]
   }
 };
 
+// epa_edge: EPA's final closest polytope edge (two Minkowski points) -- the
+// penetration is its closest point to the origin (epa below); the backward
+// (cotix_grad.h convex_contact_vjp) differentiates through the edge's points
 template <int NE, class ES, class SA, class SB>
-CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters, ES& es) {
+CX_DEV void epa_edge(const SA& a, const SB& b, const v2* simplex, int iters, ES& es, v2* e0, v2* e1) {
   float dist[NE];
   const v2 z = v2{0.0f, 0.0f};
 #pragma unroll
@@ -823,7 +826,14 @@ CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters, ES& es) {
     best0 = es.g0(bei);
     best1 = es.g1(bei);
   }
-  return closest_on_edge_to_origin(best0, best1);
+  *e0 = best0;
+  *e1 = best1;
+}
+template <int NE, class ES, class SA, class SB>
+CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters, ES& es) {
+  v2 e0, e1;
+  epa_edge<NE, ES>(a, b, simplex, iters, es, &e0, &e1);
+  return closest_on_edge_to_origin(e0, e1);
 }
 template <int NE, class SA, class SB>
 CX_DEV v2 epa(const SA& a, const SB& b, const v2* simplex, int iters) {

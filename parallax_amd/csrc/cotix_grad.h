@@ -170,6 +170,208 @@ CX_DEV void contact_vjp(int fn, const Shape& a, const Shape& b, v2 gpen, v2 gcp,
   }
 }
 
+// ---------------------------------------------------------------------------
+// GJK / EPA contacts (polygon_vs_polygon cotix/_contacts.py:294-315,
+// aabb_vs_polygon :270-291), contact branch.  EPA's supports are vertices of a
+// polygon or corners of an AABB chosen by argmax (constants), so the
+// penetration depends on the shapes only through the two Minkowski points of
+// EPA's final edge (_closest_point_on_edge_to_point of that edge,
+// cotix/_collisions.py:156-166,271-273); the contact point is the mean of the
+// included contact_from_edges terms (:205-267, inclusion = the forward's
+// containment / intersection tests, constants).  Cotangents are accumulated
+// per vertex (cvx_vert order: polygon slots, AABB corners).
+// ---------------------------------------------------------------------------
+struct VGrad {
+  float x[MAXV], y[MAXV];
+  CX_MF void zero() {
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) x[k] = y[k] = 0.0f;
+  }
+  CX_MF void add(int k, v2 g) {  // k varies per lane: select chain, no scratch
+#pragma unroll
+    for (int q = 0; q < MAXV; ++q) {
+      x[q] += q == k ? g.x : 0.0f;
+      y[q] += q == k ? g.y : 0.0f;
+    }
+  }
+};
+// closest_on_edge_to_origin(a, b) (cotix_device.h) -> cotangents of a, b
+CX_DEV void closest_vjp(v2 a, v2 b, v2 g, v2* ga, v2* gb) {
+  const v2 d = sub(a, b);
+  const float len = sumsq(d);
+  if (len == 0.0f) {  // 0 - a
+    *ga = sub(*ga, g);
+    return;
+  }
+  const v2 pb = sub(v2{0.0f, 0.0f}, b);
+  const float num = dot(pb, d), t = num / len, tc = clip_(t, 0.0f, 1.0f);
+  const v2 gproj = neg(g);  // r = 0 - proj, proj = b + d * tc
+  v2 gd = scl(gproj, tc);
+  float gt = 0.0f, glo = 0.0f, ghi = 0.0f;
+  vjp_clip(t, 0.0f, 1.0f, dot(gproj, d), &gt, &glo, &ghi);
+  const float gnum = gt / len, glen = -gt * num / (len * len);
+  gd = add(gd, scl(pb, gnum));
+  gd = add(gd, scl(d, 2.0f * glen));
+  const v2 gpb = scl(d, gnum);
+  *ga = add(*ga, gd);
+  *gb = sub(add(*gb, sub(gproj, gpb)), gd);
+}
+// the Minkowski point pt = vert_A(i) - vert_B(j): the first (i, j), A-major,
+// whose difference equals pt (the oracle's rule, oracle/cotix_oracle/grad.py)
+CX_DEV void minkowski_vjp(const Shape& A, const Shape& B, v2 pt, v2 g, VGrad& ga, VGrad& gb) {
+  const int na = cvx_count(A), nb = cvx_count(B);
+  int fi = -1, fj = -1;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j)
+      if (i < na && j < nb && fi < 0) {
+        const v2 d = sub(cvx_vert(A, i), cvx_vert(B, j));
+        if (d.x == pt.x && d.y == pt.y) {
+          fi = i;
+          fj = j;
+        }
+      }
+  if (fi < 0) return;  // (not reached: EPA's points are Minkowski vertex pairs)
+  ga.add(fi, g);
+  gb.add(fj, neg(g));
+}
+// edge_vs_edge (cotix_device.h), intersecting branch: x = p + r t,
+// t = crs(q - p, s) / crs(r, s); cotangent gx -> the four endpoints
+CX_DEV void edge_vs_edge_vjp(v2 pa0, v2 pa1, v2 qb0, v2 qb1, v2 gx, v2* ga0, v2* ga1, v2* gb0, v2* gb1) {
+  const v2 p = pa0, r = sub(pa1, pa0), q = qb0, s = sub(qb1, qb0), w = sub(q, p);
+  const float c = r.x * s.y - s.x * r.y, nn = w.x * s.y - s.x * w.y, t = nn / c;
+  v2 gp = gx, gr = scl(gx, t), gw = v2{0.0f, 0.0f}, gs = v2{0.0f, 0.0f};
+  const float gt = dot(gx, r), gn = gt / c, gc = -gt * nn / (c * c);
+  // crs(u, v) = u.x v.y - v.x u.y: d/du = (v.y, -v.x), d/dv = (-u.y, u.x)
+  gw = add(gw, scl(v2{s.y, -s.x}, gn));
+  gs = add(gs, scl(v2{-w.y, w.x}, gn));
+  gr = add(gr, scl(v2{s.y, -s.x}, gc));
+  gs = add(gs, scl(v2{-r.y, r.x}, gc));
+  const v2 gq = gw;
+  gp = sub(gp, gw);
+  *ga1 = add(*ga1, gr);
+  *ga0 = add(add(*ga0, gp), neg(gr));
+  *gb1 = add(*gb1, gs);
+  *gb0 = add(add(*gb0, gq), neg(gs));
+}
+// vertex k / edge k of a convex shape for a run-time k (select chains on the
+// registers: no scratch copy of the shape); edge k = (v_k, v_prev(k))
+CX_DEV v2 cvx_vert_r(const Shape& s, int k) {
+  if (s.kind == KIND_AABB)
+    return v2{(k == 0 || k == 1) ? s.w[2] : s.w[0], (k == 0 || k == 3) ? s.w[3] : s.w[1]};
+  return vert(s, k);
+}
+CX_DEV int cvx_edge_prev(const Shape& s, int k) {
+  if (s.kind == KIND_AABB) return (k + 1) & 3;
+  return k == 0 ? s.n - 1 : k - 1;
+}
+CX_DEV void contact_from_edges_vjp(const Shape& A, const Shape& B, v2 gcp, VGrad& ga, VGrad& gb) {
+  const int na = cvx_count(A), nb = cvx_count(B);
+  float n = 0.0f;  // the forward's term count
+  for (int k = 0; k < na; ++k) n = shape_contains(B, cvx_vert_r(A, k)) ? n + 1.0f : n;
+  for (int k = 0; k < nb; ++k) n = shape_contains(A, cvx_vert_r(B, k)) ? n + 1.0f : n;
+  for (int jb = 0; jb < nb; ++jb)
+    for (int ia = 0; ia < na; ++ia) {
+      const v2 x = edge_vs_edge(cvx_vert_r(A, ia), cvx_vert_r(A, cvx_edge_prev(A, ia)), cvx_vert_r(B, jb),
+                                cvx_vert_r(B, cvx_edge_prev(B, jb)));
+      n = vnan(x) ? n : n + 1.0f;
+    }
+  if (!(n > 0.0f)) return;
+  const v2 g = divs(gcp, n);  // cp = acc / n
+  for (int k = 0; k < na; ++k)
+    if (shape_contains(B, cvx_vert_r(A, k))) ga.add(k, g);
+  for (int k = 0; k < nb; ++k)
+    if (shape_contains(A, cvx_vert_r(B, k))) gb.add(k, g);
+  for (int jb = 0; jb < nb; ++jb)
+    for (int ia = 0; ia < na; ++ia) {
+      const int pa = cvx_edge_prev(A, ia), pb = cvx_edge_prev(B, jb);
+      const v2 a0 = cvx_vert_r(A, ia), a1 = cvx_vert_r(A, pa), b0 = cvx_vert_r(B, jb), b1 = cvx_vert_r(B, pb);
+      if (vnan(edge_vs_edge(a0, a1, b0, b1))) continue;
+      v2 g0 = v2{0.0f, 0.0f}, g1 = g0, h0 = g0, h1 = g0;
+      edge_vs_edge_vjp(a0, a1, b0, b1, g, &g0, &g1, &h0, &h1);
+      ga.add(ia, g0);
+      ga.add(pa, g1);
+      gb.add(jb, h0);
+      gb.add(pb, h1);
+    }
+}
+// the whole convex contact: re-runs GJK and EPA (the forward's exact code,
+// so the final edge is the forward's) and returns the per-vertex cotangents
+CX_DEV void convex_contact_vjp(const Shape& A, const Shape& B, const NarrowParams& np, v2 gpen, v2 gcp, VGrad& ga,
+                               VGrad& gb) {
+  v2 simplex[3];
+  if (!gjk(A, B, np.d0, simplex, np.gjk_steps)) return;  // (not reached for a resolved contact)
+  const int it0 = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
+  const int iters = it0 < np.epa_cap ? it0 : np.epa_cap;
+  v2 e0, e1;
+  if (iters + 3 <= 14) {
+    EdgeRegs<14> es;
+    epa_edge<14>(A, B, simplex, iters, es, &e0, &e1);
+  } else {
+    EdgeRegs<20> es;
+    epa_edge<20>(A, B, simplex, iters, es, &e0, &e1);
+  }
+  v2 g0 = v2{0.0f, 0.0f}, g1 = v2{0.0f, 0.0f};
+  closest_vjp(e0, e1, gpen, &g0, &g1);
+  minkowski_vjp(A, B, e0, g0, ga, gb);
+  minkowski_vjp(A, B, e1, g1, ga, gb);
+  contact_from_edges_vjp(A, B, gcp, ga, gb);
+}
+
+// ---------------------------------------------------------------------------
+// LunarLander joints (LunarLander.step, cotix/_lunar_lander.py:176-212; the
+// forward is cotix_kernel.h lunar_constraints): four `fixed` impulse pairs,
+// then the legs' angular damping.  In: the pre-joint bodies (lander, right
+// leg, left leg) and the cotangents of the post-joint ones; out: the
+// cotangents of the pre-joint bodies (positions and angles through the
+// anchors, velocities through the impulses).
+// ---------------------------------------------------------------------------
+// d/dangle of rotate(v) = [[c,-s],[s,c]] v (JAX: d sin = cos, d cos = -sin)
+CX_DEV float drot_dot(v2 g, v2 v, float s, float c) {
+  return g.x * (-s * v.x - c * v.y) + g.y * (c * v.x - s * v.y);
+}
+CX_DEV void fixed_vjp(const Dyn& b1, const Params& m1, v2 c1, const Dyn& b2, const Params& m2, v2 c2, Dyn& g1, Dyn& g2,
+                      v2& gc1, v2& gc2) {
+  const float f05 = 0.05f;
+  const v2 r1 = sub(c1, v2{b1.px, b1.py}), r2 = sub(c2, v2{b2.px, b2.py});
+  const v2 dp = sub(c1, c2);
+  const v2 dv = sub(velocity_at(b1, c1), velocity_at(b2, c2));
+  const float nd = nrm(dv), k = nd + 0.1f;
+  const v2 imp = v2{dp.x * 1.0f + (dv.x * k) * f05, dp.y * 1.0f + (dv.y * k) * f05};
+  // apply_impulse(b1, -imp, c1), apply_impulse(b2, imp, c2)
+  v2 gimp = v2{-g1.vx / m1.mass + g2.vx / m2.mass, -g1.vy / m1.mass + g2.vy / m2.mass};
+  const float gt1 = g1.w / m1.inertia, gt2 = g2.w / m2.inertia;
+  v2 gr1 = scl(v2{-imp.y, imp.x}, gt1), gr2 = scl(v2{imp.y, -imp.x}, gt2);  // torque = crs(r, -+imp)
+  gimp = add(gimp, scl(v2{r1.y, -r1.x}, gt1));
+  gimp = add(gimp, scl(v2{-r2.y, r2.x}, gt2));
+  // imp = dp + (dv * k) * 0.05, k = |dv| + 0.1
+  const v2 gdp = gimp;
+  v2 gdv = scl(gimp, k * f05);
+  const float gk = f05 * dot(gimp, dv);
+  gdv = add(gdv, scl(divs(dv, nd), gk));
+  // dv = velocity_at(b1, c1) - velocity_at(b2, c2); velocity_at = v + perp(c - p) w
+  const v2 gu1 = gdv, gu2 = neg(gdv);
+  Dyn o1 = g1, o2 = g2;
+  o1.vx += gu1.x;
+  o1.vy += gu1.y;
+  o1.w += -r1.y * gu1.x + r1.x * gu1.y;
+  gr1 = add(gr1, v2{gu1.y * b1.w, -gu1.x * b1.w});
+  o2.vx += gu2.x;
+  o2.vy += gu2.y;
+  o2.w += -r2.y * gu2.x + r2.x * gu2.y;
+  gr2 = add(gr2, v2{gu2.y * b2.w, -gu2.x * b2.w});
+  // r = c - p; dp = c1 - c2
+  gc1 = add(gc1, add(gr1, gdp));
+  gc2 = add(gc2, sub(gr2, gdp));
+  o1.px -= gr1.x;
+  o1.py -= gr1.y;
+  o2.px -= gr2.x;
+  o2.py -= gr2.y;
+  g1 = o1;
+  g2 = o2;
+}
+
 // resolve_collision_notnan (cotix/_collision_resolution.py:76-146) in the
 // branch that applies the impulses.  In: the pre-resolution bodies, the
 // cotangents g1/g2 of the post-resolution bodies.  Out: g1/g2 become the

@@ -283,11 +283,12 @@ CX_HD Lay layout(int nb, int np, int W, int nc, int nt, int G, int PE) {
   // the premature-out reward, key and err; the premature-out state itself is
   // kept in rst (free in eval: its restarts are taken at entry, reset_mode 2)
   // per world vertex (word offset / 2 of the world parts): the broadphase
-  // guard's edge pseudo-angle (ph_TV4).  It overlays adj and rec, which only
-  // the backward re-play uses, and the backward program is admitted for
-  // analytic (polygon-free) scenes only (cotix_rollout_backward): the
-  // LunarLander tile stays within the LDS
-  // (a scene with more polygon vertices gets words of its own)
+  // guard's edge pseudo-angle (ph_TV4, ph_T; written only with
+  // COTIX_STAGE_BROADPHASE).  It overlays adj and rec, which only the backward
+  // re-play uses, and the backward runs without the broadphase (an exact
+  // filter: the same contacts; cotix_rollout_backward clears the stage bit):
+  // the LunarLander tile stays within the LDS (a scene with more polygon
+  // vertices gets words of its own)
   const bool own = PE > nb * (6 + REC_W);
   L.pedge = own ? L.pbox + 4 * np : L.adj;
   L.jfin = L.pbox + 4 * np + (own ? PE : 0);
@@ -402,12 +403,12 @@ CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, con
 // (without it the GJK/EPA supports are compiled for polygons only)
 enum : int { FNS_ANALYTIC = 1, FNS_CONVEX = 2, FNS_CIRCLE_POLY = 4, FNS_AABB_POLY = 8 };
 // the FNSET instantiation of the step kernel for a scene's function set
-// (launcher and host emulation): mode 2 (backward) and analytic scenes get the
-// analytic program, modes 1 (rollout) and 3 (eval with a judge or control) the
+// (launcher and host emulation): analytic scenes get the analytic program,
+// modes 1 (rollout), 2 (its backward) and 3 (eval with a judge or control) the
 // full one
 CX_HD int launch_fnset(int fs, int mode) {
-  if (mode == 2 || (fs & ~FNS_ANALYTIC) == 0) return FNS_ANALYTIC;
-  if (mode == 1 || mode == 3) return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
+  if ((fs & ~FNS_ANALYTIC) == 0) return FNS_ANALYTIC;
+  if (mode == 1 || mode == 2 || mode == 3) return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
   if ((fs & ~(FNS_ANALYTIC | FNS_CONVEX)) == 0) return FNS_ANALYTIC | FNS_CONVEX;
   if ((fs & FNS_CIRCLE_POLY) == 0) return FNS_ANALYTIC | FNS_CONVEX | FNS_AABB_POLY;
   return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
@@ -592,12 +593,18 @@ CX_DEV bool keys_on(const KArgs& a) {
   return (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !CXK_SKIP(a, 16);
 }
 CX_DEV bool k_in_prologue(const KArgs& a) { return keys_on(a) && a.n_steps == 1; }
-template <int EW, bool EVAL = false>
-CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+// the polygon programs' wave-scratch words that live across steps (every
+// program's first phase: the forward's load, the backward's adjoint init)
+template <int EW>
+CX_DEV void ws_poly_init(const Ctx& c, Tile<EW> t, int lane) {
   if (c.sh.poly) {  // phase F's flag array incl. its padding to a multiple of 64
     for (int w = lane; w < c.W.cf_list - c.W.cf_flag; w += WAVE) t.ws[c.W.cf_flag + w] = 0u;
     if (lane == 0) t.ws[c.W.bl_epa] = 0u;  // the first step's B list: one lane per item
   }
+}
+template <int EW, bool EVAL = false>
+CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  ws_poly_init<EW>(c, t, lane);
   // reset_mode 2 (cotix_eval's next-step autoreset): an env finished at entry
   // starts from its reset state (key chain continues, err and finished cleared)
   const bool r2 = a.reset_mode == 2 && a.dyn_reset != nullptr && a.finished != nullptr;
@@ -918,7 +925,7 @@ CX_DEV void ph_T(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       t.f(bo + 1, e) = circ ? w2 - w0 : w1;
       t.f(bo + 2, e) = circ ? w1 + w0 : w2;
       t.f(bo + 3, e) = circ ? w2 + w0 : w3;
-      if (sc.poly) {
+      if (sc.poly && (a.stages & COTIX_STAGE_BROADPHASE)) {
         // the broadphase guard's edge pseudo-angles of an AABB: the axes
         // (get_edges, cotix/_convex_shapes.py:82-93), exactly 0 and 1 (ph_TV4);
         // unused for a circle
@@ -2572,7 +2579,7 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         }
       }
     }
-    if ((a.stages & COTIX_STAGE_LUNAR) && nb >= 3) {
+    if (!REC && (a.stages & COTIX_STAGE_LUNAR) && nb >= 3) {  // (the re-play: phase G reverses them)
       Dyn d[3];
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
@@ -2918,7 +2925,140 @@ CX_DEV void ph_adj_init(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
 // d state_{step+1}; the tile holds the re-played step (post-Euler positions,
 // contacts, choices, recorded pre-resolution velocities).  Exit: adj = d ret
 // / d state_step, grad_action[step] written.
+// a part's world geometry (the tile's world words) as a Shape
 template <int EW>
+CX_DEV cx::Shape world_shape(const Ctx& c, Tile<EW> t, int p, int e) {
+  using namespace cx;
+  Shape S;
+  S.kind = t.ti(c.sh.o_pkind + p);
+  S.n = S.kind == KIND_POLY ? t.ti(c.sh.o_pn + p) : 0;
+  const int w = c.L.world + t.ti(c.sh.o_pwoff + p);
+#pragma unroll
+  for (int k = 0; k < 2 * MAXV; ++k) S.w[k] = (k < 4 || k < 2 * S.n) ? t.f(w + (k < 4 || k < 2 * S.n ? k : 0), e) : 0.0f;
+  return S;
+}
+// the cotangent of polygon part p's world vertices -> its body's position and
+// angle (the world part is Polygon.transform's forward_vector of the local
+// vertices, re-sorted: world slot k holds the local vertex whose transform
+// has its bits; phase TV1's exact arithmetic)
+template <int EW>
+CX_DEV void poly_pose_vjp(const Ctx& c, Tile<EW> t, int p, int e, const cx::Shape& W, const cx::VGrad& gv) {
+  using namespace cx;
+  const Lay& L = c.L;
+  const int b = t.ti(c.sh.o_pbody + p), o = L.dyn + 6 * b, lg = L.geo + t.ti(c.sh.o_pgoff + p);
+  const float px = t.f(o, e), py = t.f(o + 1, e);
+  float s, cs;
+  sincos32(t.f(o + 4, e), &s, &cs);
+  float gpx = 0.0f, gpy = 0.0f, gang = 0.0f;
+  for (int j = 0; j < W.n; ++j) {
+    const float x = t.f(lg + 2 * j, e), y = t.f(lg + 2 * j + 1, e);
+    const float t0 = (cs * x + (-s) * y) + px * 1.0f, t1 = (s * x + cs * y) + py * 1.0f;
+    v2 g = v2{0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {  // the slot holding this vertex (first match)
+      const bool hit = k < W.n && W.w[2 * k] == t0 && W.w[2 * k + 1] == t1 && g.x == 0.0f && g.y == 0.0f;
+      g.x = hit ? gv.x[k] : g.x;
+      g.y = hit ? gv.y[k] : g.y;
+    }
+    gpx += g.x;
+    gpy += g.y;
+    gang += drot_dot(g, v2{x, y}, s, cs);
+  }
+  const int q = L.adj + 6 * b;
+  t.f(q, e) = t.f(q, e) + gpx;
+  t.f(q + 1, e) = t.f(q + 1, e) + gpy;
+  t.f(q + 4, e) = t.f(q + 4, e) + gang;
+}
+// the joints of LunarLander.step in reverse (cotix_grad.h fixed_vjp): the
+// tile holds the post-collider, pre-joint bodies (the re-play skips them)
+template <int EW>
+CX_DEV void joints_vjp(const Ctx& c, Tile<EW> t, int e) {
+  using namespace cx;
+  const Lay& L = c.L;
+  Dyn d[3], g[3];
+  Params m[3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int o = L.dyn + 6 * b, q = L.adj + 6 * b;
+    d[b] = Dyn{t.f(o, e), t.f(o + 1, e), t.f(o + 2, e), t.f(o + 3, e), t.f(o + 4, e), t.f(o + 5, e)};
+    g[b] = Dyn{t.f(q, e), t.f(q + 1, e), t.f(q + 2, e), t.f(q + 3, e), t.f(q + 4, e), t.f(q + 5, e)};
+    m[b] = load_par(t.tb, c.sh.o_par + 4 * b);
+  }
+  // forward (lunar_constraints, the same expressions): anchors, then the
+  // bodies before each of the four impulse pairs
+  const float f05 = 0.05f;
+  float sn[3], cn[3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) sincos32(d[b].a, &sn[b], &cn[b]);
+  auto rot = [](v2 v, float s_, float c_) { return v2{c_ * v.x + (-s_) * v.y, s_ * v.x + c_ * v.y}; };
+  const v2 lp = v2{d[0].px, d[0].py};
+  const v2 loc[4] = {v2{24.0f * f05, -8.0f * f05}, v2{24.0f * f05, 0.0f * f05}, v2{-24.0f * f05, -8.0f * f05},
+                     v2{-24.0f * f05, 0.0f * f05}};
+  const v2 tip = v2{0.0f, 0.4f};
+  v2 c1[4], c2[4];
+  int leg[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    leg[f] = f < 2 ? 2 : 1;  // left leg (body 2) for the first pair, right leg (body 1) for the second
+    const Dyn& L2 = d[leg[f]];
+    c1[f] = add(rot(loc[f], sn[0], cn[0]), lp);
+    c2[f] = (f & 1) ? add(v2{L2.px, L2.py}, rot(tip, sn[leg[f]], cn[leg[f]])) : v2{L2.px, L2.py};
+  }
+  Dyn pre1[4], pre2[4];
+  Dyn cur[3] = {d[0], d[1], d[2]};
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    pre1[f] = cur[0];
+    pre2[f] = cur[leg[f]];
+    Dyn& b1 = cur[0];
+    Dyn& b2 = cur[leg[f]];
+    const v2 dp = sub(c1[f], c2[f]);
+    const v2 dv = sub(velocity_at(b1, c1[f]), velocity_at(b2, c2[f]));
+    const float k = nrm(dv) + 0.1f;
+    const v2 imp = v2{dp.x * 1.0f + (dv.x * k) * f05, dp.y * 1.0f + (dv.y * k) * f05};
+    auto apply = [](Dyn& b, const Params& mm, v2 im, v2 pt) {
+      const v2 arm = sub(pt, v2{b.px, b.py});
+      const float torque = crs(arm, im);
+      b.vx = b.vx + im.x / mm.mass;
+      b.vy = b.vy + im.y / mm.mass;
+      b.w = b.w + torque / mm.inertia;
+    };
+    apply(b1, m[0], neg(imp), c1[f]);
+    apply(b2, m[leg[f]], imp, c2[f]);
+  }
+  // reverse
+  g[1].w = g[1].w * 0.95f;
+  g[2].w = g[2].w * 0.95f;
+  v2 gc1[4], gc2[4];
+#pragma unroll
+  for (int f = 3; f >= 0; --f) {
+    gc1[f] = v2{0.0f, 0.0f};
+    gc2[f] = v2{0.0f, 0.0f};
+    fixed_vjp(pre1[f], m[0], c1[f], pre2[f], m[leg[f]], c2[f], g[0], g[leg[f]], gc1[f], gc2[f]);
+  }
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {  // anchors: rotate(local, angle) + position
+    g[0].px += gc1[f].x;
+    g[0].py += gc1[f].y;
+    g[0].a += drot_dot(gc1[f], loc[f], sn[0], cn[0]);
+    Dyn& gl = g[leg[f]];
+    gl.px += gc2[f].x;
+    gl.py += gc2[f].y;
+    if (f & 1) gl.a += drot_dot(gc2[f], tip, sn[leg[f]], cn[leg[f]]);
+  }
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int q = L.adj + 6 * b;
+    t.f(q, e) = g[b].px;
+    t.f(q + 1, e) = g[b].py;
+    t.f(q + 2, e) = g[b].vx;
+    t.f(q + 3, e) = g[b].vy;
+    t.f(q + 4, e) = g[b].a;
+    t.f(q + 5, e) = g[b].w;
+  }
+}
+
+template <int EW, int FNSET = FNS_ANALYTIC>
 CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
@@ -2927,6 +3067,7 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   for (int e = lane; e < EW; e += WAVE) {
     const int g = env0 + e;
     if (g >= a.B) continue;
+    if (FNSET != FNS_ANALYTIC && (a.stages & COTIX_STAGE_LUNAR) && nb >= 3) joints_vjp<EW>(c, t, e);
     if (a.stages & COTIX_STAGE_COLLIDER) {
       for (int i = nb - 1; i >= 0; --i) {  // resolutions in reverse order
         const int ro = L.rec + REC_W * i;
@@ -2947,6 +3088,30 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
         const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
         const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
+        if (FNSET != FNS_ANALYTIC && (fn == FN_POLY_POLY || fn == FN_AABB_POLY)) {
+          // (store the resolution's body cotangents first: the contact's go on top)
+          const float gw_[12] = {gi.px, gi.py, gi.vx, gi.vy, gi.a, gi.w, gj.px, gj.py, gj.vx, gj.vy, gj.a, gj.w};
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            t.f(ai + k, e) = gw_[k];
+            t.f(aj + k, e) = gw_[6 + k];
+          }
+          const Shape WA = world_shape<EW>(c, t, pa, e), WB = world_shape<EW>(c, t, pb, e);
+          VGrad va, vb;
+          va.zero();
+          vb.zero();
+          convex_contact_vjp(WA, WB, narrow_of(sc), gpen, gcp, va, vb);
+          const int qa = L.adj + 6 * t.ti(sc.o_pbody + pa), qb = L.adj + 6 * t.ti(sc.o_pbody + pb);
+          if (ka == KIND_AABB) {  // corners [up, (up.x, lo.y), lo, (lo.x, up.y)] -> translation
+            t.f(qa, e) = t.f(qa, e) + (((va.x[0] + va.x[1]) + va.x[2]) + va.x[3]);
+            t.f(qa + 1, e) = t.f(qa + 1, e) + (((va.y[0] + va.y[1]) + va.y[2]) + va.y[3]);
+          } else {
+            poly_pose_vjp<EW>(c, t, pa, e, WA, va);
+          }
+          poly_pose_vjp<EW>(c, t, pb, e, WB, vb);
+          (void)qb;
+          continue;
+        }
         Shape SA, SB;
         SA.kind = ka;
         SB.kind = kb;
@@ -3200,6 +3365,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
 template <int EW, int FNSET, class R>
 CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
   run(PH_ADJ, [&](int l) {
+    ws_poly_init<EW>(c, t, l);
     ph_geo<EW>(a, c, t, env0, l);
     ph_adj_init<EW>(a, c, t, env0, l);
     stage_ret_w<EW>(a, c, t, l);
@@ -3218,7 +3384,7 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
     run(PH_A, [&](int l) { ph_A<EW, false>(a, c, t, env0, l, step); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0, c.L.sk0, mc);
     run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
-    run(PH_G, [&](int l) { ph_G<EW>(a, c, t, env0, l, step); });
+    run(PH_G, [&](int l) { ph_G<EW, FNSET>(a, c, t, env0, l, step); });
   }
   run(PH_ADJ, [&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });
 }

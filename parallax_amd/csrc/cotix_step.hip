@@ -488,9 +488,11 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
     return -1;
   if (!ret_weights) return fail("null argument");
   if (grad_action && !action) return fail("grad_action needs the action the rollout was run with");
-  if (scene->fnset & ~FNS_ANALYTIC)
-    return fail("differentiable rollout: polygon contacts (GJK/EPA) are not differentiated; circle/AABB scenes only");
-  if (stages & COTIX_STAGE_LUNAR) return fail("differentiable rollout: the LunarLander joint stage is not supported");
+  if (scene->fnset & cxk::FNS_CIRCLE_POLY)
+    return fail("differentiable rollout: circle x polygon contacts are not differentiated (EPA's circle supports "
+                "chain through every iteration); circle/AABB/polygon scenes without that pair only");
+  if ((stages & COTIX_STAGE_LUNAR) && !(scene->fnset & ~FNS_ANALYTIC))
+    return fail("differentiable rollout: the LunarLander joint stage needs the polygon program (a polygon scene)");
   if (B == 0 || n_steps == 0) return 0;
   cxk::KArgs ka{};
   ka.dyn = nullptr;
@@ -501,7 +503,9 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
   ka.B = B;
   ka.n_steps = n_steps;
   ka.dt = dt;
-  ka.stages = stages;
+  // the re-play without the broadphase (an exact filter: the same contacts);
+  // its per-edge words overlay the adjoint (cxk::layout)
+  ka.stages = stages & ~COTIX_STAGE_BROADPHASE;
   ka.action = action;
   ka.action_body = action_body;
   ka.save_dyn = const_cast<float*>(saved_dyn);

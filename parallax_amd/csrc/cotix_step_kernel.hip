@@ -188,7 +188,10 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
 #endif
 #undef COTIX_LAUNCH_SPEC
   if (mode == 2) {
-    COTIX_LAUNCH(F_AN, 2);  // the host admits analytic scenes only
+    if (F == F_AN)
+      COTIX_LAUNCH(F_AN, 2);
+    else
+      COTIX_LAUNCH(F_ALL, 2);  // polygon scenes (the host rejects circle x polygon contacts)
   } else if (mode == 3) {
     if (F == F_AN)
       COTIX_LAUNCH(F_AN, 3);

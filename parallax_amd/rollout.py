@@ -10,7 +10,9 @@ adds gravity (examples/test_viz.py:27-31) -- and the return is
 over the n_bodies*6 state words (default: the ball's x position, body 4 of
 RoboCup).  Derivatives are jax.grad's through the reference: the executed
 branch of every lax.cond, RandomizedCollider choices held fixed, balanced
-ties for max/min/clip.  Circle/AABB scenes only (no GJK/EPA derivative).
+ties for max/min/clip.  Circle, AABB and polygon contacts (GJK/EPA through
+EPA's final edge and contact_from_edges) and the LunarLander joints
+(stages=_ffi.STAGES_LUNAR); circle x polygon scenes are rejected.
 """
 import numpy as np
 import torch

@@ -69,7 +69,7 @@ void run_blocks(const cxk::KArgs& a, int mode) {
     cxk_simt::run([&](int lane) {
       const HostRun run{lane};
       if (mode == 2)
-        cxk::run_wave_backward<EW, 1>(a, c, t, env0, run);
+        F == 1 ? cxk::run_wave_backward<EW, 1>(a, c, t, env0, run) : cxk::run_wave_backward<EW, 15>(a, c, t, env0, run);
       else if (mode == 1)
         F == 1 ? cxk::run_wave<EW, 1, true>(a, c, t, env0, run) : cxk::run_wave<EW, 15, true>(a, c, t, env0, run);
       else if (mode == 3)
@@ -234,8 +234,12 @@ int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* sa
                          int gstride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
                          const float* ret_w, float* grad_action, float* grad_dyn0, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
-  if (s->fnset & ~1) {
-    g_err = "differentiable rollout: circle/AABB scenes only";
+  if (s->fnset & cxk::FNS_CIRCLE_POLY) {  // (the library's admission, cotix_step.hip)
+    g_err = "differentiable rollout: circle x polygon contacts are not differentiated";
+    return -1;
+  }
+  if ((stages & COTIX_STAGE_LUNAR) && !(s->fnset & ~1)) {
+    g_err = "differentiable rollout: the LunarLander joint stage needs the polygon program";
     return -1;
   }
   cxk::KArgs a{};
@@ -245,7 +249,7 @@ int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* sa
   a.B = B;
   a.n_steps = n_steps;
   a.dt = dt;
-  a.stages = stages;
+  a.stages = stages & ~COTIX_STAGE_BROADPHASE;  // (the library's re-play, cotix_step.hip)
   a.action = action;
   a.action_body = action_body;
   a.save_dyn = const_cast<float*>(saved_dyn);

@@ -50,6 +50,74 @@ def robocup_case(B, T, seed=0):
                 actions=actions, w=w, ab=4, step=P.robocup_step)
 
 
+def lunar_case(B, T, seed=0, drop=-0.02):
+    """LunarLander (cotix/_lunar_lander.py) started with its legs on the landing
+    pad (y = -2 between x = -2 and 2): polygon x polygon contacts (GJK/EPA,
+    contact_from_edges) and the four joints from the first step.  Per env a
+    random lander/leg velocity and a small common offset."""
+    make = lambda: P.lunar_lander_bodies(prng.PRNGKey(0))  # noqa: E731
+    base = np.array([b.dyn() for b in make()], np.float32)
+    rng = np.random.default_rng(seed)
+    S0 = np.repeat(base[None], B, axis=0)
+    for e in range(B):
+        dx, dy = rng.uniform(-0.3, 0.3), -(5.0 + 1.2) + drop + rng.uniform(-0.05, 0.05)
+        for b in range(3):
+            S0[e, b, 0] += dx
+            S0[e, b, 1] += dy
+            S0[e, b, 2] = rng.uniform(-0.5, 0.5)
+            S0[e, b, 3] = rng.uniform(-1.0, 0.2)
+            S0[e, b, 5] = rng.uniform(-0.5, 0.5)
+    keys = np.asarray(prng.split(prng.PRNGKey(21 + seed), B), np.uint32)
+    actions = (rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32)
+    w = np.zeros(4 * 6, np.float32)
+    w[0] = 1.0          # lander x
+    w[1] = 0.5          # lander y
+    w[4] = 2.0          # lander angle
+    w[2 * 6 + 3] = 0.25  # left leg vy
+    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=0,
+                step=P.lunar_lander_step)
+
+
+def poly_box_bodies():
+    """A static AABB floor and wall with two dynamic polygons (a Polygon4 box
+    and a Polygon6 hexagon) resting on the floor against each other:
+    aabb_vs_polygon and polygon_vs_polygon contacts of rotating bodies."""
+    from cotix_oracle import geometry as Gm
+    floor = P.Body([Gm.AABB((-5.0, -1.0), (5.0, 0.0))], mass=np.inf, inertia=np.inf, elasticity=0.3,
+                   friction_coefficient=0.4)
+    wall = P.Body([Gm.AABB((-1.2, 0.0), (-0.9, 2.0))], mass=np.inf, inertia=np.inf, elasticity=0.3,
+                  friction_coefficient=0.4)
+    sq = Gm.Polygon([(-0.3, -0.3), (0.3, -0.3), (0.3, 0.3), (-0.3, 0.3)], kind="Polygon4")
+    hexv = [(0.35 * np.cos(k * np.pi / 3), 0.35 * np.sin(k * np.pi / 3)) for k in range(6)]
+    hx = Gm.Polygon(hexv, kind="Polygon6")
+    box = P.Body([sq], mass=1.0, inertia=0.06, position=(-0.55, 0.28), angle=0.1, elasticity=0.5,
+                 friction_coefficient=0.3)
+    hexa = P.Body([hx], mass=1.5, inertia=0.09, position=(0.1, 0.32), angle=0.05, elasticity=0.5,
+                  friction_coefficient=0.3)
+    return [floor, wall, box, hexa]
+
+
+def poly_box_case(B, T, seed=0):
+    make = poly_box_bodies
+    base = np.array([b.dyn() for b in make()], np.float32)
+    rng = np.random.default_rng(seed)
+    S0 = np.repeat(base[None], B, axis=0)
+    for e in range(B):
+        for b in (2, 3):
+            S0[e, b, 0] += rng.uniform(-0.03, 0.03)
+            S0[e, b, 1] += rng.uniform(-0.03, 0.0)
+            S0[e, b, 2:4] = rng.uniform(-0.5, 0.5, 2)
+            S0[e, b, 4] += rng.uniform(-0.1, 0.1)
+            S0[e, b, 5] = rng.uniform(-1.0, 1.0)
+    keys = np.asarray(prng.split(prng.PRNGKey(31 + seed), B), np.uint32)
+    actions = (rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32)
+    w = np.zeros(4 * 6, np.float32)
+    w[2 * 6 + 0] = 1.0   # box x
+    w[3 * 6 + 1] = 0.5   # hexagon y
+    w[3 * 6 + 4] = 1.0   # hexagon angle
+    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=2, step=P.robocup_step)
+
+
 def oracle(case, envs=None):
     """Per env: (ret, grad_actions [T,2], grad_S0 [nb,6]) from the torch VJP chain."""
     B = case["S0"].shape[0]

@@ -538,23 +538,34 @@ def test_config1_lunar_single_env_10000_steps_vs_cport(torch_cuda, cport_lib):
 # ---------------------------------------------------------------------------
 # differentiable rollout (BASELINE config 5)
 # ---------------------------------------------------------------------------
-def _gpu_rollout(torch, case, bodies_pa, want_dyn0=True):
+def _gpu_rollout(torch, case, bodies_pa, want_dyn0=True, stages=None, world=None):
     import parallax_amd as pa
     B = case["S0"].shape[0]
-    w = pa.World(bodies_pa, B, "cuda", torch.tensor(u32_to_i32(case["keys"]), device="cuda"))
+    keys = torch.tensor(u32_to_i32(case["keys"]), device="cuda")
+    w = pa.World(bodies_pa, B, "cuda", keys) if world is None else world
+    if world is not None:
+        w.keys.copy_(keys)
     w.dyn.copy_(torch.tensor(case["S0"], device="cuda").permute(1, 2, 0))
     acts = torch.tensor(case["actions"], device="cuda")
-    ret, saved = pa.rollout_forward(w, acts, case["ab"], case["w"])
+    ret, saved = pa.rollout_forward(w, acts, case["ab"], case["w"],
+                                    stages=pa._ffi.STAGES_ROBOCUP if stages is None else stages)
     ga, gd = pa.rollout_backward(w, saved, want_dyn0=want_dyn0)
     torch.cuda.synchronize()
     return w, ret.cpu().numpy(), ga.cpu().numpy(), (gd.cpu().numpy() if gd is not None else None), saved
 
 
+def _pa_part(pa, p):
+    if p.kind == "AABB":
+        return pa.AABB(list(p.lower), list(p.upper))
+    if p.kind == "Circle":
+        return pa.Circle(p.radius, list(p.position))
+    return getattr(pa, p.kind)([list(v) for v in p.vertices_], presorted=True)
+
+
 def _pa_bodies(pa, oracle_bodies):
     out = []
     for b in oracle_bodies:
-        parts = [pa.AABB(list(p.lower), list(p.upper)) if p.kind == "AABB" else pa.Circle(p.radius, list(p.position))
-                 for p in b.parts]
+        parts = [_pa_part(pa, p) for p in b.parts]
         out.append(pa.AnyBody(shape=pa.UniversalShape(*parts), mass=b.mass, inertia=b.inertia,
                               position=list(b.position), velocity=list(b.velocity), angle=b.angle,
                               angular_velocity=b.angular_velocity, elasticity=b.elasticity,
@@ -576,6 +587,42 @@ def test_rollout_grad_box_world_vs_oracle(torch_cuda):
         assert ok, "env %d grad_action %s" % (e, msg)
         ok, msg = GC.close(gd[:, :, e], ogS)
         assert ok, "env %d grad_dyn0 %s" % (e, msg)
+
+
+def _check_grad_vs_oracle(case, ret, ga, gd):
+    import grad_cases as GC
+    orc = GC.oracle(case)
+    for e in orc:
+        r, oga, ogS = orc[e]
+        assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)
+        ok, msg = GC.close(ga[:, e], oga)
+        assert ok, "env %d grad_action %s" % (e, msg)
+        ok, msg = GC.close(gd[:, :, e], ogS)
+        assert ok, "env %d grad_dyn0 %s" % (e, msg)
+
+
+def test_rollout_grad_lunar_vs_oracle(torch_cuda):
+    """Gradients through GJK/EPA polygon contacts and the LunarLander joints
+    (legs on the landing pad from step 0; broadphase on in the forward)."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    case = GC.lunar_case(8, 12, seed=0)
+    ll = pa.LunarLander(batch=8)
+    _, ret, ga, gd, _ = _gpu_rollout(torch, case, None, stages=pa._ffi.STAGES_LUNAR | pa._ffi.STAGE_BROADPHASE,
+                                     world=ll.world)
+    _check_grad_vs_oracle(case, ret, ga, gd)
+    assert np.abs(gd).max() > 1.0
+
+
+def test_rollout_grad_polygon_box_vs_oracle(torch_cuda):
+    """AABB x polygon and polygon x polygon contacts of rotating polygons."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    case = GC.poly_box_case(8, 10, seed=0)
+    _, ret, ga, gd, _ = _gpu_rollout(torch, case, _pa_bodies(pa, case["make"]()))
+    _check_grad_vs_oracle(case, ret, ga, gd)
 
 
 def test_rollout_grad_robocup_vs_oracle(torch_cuda):

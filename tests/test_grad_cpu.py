@@ -96,16 +96,105 @@ def test_emu_rollout_robocup(emu_lib):
     assert finite >= 1
 
 
-def test_backward_rejects_polygon_scenes(emu_lib):
+LUNAR_STAGES = 1 | 2 | 4 | 8 | 16 | 32  # incl. the broadphase (the backward re-plays without it)
+
+
+def _fd_actions(case, e, points, eps=1e-2):
+    """Central differences of the faithful oracle's return in the actions."""
+    T = case["actions"].shape[0]
+    out = []
+    for (t, c) in points:
+        vals = []
+        for s in (1, -1):
+            a = case["actions"][:, e].copy()
+            a[t, c] += s * eps
+            bodies = case["make"]()
+            for b, row in zip(bodies, case["S0"][e]):
+                b.set_dyn(row)
+            key, tot = case["keys"][e], 0.0
+            for tt in range(T):
+                bodies, key = case["step"](bodies, key, GC.D0, action=a[tt], action_body=case["ab"])
+                tot += float(np.dot(case["w"], np.array([b.dyn() for b in bodies], np.float64).reshape(-1)))
+            vals.append(tot)
+        out.append((vals[0] - vals[1]) / (2 * eps))
+    return out
+
+
+@pytest.mark.parametrize("scene", ["lunar", "poly_box"])
+def test_oracle_grad_polygons_vs_finite_differences(scene):
+    """The checker through GJK/EPA, contact_from_edges and (LunarLander) the
+    joints: torch VJP chain vs central differences of the faithful oracle
+    (cases without discrete flips at eps = 1e-2)."""
+    case = GC.lunar_case(4, 6, seed=0) if scene == "lunar" else GC.poly_box_case(4, 10, seed=0)
+    orc = GC.oracle(case)
+    pts = [(0, 0), (0, 1), (2, 0), (5, 1)]
+    nontrivial = 0
+    for e in range(4):
+        ga = orc[e][1]
+        for (t, c), fd in zip(pts, _fd_actions(case, e, pts)):
+            assert abs(fd - ga[t, c]) <= 2e-3 * (1 + abs(fd)), (e, t, c, fd, ga[t, c])
+            nontrivial += int(abs(ga[t, c]) > 1e-3)
+    assert nontrivial >= 8
+
+
+def _emu_run_st(emu, lib, case, stages, E=4):
+    h, geom = emu.oracle_scene(lib, case["make"]())
+    dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
+    keys = np.array(case["keys"], np.uint32, copy=True)
+    err = np.zeros(dyn.shape[2], np.uint32)
+    ret, sd, sk = emu.rollout(lib, h, dyn, keys, err, geom, 0, stages, case["actions"], case["ab"], case["w"], E=E)
+    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, stages, case["actions"], case["ab"], case["w"], E=E)
+    return ret, ga, gd
+
+
+def _check_vs_oracle(case, ret, ga, gd):
+    orc = GC.oracle(case)
+    for e in orc:
+        r, oga, ogS = orc[e]
+        assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)  # bit-exact
+        ok, msg = GC.close(ga[:, e], oga)
+        assert ok, "env %d grad_action: %s" % (e, msg)
+        ok, msg = GC.close(gd[:, :, e], ogS)
+        assert ok, "env %d grad_dyn0: %s" % (e, msg)
+
+
+@pytest.mark.parametrize("E", [1, 4])
+def test_emu_rollout_lunar(emu_lib, E):
+    """LunarLander with its legs on the pad: polygon x polygon contacts every
+    step plus the four joints, 12 steps, against the VJP oracle."""
     emu, lib = emu_lib
+    case = GC.lunar_case(4, 12, seed=0)
+    ret, ga, gd = _emu_run_st(emu, lib, case, LUNAR_STAGES, E)
+    _check_vs_oracle(case, ret, ga, gd)
+    assert np.abs(gd[:, :, :]).max() > 1.0
+
+
+def test_emu_rollout_poly_box(emu_lib):
+    """AABB x polygon and polygon x polygon contacts of two rotating polygons."""
+    emu, lib = emu_lib
+    case = GC.poly_box_case(6, 10, seed=0)
+    ret, ga, gd = _emu_run_st(emu, lib, case, 1 | 4 | 16)
+    _check_vs_oracle(case, ret, ga, gd)
+
+
+def test_backward_rejects_circle_polygon_and_analytic_joints(emu_lib):
+    """Circle x polygon contacts are not differentiated (EPA's circle supports
+    chain through every iteration); the joint stage needs the polygon program."""
+    emu, lib = emu_lib
+    from cotix_oracle import geometry as Gm
     from cotix_oracle import physics as P
-    from cotix_oracle import prng
-    h, geom = emu.oracle_scene(lib, P.lunar_lander_bodies(prng.PRNGKey(0)))
-    sd = np.zeros((1, 4, 6, 1), np.float32)
+    bodies = GC.poly_box_bodies() + [P.Body([Gm.Circle(0.2, (0.0, 0.0))], position=(1.5, 0.2))]
+    h, geom = emu.oracle_scene(lib, bodies)
+    sd = np.zeros((1, 5, 6, 1), np.float32)
     sk = np.zeros((1, 1, 2), np.uint32)
-    with pytest.raises(RuntimeError, match="circle/AABB"):
+    with pytest.raises(RuntimeError, match="circle x polygon"):
         emu.rollout_backward(lib, h, sd, sk, geom, 0, 1 | 4 | 16, np.zeros((1, 1, 2), np.float32), 0,
-                             np.zeros(24, np.float32))
+                             np.zeros(30, np.float32))
+    case = GC.box_case(1, 1)
+    h, geom = emu.oracle_scene(lib, case["make"]())
+    with pytest.raises(RuntimeError, match="joint stage"):
+        emu.rollout_backward(lib, h, np.zeros((1, 7, 6, 1), np.float32), sk, geom, 0, 1 | 4 | 8 | 16,
+                             np.zeros((1, 1, 2), np.float32), 0, np.zeros(42, np.float32))
 
 
 @pytest.mark.parametrize("nterms", [8, 42])

@@ -266,57 +266,94 @@ CX_DEV int cvx_edge_prev(const Shape& s, int k) {
   if (s.kind == KIND_AABB) return (k + 1) & 3;
   return k == 0 ? s.n - 1 : k - 1;
 }
+// one pass: every included term's VJP with the cotangent gcp, then / n
+// (cp = acc / n is linear in the terms).  The vertex and edge loops are
+// unrolled to MAXV with k < n guards (as contact_from_edges): vertex picks
+// and cotangent slots are compile-time indices (no select chains) except the
+// wrap-around edge's last vertex.
 CX_DEV void contact_from_edges_vjp(const Shape& A, const Shape& B, v2 gcp, VGrad& ga, VGrad& gb) {
   const int na = cvx_count(A), nb = cvx_count(B);
+  const v2 lastA = A.kind == KIND_AABB ? v2{0.0f, 0.0f} : vert(A, A.n - 1);
+  const v2 lastB = B.kind == KIND_AABB ? v2{0.0f, 0.0f} : vert(B, B.n - 1);
+  VGrad ca, cb;
+  ca.zero();
+  cb.zero();
   float n = 0.0f;  // the forward's term count
-  for (int k = 0; k < na; ++k) n = shape_contains(B, cvx_vert_r(A, k)) ? n + 1.0f : n;
-  for (int k = 0; k < nb; ++k) n = shape_contains(A, cvx_vert_r(B, k)) ? n + 1.0f : n;
-  for (int jb = 0; jb < nb; ++jb)
-    for (int ia = 0; ia < na; ++ia) {
-      const v2 x = edge_vs_edge(cvx_vert_r(A, ia), cvx_vert_r(A, cvx_edge_prev(A, ia)), cvx_vert_r(B, jb),
-                                cvx_vert_r(B, cvx_edge_prev(B, jb)));
-      n = vnan(x) ? n : n + 1.0f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (k < na && shape_contains(B, cvx_vert(A, k))) {
+      ca.x[k] += gcp.x;
+      ca.y[k] += gcp.y;
+      n = n + 1.0f;
+    }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k)
+    if (k < nb && shape_contains(A, cvx_vert(B, k))) {
+      cb.x[k] += gcp.x;
+      cb.y[k] += gcp.y;
+      n = n + 1.0f;
+    }
+#pragma unroll
+  for (int jb = 0; jb < MAXV; ++jb)
+    if (jb < nb) {
+      v2 b0, b1;
+      cvx_edge(B, jb, lastB, &b0, &b1);
+      const int pb = cvx_edge_prev(B, jb);
+#pragma unroll
+      for (int ia = 0; ia < MAXV; ++ia)
+        if (ia < na) {
+          v2 a0, a1;
+          cvx_edge(A, ia, lastA, &a0, &a1);
+          if (vnan(edge_vs_edge(a0, a1, b0, b1))) continue;
+          n = n + 1.0f;
+          v2 g0 = v2{0.0f, 0.0f}, g1 = g0, h0 = g0, h1 = g0;
+          edge_vs_edge_vjp(a0, a1, b0, b1, gcp, &g0, &g1, &h0, &h1);
+          ca.x[ia] += g0.x;
+          ca.y[ia] += g0.y;
+          ca.add(cvx_edge_prev(A, ia), g1);
+          cb.x[jb] += h0.x;
+          cb.y[jb] += h0.y;
+          cb.add(pb, h1);
+        }
     }
   if (!(n > 0.0f)) return;
-  const v2 g = divs(gcp, n);  // cp = acc / n
-  for (int k = 0; k < na; ++k)
-    if (shape_contains(B, cvx_vert_r(A, k))) ga.add(k, g);
-  for (int k = 0; k < nb; ++k)
-    if (shape_contains(A, cvx_vert_r(B, k))) gb.add(k, g);
-  for (int jb = 0; jb < nb; ++jb)
-    for (int ia = 0; ia < na; ++ia) {
-      const int pa = cvx_edge_prev(A, ia), pb = cvx_edge_prev(B, jb);
-      const v2 a0 = cvx_vert_r(A, ia), a1 = cvx_vert_r(A, pa), b0 = cvx_vert_r(B, jb), b1 = cvx_vert_r(B, pb);
-      if (vnan(edge_vs_edge(a0, a1, b0, b1))) continue;
-      v2 g0 = v2{0.0f, 0.0f}, g1 = g0, h0 = g0, h1 = g0;
-      edge_vs_edge_vjp(a0, a1, b0, b1, g, &g0, &g1, &h0, &h1);
-      ga.add(ia, g0);
-      ga.add(pa, g1);
-      gb.add(jb, h0);
-      gb.add(pb, h1);
-    }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    ga.x[k] += ca.x[k] / n;
+    ga.y[k] += ca.y[k] / n;
+    gb.x[k] += cb.x[k] / n;
+    gb.y[k] += cb.y[k] / n;
+  }
 }
 // the whole convex contact: re-runs GJK and EPA (the forward's exact code,
-// so the final edge is the forward's) and returns the per-vertex cotangents
+// so the final edge is the forward's) and returns the per-vertex cotangents;
+// `make` supplies EPA's edge storage (MakeRegs: registers; MakeCol: a
+// per-lane LDS column, as the step kernel's phase B)
+template <class MakeStore = MakeRegs>
 CX_DEV void convex_contact_vjp(const Shape& A, const Shape& B, const NarrowParams& np, v2 gpen, v2 gcp, VGrad& ga,
-                               VGrad& gb) {
-  v2 simplex[3];
-  if (!gjk(A, B, np.d0, simplex, np.gjk_steps)) return;  // (not reached for a resolved contact)
-  const int it0 = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
-  const int iters = it0 < np.epa_cap ? it0 : np.epa_cap;
-  v2 e0, e1;
-  if (iters + 3 <= 14) {
-    EdgeRegs<14> es;
-    epa_edge<14>(A, B, simplex, iters, es, &e0, &e1);
-  } else {
-    EdgeRegs<20> es;
-    epa_edge<20>(A, B, simplex, iters, es, &e0, &e1);
+                               VGrad& gb, MakeStore make = MakeStore{}) {
+  // (each half only for a nonzero cotangent: phase GE's unit cotangents
+  // take one of the two paths per lane)
+  if (gpen.x != 0.0f || gpen.y != 0.0f) {
+    v2 simplex[3];
+    if (gjk(A, B, np.d0, simplex, np.gjk_steps)) {  // (always, for a resolved contact)
+      const int it0 = (A.kind == KIND_AABB) ? (4 + B.n + 1) : (A.n + B.n + 1);
+      const int iters = it0 < np.epa_cap ? it0 : np.epa_cap;
+      v2 e0, e1;
+      if (iters + 3 <= 14) {
+        auto es = make.template get<14>();
+        epa_edge<14>(A, B, simplex, iters, es, &e0, &e1);
+      } else {
+        auto es = make.template get<20>();
+        epa_edge<20>(A, B, simplex, iters, es, &e0, &e1);
+      }
+      v2 g0 = v2{0.0f, 0.0f}, g1 = v2{0.0f, 0.0f};
+      closest_vjp(e0, e1, gpen, &g0, &g1);
+      minkowski_vjp(A, B, e0, g0, ga, gb);
+      minkowski_vjp(A, B, e1, g1, ga, gb);
+    }
   }
-  v2 g0 = v2{0.0f, 0.0f}, g1 = v2{0.0f, 0.0f};
-  closest_vjp(e0, e1, gpen, &g0, &g1);
-  minkowski_vjp(A, B, e0, g0, ga, gb);
-  minkowski_vjp(A, B, e1, g1, ga, gb);
-  contact_from_edges_vjp(A, B, gcp, ga, gb);
+  if (gcp.x != 0.0f || gcp.y != 0.0f) contact_from_edges_vjp(A, B, gcp, ga, gb);
 }
 
 // ---------------------------------------------------------------------------

@@ -2937,13 +2937,21 @@ CX_DEV cx::Shape world_shape(const Ctx& c, Tile<EW> t, int p, int e) {
   for (int k = 0; k < 2 * MAXV; ++k) S.w[k] = (k < 4 || k < 2 * S.n) ? t.f(w + (k < 4 || k < 2 * S.n ? k : 0), e) : 0.0f;
   return S;
 }
-// the cotangent of polygon part p's world vertices -> its body's position and
-// angle (the world part is Polygon.transform's forward_vector of the local
+// the cotangent of part p's world vertices -> its body's (px, py, angle).
+// A polygon's world part is Polygon.transform's forward_vector of the local
 // vertices, re-sorted: world slot k holds the local vertex whose transform
-// has its bits; phase TV1's exact arithmetic)
+// has its bits (phase TV1's exact arithmetic).  An AABB translates only
+// (corners [up, (up.x, lo.y), lo, (lo.x, up.y)]).
 template <int EW>
-CX_DEV void poly_pose_vjp(const Ctx& c, Tile<EW> t, int p, int e, const cx::Shape& W, const cx::VGrad& gv) {
+CX_DEV void part_pose_vjp(const Ctx& c, Tile<EW> t, int p, int e, const cx::Shape& W, const cx::VGrad& gv,
+                          float* out) {
   using namespace cx;
+  if (W.kind == KIND_AABB) {
+    out[0] = ((gv.x[0] + gv.x[1]) + gv.x[2]) + gv.x[3];
+    out[1] = ((gv.y[0] + gv.y[1]) + gv.y[2]) + gv.y[3];
+    out[2] = 0.0f;
+    return;
+  }
   const Lay& L = c.L;
   const int b = t.ti(c.sh.o_pbody + p), o = L.dyn + 6 * b, lg = L.geo + t.ti(c.sh.o_pgoff + p);
   const float px = t.f(o, e), py = t.f(o + 1, e);
@@ -2954,20 +2962,21 @@ CX_DEV void poly_pose_vjp(const Ctx& c, Tile<EW> t, int p, int e, const cx::Shap
     const float x = t.f(lg + 2 * j, e), y = t.f(lg + 2 * j + 1, e);
     const float t0 = (cs * x + (-s) * y) + px * 1.0f, t1 = (s * x + cs * y) + py * 1.0f;
     v2 g = v2{0.0f, 0.0f};
+    bool found = false;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {  // the slot holding this vertex (first match)
-      const bool hit = k < W.n && W.w[2 * k] == t0 && W.w[2 * k + 1] == t1 && g.x == 0.0f && g.y == 0.0f;
+      const bool hit = k < W.n && !found && W.w[2 * k] == t0 && W.w[2 * k + 1] == t1;
       g.x = hit ? gv.x[k] : g.x;
       g.y = hit ? gv.y[k] : g.y;
+      found = found || hit;
     }
     gpx += g.x;
     gpy += g.y;
     gang += drot_dot(g, v2{x, y}, s, cs);
   }
-  const int q = L.adj + 6 * b;
-  t.f(q, e) = t.f(q, e) + gpx;
-  t.f(q + 1, e) = t.f(q + 1, e) + gpy;
-  t.f(q + 4, e) = t.f(q + 4, e) + gang;
+  out[0] = gpx;
+  out[1] = gpy;
+  out[2] = gang;
 }
 // the joints of LunarLander.step in reverse (cotix_grad.h fixed_vjp): the
 // tile holds the post-collider, pre-joint bodies (the re-play skips them)
@@ -3058,6 +3067,50 @@ CX_DEV void joints_vjp(const Ctx& c, Tile<EW> t, int e) {
   }
 }
 
+// phase GE (polygon backward): the GJK/EPA contacts' derivatives, ahead of
+// the serial adjoint chain of phase G.  A contact's VJP is linear in its
+// cotangent (pen, cp), so item = (basis k, resolution i, env) computes the
+// VJP of the unit cotangent k (pen.x, pen.y, cp.x, cp.y) down to the two
+// bodies' (px, py, angle) (cotix_grad.h convex_contact_vjp: GJK, EPA's final
+// edge -- in the lane's LDS column, as phase B -- contact_from_edges;
+// part_pose_vjp): 24 words per resolution in the key-window words, which the
+// backward does not use (it splits each step's keys in phase A); phase G
+// contracts them with the contact's actual cotangent.  Scenes whose 24 * nb
+// words exceed the key window do the VJP inside phase G instead.
+CX_HD bool ge_fits(const Ctx& c) { return 24 * c.nb <= KWIN * c.L.kww; }
+template <int EW>
+CX_DEV int ge_word(const Ctx& c, int i, int k) {
+  return c.L.kw + 24 * i + 6 * k;
+}
+template <int EW>
+CX_DEV void ph_GE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const Lay& L = c.L;
+  float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
+  for (int w = lane; w < c.nb * EW * 4; w += WAVE) {
+    const int e = w % EW, q = w / EW, i = q >> 2, k = q & 3;
+    if (env0 + e >= a.B || t.w(L.rec + REC_W * i, e) == 0u) continue;
+    const int j = (int)t.w(L.ch + i, e);
+    const int cid = (int)((t.w(L.m + i * c.nb + j, e) >> 18) & 511u);
+    const int fn = t.ti(sc.o_cfn + cid);
+    if (fn != FN_POLY_POLY && fn != FN_AABB_POLY) continue;
+    const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid);
+    const Shape WA = world_shape<EW>(c, t, pa, e), WB = world_shape<EW>(c, t, pb, e);
+    VGrad va, vb;
+    va.zero();
+    vb.zero();
+    const v2 gpen = v2{k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f}, gcp = v2{k == 2 ? 1.0f : 0.0f, k == 3 ? 1.0f : 0.0f};
+    convex_contact_vjp(WA, WB, narrow_of(sc), gpen, gcp, va, vb, MakeCol{col, WAVE});
+    float o[6];
+    part_pose_vjp<EW>(c, t, pa, e, WA, va, o);
+    part_pose_vjp<EW>(c, t, pb, e, WB, vb, o + 3);
+    const int ow = ge_word<EW>(c, i, k);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) t.f(ow + r, e) = o[r];
+  }
+}
+
 template <int EW, int FNSET = FNS_ANALYTIC>
 CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   using namespace cx;
@@ -3096,20 +3149,31 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
             t.f(ai + k, e) = gw_[k];
             t.f(aj + k, e) = gw_[6 + k];
           }
-          const Shape WA = world_shape<EW>(c, t, pa, e), WB = world_shape<EW>(c, t, pb, e);
-          VGrad va, vb;
-          va.zero();
-          vb.zero();
-          convex_contact_vjp(WA, WB, narrow_of(sc), gpen, gcp, va, vb);
-          const int qa = L.adj + 6 * t.ti(sc.o_pbody + pa), qb = L.adj + 6 * t.ti(sc.o_pbody + pb);
-          if (ka == KIND_AABB) {  // corners [up, (up.x, lo.y), lo, (lo.x, up.y)] -> translation
-            t.f(qa, e) = t.f(qa, e) + (((va.x[0] + va.x[1]) + va.x[2]) + va.x[3]);
-            t.f(qa + 1, e) = t.f(qa + 1, e) + (((va.y[0] + va.y[1]) + va.y[2]) + va.y[3]);
+          float gp[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+          if (ge_fits(c)) {  // the contact's VJP from phase GE's basis responses
+            const float gk[4] = {gpen.x, gpen.y, gcp.x, gcp.y};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int m = ge_word<EW>(c, i, k);
+#pragma unroll
+              for (int q = 0; q < 6; ++q) gp[q] += gk[k] * t.f(m + q, e);
+            }
           } else {
-            poly_pose_vjp<EW>(c, t, pa, e, WA, va);
+            const Shape WA = world_shape<EW>(c, t, pa, e), WB = world_shape<EW>(c, t, pb, e);
+            VGrad va, vb;
+            va.zero();
+            vb.zero();
+            convex_contact_vjp(WA, WB, narrow_of(sc), gpen, gcp, va, vb);
+            part_pose_vjp<EW>(c, t, pa, e, WA, va, gp);
+            part_pose_vjp<EW>(c, t, pb, e, WB, vb, gp + 3);
           }
-          poly_pose_vjp<EW>(c, t, pb, e, WB, vb);
-          (void)qb;
+          const int qa = L.adj + 6 * t.ti(sc.o_pbody + pa), qb = L.adj + 6 * t.ti(sc.o_pbody + pb);
+          t.f(qa, e) = t.f(qa, e) + gp[0];
+          t.f(qa + 1, e) = t.f(qa + 1, e) + gp[1];
+          t.f(qa + 4, e) = t.f(qa + 4, e) + gp[2];
+          t.f(qb, e) = t.f(qb, e) + gp[3];
+          t.f(qb + 1, e) = t.f(qb + 1, e) + gp[4];
+          t.f(qb + 4, e) = t.f(qb + 4, e) + gp[5];
           continue;
         }
         Shape SA, SB;
@@ -3186,7 +3250,7 @@ CX_DEV void ph_adj_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int
 // only by the phase-timing build (COTIX_PHASE_PROF, tools/phase_prof.py).
 enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH_C3, PH_D, PH_E, PH_RET, PH_STORE,
              PH_RESTORE, PH_G, PH_ADJ, PH_F, PH_K, PH_E1, PH_R, PH_TRACE, PH_BP0, PH_BP1, PH_F0, PH_F1, PH_F2, PH_F3,
-             PH_TV0, PH_TV1, PH_TV2, PH_TV3, PH_J, PH_COUNT };
+             PH_TV0, PH_TV1, PH_TV2, PH_TV3, PH_J, PH_GE, PH_COUNT };
 // ---------------------------------------------------------------------------
 // kso: tile offset of this step's sk0 (skt follows): the key window slot, or
 // L.sk0 where phase A splits the keys (backward re-play)
@@ -3384,6 +3448,8 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
     run(PH_A, [&](int l) { ph_A<EW, false>(a, c, t, env0, l, step); });
     if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, false>(a, c, t, env0, run, 0, c.L.sk0, mc);
     run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
+    if (FNSET != FNS_ANALYTIC && (a.stages & COTIX_STAGE_COLLIDER) && ge_fits(c))
+      run(PH_GE, [&](int l) { ph_GE<EW>(a, c, t, env0, l); });
     run(PH_G, [&](int l) { ph_G<EW, FNSET>(a, c, t, env0, l, step); });
   }
   run(PH_ADJ, [&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });

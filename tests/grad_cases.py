@@ -78,10 +78,12 @@ def lunar_case(B, T, seed=0, drop=-0.02):
                 step=P.lunar_lander_step)
 
 
-def poly_box_bodies():
+def poly_box_bodies(octagons=False):
     """A static AABB floor and wall with two dynamic polygons (a Polygon4 box
-    and a Polygon6 hexagon) resting on the floor against each other:
-    aabb_vs_polygon and polygon_vs_polygon contacts of rotating bodies."""
+    and a Polygon6 hexagon, or two 8-gons) resting on the floor against each
+    other: aabb_vs_polygon and polygon_vs_polygon contacts of rotating bodies
+    (8-gon pairs have 80 contact_from_edges terms: the backward's in-chain
+    path)."""
     from cotix_oracle import geometry as Gm
     floor = P.Body([Gm.AABB((-5.0, -1.0), (5.0, 0.0))], mass=np.inf, inertia=np.inf, elasticity=0.3,
                    friction_coefficient=0.4)
@@ -90,6 +92,11 @@ def poly_box_bodies():
     sq = Gm.Polygon([(-0.3, -0.3), (0.3, -0.3), (0.3, 0.3), (-0.3, 0.3)], kind="Polygon4")
     hexv = [(0.35 * np.cos(k * np.pi / 3), 0.35 * np.sin(k * np.pi / 3)) for k in range(6)]
     hx = Gm.Polygon(hexv, kind="Polygon6")
+    if octagons:
+        sq = Gm.Polygon([(0.32 * np.cos(k * np.pi / 4 + 0.3), 0.32 * np.sin(k * np.pi / 4 + 0.3)) for k in range(8)],
+                        kind="Polygon")
+        hx = Gm.Polygon([(0.35 * np.cos(k * np.pi / 4), 0.35 * np.sin(k * np.pi / 4)) for k in range(8)],
+                        kind="Polygon")
     box = P.Body([sq], mass=1.0, inertia=0.06, position=(-0.55, 0.28), angle=0.1, elasticity=0.5,
                  friction_coefficient=0.3)
     hexa = P.Body([hx], mass=1.5, inertia=0.09, position=(0.1, 0.32), angle=0.05, elasticity=0.5,
@@ -97,8 +104,8 @@ def poly_box_bodies():
     return [floor, wall, box, hexa]
 
 
-def poly_box_case(B, T, seed=0):
-    make = poly_box_bodies
+def poly_box_case(B, T, seed=0, octagons=False):
+    make = lambda: poly_box_bodies(octagons)  # noqa: E731
     base = np.array([b.dyn() for b in make()], np.float32)
     rng = np.random.default_rng(seed)
     S0 = np.repeat(base[None], B, axis=0)

@@ -615,6 +615,38 @@ def test_rollout_grad_lunar_vs_oracle(torch_cuda):
     assert np.abs(gd).max() > 1.0
 
 
+def test_rollout_grad_lunar_settled_full_size_sampled(torch_cuda):
+    """The bench's grad_lunar workload at full size: 4096 LunarLanders settled
+    on the terrain (2560 driver steps), a 32-step rollout with the lander's
+    per-step dv, 8 envs sampled across the batch against the VJP oracle
+    started from the same GPU state and keys (returns bit-exact)."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    from cotix_oracle import physics as P
+    from cotix_oracle import prng
+    B, T = 4096, 32
+    ll = pa.LunarLander(batch=B)
+    st = pa._ffi.STAGES_LUNAR | pa._ffi.STAGE_BROADPHASE
+    for _ in range(40):
+        ll.world.step(64, 1e-2, st)
+    S0 = ll.world.dyn.permute(2, 0, 1).contiguous().cpu().numpy()
+    keys = ll.world.keys.cpu().numpy().view(np.uint32)
+    rng = np.random.default_rng(3)
+    actions = (rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32)
+    w = np.zeros(24, np.float32)
+    w[0] = 1.0
+    acts = torch.tensor(actions, device="cuda")
+    ret, saved = pa.rollout_forward(ll.world, acts, 0, w, stages=st)
+    ga, gd = pa.rollout_backward(ll.world, saved, want_dyn0=True)
+    ret, ga, gd = ret.cpu().numpy(), ga.cpu().numpy(), gd.cpu().numpy()
+    assert np.isfinite(ga).all(axis=(0, 2)).mean() > 0.9
+    envs = list(range(0, B, B // 8))
+    case = dict(make=lambda: P.lunar_lander_bodies(prng.PRNGKey(0)), S0=S0[envs], keys=keys[envs],
+                actions=actions[:, envs], w=w, ab=0, step=P.lunar_lander_step)
+    _check_grad_vs_oracle(case, ret[envs], ga[:, envs], gd[:, :, envs])
+
+
 def test_rollout_grad_polygon_box_vs_oracle(torch_cuda):
     """AABB x polygon and polygon x polygon contacts of rotating polygons."""
     torch = torch_cuda

@@ -169,10 +169,12 @@ def test_emu_rollout_lunar(emu_lib, E):
     assert np.abs(gd[:, :, :]).max() > 1.0
 
 
-def test_emu_rollout_poly_box(emu_lib):
-    """AABB x polygon and polygon x polygon contacts of two rotating polygons."""
+@pytest.mark.parametrize("octagons", [False, True])
+def test_emu_rollout_poly_box(emu_lib, octagons):
+    """AABB x polygon and polygon x polygon contacts of two rotating polygons
+    (octagons: the 80-term contact_from_edges pairs)."""
     emu, lib = emu_lib
-    case = GC.poly_box_case(6, 10, seed=0)
+    case = GC.poly_box_case(6, 10, seed=0, octagons=octagons)
     ret, ga, gd = _emu_run_st(emu, lib, case, 1 | 4 | 16)
     _check_vs_oracle(case, ret, ga, gd)
 

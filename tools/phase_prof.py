@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "parallax_amd", "_lib", "libcotix_amd_prof.so")
 NAMES = ["load", "save", "A", "T", "B", "C0", "C0b", "C1", "C2", "C3", "D", "E", "ret", "store", "restore", "G",
          "adj", "F", "K", "E1", "R", "trace", "B0", "B1", "F0", "F1", "F2", "F3",
-         "TV0", "TV1", "TV2", "TV3", "J", "sub0", "sub1", "sub2", "sub3", "sub4", "sub5", "sub6", "sub7"]
+         "TV0", "TV1", "TV2", "TV3", "J", "GE", "sub0", "sub1", "sub2", "sub3", "sub4", "sub5", "sub6", "sub7"]
 
 
 def build():
@@ -63,10 +63,10 @@ def main():
                 scen.dyn_reset[i, 3] = -0.3
     ew = 4  # the profiling build carries the default tiling only (COTIX_EW4_ONLY)
     waves = (B + ew - 1) // ew
-    buf = (ctypes.c_ulonglong * 40)()
+    buf = (ctypes.c_ulonglong * 48)()
 
     def phases(steps):
-        n = f(buf, 40)
+        n = f(buf, 48)
         nph = NAMES.index("sub0")
         tot = sum(buf[q] for q in range(min(n, nph)))  # the sub-phase timers (nph..) overlap the phases
         return {"cycles_per_wave_step_total": tot / waves / steps,
@@ -76,18 +76,23 @@ def main():
     if a.mode == "grad":
         world = scen.world
         nb = len(world.bodies)
+        stages, ab = pa._ffi.STAGES_ROBOCUP, nb - 1
+        if a.scenario == "lunar":  # bench.py grad_lunar: settled on the terrain, the lander's dv and x
+            stages, ab = scen.stages, 0
+            for _ in range(40):
+                world.step(64, 1e-2, stages)
         dyn0, keys0 = world.dyn.clone(), world.keys.clone()
         gen = torch.Generator(device="cpu").manual_seed(1234)
         actions = (torch.randn(a.substeps, B, 2, generator=gen) * 0.1).to(dev)
-        w = pa.rollout.ball_x_weights(nb, nb - 1)
+        w = pa.rollout.ball_x_weights(nb, ab)
         fwd, bwd = [], []
         for it in range(a.warmup + a.launches):
             world.dyn.copy_(dyn0)
             world.keys.copy_(keys0)
             world.err.zero_()
             torch.cuda.synchronize()
-            f(buf, 40)
-            _, saved = pa.rollout_forward(world, actions, nb - 1, w)
+            f(buf, 48)
+            _, saved = pa.rollout_forward(world, actions, ab, w, stages=stages)
             torch.cuda.synchronize()
             pf = phases(a.substeps)
             pa.rollout_backward(world, saved)
@@ -103,7 +108,7 @@ def main():
     env.reset()
     for _ in range(a.warmup):
         env.step(a.substeps)
-    f(buf, 40)  # reset after warm-up
+    f(buf, 48)  # reset after warm-up
     for _ in range(a.launches):
         env.step(a.substeps)
     torch.cuda.synchronize()

@@ -685,16 +685,18 @@ def main_grad(a):
     dist, rank, world_size, dev = init_dist()
     import parallax_amd as pa
     B, T = a.envs, a.substeps
-    box = a.scenario == "box"
-    r = run_grad(pa, dev, B, T, a.steps, a.warmup, rank, world_size, dist, "box" if box else "robocup")
-    nb = 7 if box else 5
+    box, lunar = a.scenario == "box", a.scenario == "lunar"
+    r = run_grad(pa, dev, B, T, a.steps, a.warmup, rank, world_size, dist,
+                 "box" if box else ("lunar" if lunar else "robocup"))
+    nb = 7 if box else (4 if lunar else 5)
+    key = "grad_box" if box else ("grad_lunar" if lunar else "grad")
     # algorithmic HBM bytes of the backward launch per env-step: saved state
     # (nb x 6 f32) + key (2 u32) + action (2 f32) read, grad_action (2 f32) written
     bwd_bytes = (nb * 6 * 4 + 8 + 8 + 8) * B * T
     achieved = bwd_bytes / (r["bwd_ms"] * 1e-3) / 1e9
     out = {
         "metric": "differentiable %d-step %s rollout, %d envs/GPU: env-steps/s with d(return)/d(action)"
-                  % (T, "box-world" if box else "RoboCup", B),
+                  % (T, "box-world" if box else ("LunarLander" if lunar else "RoboCup"), B),
         "value": r["value"],
         "unit": "env-steps/s",
         "n_gpus": world_size,
@@ -706,12 +708,16 @@ def main_grad(a):
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (%s; actions N(0, 0.1^2) per step)"
-                % ("box world, per-env random balls" if box else "RoboCup scene, per-env ball perturbation"),
+                % ("box world, per-env random balls" if box else
+                   ("LunarLander settled on its terrain after 2560 steps" if lunar else
+                    "RoboCup scene, per-env ball perturbation")),
         "config": {
             "workload": ("BoxWorld %d envs/GPU, %d-step rollout, grad of sum_t x of the last ball w.r.t. its "
                          "per-step dv (config 5 on a finite scene)" if box else
-                         "RoboCup (cotix/_robocup.py) %d envs/GPU, %d-step rollout, grad of sum_t ball x "
-                         "w.r.t. per-step ball dv (BASELINE config 5)") % (B, T),
+                         ("LunarLander %d envs/GPU settled on the terrain, %d-step rollout, grad of sum_t lander "
+                          "x w.r.t. the lander's per-step dv (GJK/EPA contacts and joints)" if lunar else
+                          "RoboCup (cotix/_robocup.py) %d envs/GPU, %d-step rollout, grad of sum_t ball x "
+                          "w.r.t. per-step ball dv (BASELINE config 5)")) % (B, T),
             "envs_per_gpu": B,
             "rollout_steps": T,
             "fwd_ms": r["fwd_ms"],
@@ -735,13 +741,13 @@ def main_grad(a):
             "note": "VALU/latency-bound (the backward re-plays each step's forward)",
         },
     }
-    v = grad_valu("grad_box" if box else "grad", B, T, r["fwd_ms"], r["bwd_ms"])
+    v = grad_valu(key, B, T, r["fwd_ms"], r["bwd_ms"])
     if v is None:
         out["roofline"]["frac_note"] = "no committed PMC pass of this build and workload: frac left null"
     else:
         out["roofline"].update(achieved=v["bwd"]["achieved"], frac=v["bwd"]["frac"], traffic=v["bwd"]["traffic"],
                                fwd=v["fwd"], traffic_source=v["source"])
-    if rank == 0 and world_size == 1 and a.cpu_baseline == "auto":
+    if rank == 0 and world_size == 1 and a.cpu_baseline == "auto" and not lunar:
         out["cpu_baseline"] = cpu_baseline_grad(T, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

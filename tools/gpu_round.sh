@@ -19,7 +19,8 @@ fi
 # driver steps 2560-3200, the stretch of the bench line's lunar_contact figure)
 ALL=("robocup:--scenario robocup --warmup 2" "lunar:--scenario lunar --warmup 2" \
      "lunar_contact:--scenario lunar --warmup 40" "box:--scenario box --warmup 2" \
-     "grad:--mode grad --scenario robocup --warmup 1" "grad_box:--mode grad --scenario box --warmup 1")
+     "grad:--mode grad --scenario robocup --warmup 1" "grad_box:--mode grad --scenario box --warmup 1" \
+     "grad_lunar:--mode grad --scenario lunar --warmup 1")
 for wl in "${ALL[@]}"; do
   sc=${wl%%:*}
   [ -n "$WLS" ] && [[ " $WLS " != *" $sc "* ]] && continue  # WLS: a subset of the workloads
@@ -36,5 +37,5 @@ for wl in "${ALL[@]}"; do
   echo "profile $sc ok"
 done
 if [ "${PHASES:-1}" = 1 ]; then
-timeout -k 10 200 python tools/phase_prof.py > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --scenario lunar > $O/phase_lunar.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario box --launches 3 > $O/phase_grad_box.json && echo "phase ok"
+timeout -k 10 200 python tools/phase_prof.py > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --scenario lunar > $O/phase_lunar.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario box --launches 3 > $O/phase_grad_box.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario lunar --launches 3 > $O/phase_grad_lunar.json && echo "phase ok"
 fi

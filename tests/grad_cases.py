@@ -125,6 +125,36 @@ def poly_box_case(B, T, seed=0, octagons=False):
     return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=2, step=P.robocup_step)
 
 
+def quad_row_case(B, T, seed=0):
+    """Nine Polygon4 bodies (one contact-type key): a static floor quad and a
+    row of eight touching boxes on it -- 24 * nb words exceed the key window,
+    so the backward does the GJK/EPA contact VJPs inside its serial chain."""
+    from cotix_oracle import geometry as Gm
+
+    def make():
+        floor = P.Body([Gm.Polygon([(-6, -1), (6, -1), (6, 0), (-6, 0)], kind="Polygon4")], mass=np.inf,
+                       inertia=np.inf, elasticity=0.2, friction_coefficient=0.5)
+        out = [floor]
+        for q in range(8):
+            sq = Gm.Polygon([(-0.25, -0.25), (0.25, -0.25), (0.25, 0.25), (-0.25, 0.25)], kind="Polygon4")
+            out.append(P.Body([sq], mass=1.0, inertia=0.04, position=(-2.0 + 0.49 * q, 0.24), angle=0.02 * q,
+                              elasticity=0.4, friction_coefficient=0.3))
+        return out
+    base = np.array([b.dyn() for b in make()], np.float32)
+    rng = np.random.default_rng(seed)
+    S0 = np.repeat(base[None], B, axis=0)
+    for e in range(B):
+        for b in range(1, 9):
+            S0[e, b, 2:4] = rng.uniform(-0.3, 0.3, 2)
+            S0[e, b, 5] = rng.uniform(-0.5, 0.5)
+    keys = np.asarray(prng.split(prng.PRNGKey(41 + seed), B), np.uint32)
+    actions = (rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32)
+    w = np.zeros(9 * 6, np.float32)
+    w[4 * 6 + 0] = 1.0
+    w[5 * 6 + 4] = 0.5
+    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=4, step=P.robocup_step)
+
+
 def oracle(case, envs=None):
     """Per env: (ret, grad_actions [T,2], grad_S0 [nb,6]) from the torch VJP chain."""
     B = case["S0"].shape[0]

@@ -657,6 +657,16 @@ def test_rollout_grad_polygon_box_vs_oracle(torch_cuda):
     _check_grad_vs_oracle(case, ret, ga, gd)
 
 
+def test_rollout_grad_quad_row_vs_oracle(torch_cuda):
+    """Nine polygons of one contact type: the contact VJPs inside phase G."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    case = GC.quad_row_case(8, 6, seed=0)
+    _, ret, ga, gd, _ = _gpu_rollout(torch, case, _pa_bodies(pa, case["make"]()))
+    _check_grad_vs_oracle(case, ret, ga, gd)
+
+
 def test_rollout_grad_robocup_vs_oracle(torch_cuda):
     torch = torch_cuda
     import parallax_amd as pa

@@ -179,6 +179,15 @@ def test_emu_rollout_poly_box(emu_lib, octagons):
     _check_vs_oracle(case, ret, ga, gd)
 
 
+def test_emu_rollout_quad_row(emu_lib):
+    """Nine polygons of one contact type: the contact VJPs inside phase G's
+    chain (no room for phase GE's responses in the key window)."""
+    emu, lib = emu_lib
+    case = GC.quad_row_case(4, 6, seed=0)
+    ret, ga, gd = _emu_run_st(emu, lib, case, 1 | 4 | 16)
+    _check_vs_oracle(case, ret, ga, gd)
+
+
 def test_backward_rejects_circle_polygon_and_analytic_joints(emu_lib):
     """Circle x polygon contacts are not differentiated (EPA's circle supports
     chain through every iteration); the joint stage needs the polygon program."""

@@ -538,11 +538,13 @@ def test_config1_lunar_single_env_10000_steps_vs_cport(torch_cuda, cport_lib):
 # ---------------------------------------------------------------------------
 # differentiable rollout (BASELINE config 5)
 # ---------------------------------------------------------------------------
-def _gpu_rollout(torch, case, bodies_pa, want_dyn0=True, stages=None, world=None):
+def _gpu_rollout(torch, case, bodies_pa, want_dyn0=True, stages=None, world=None, envs_per_wave=0):
     import parallax_amd as pa
     B = case["S0"].shape[0]
     keys = torch.tensor(u32_to_i32(case["keys"]), device="cuda")
     w = pa.World(bodies_pa, B, "cuda", keys) if world is None else world
+    if envs_per_wave:
+        w.set_variant(envs_per_wave)
     if world is not None:
         w.keys.copy_(keys)
     w.dyn.copy_(torch.tensor(case["S0"], device="cuda").permute(1, 2, 0))
@@ -658,12 +660,13 @@ def test_rollout_grad_polygon_box_vs_oracle(torch_cuda):
 
 
 def test_rollout_grad_quad_row_vs_oracle(torch_cuda):
-    """Nine polygons of one contact type: the contact VJPs inside phase G."""
+    """Nine polygons of one contact type: the contact VJPs inside phase G
+    (one env per wave: the scene's tile exceeds the LDS at the default four)."""
     torch = torch_cuda
     import parallax_amd as pa
     import grad_cases as GC
     case = GC.quad_row_case(8, 6, seed=0)
-    _, ret, ga, gd, _ = _gpu_rollout(torch, case, _pa_bodies(pa, case["make"]()))
+    _, ret, ga, gd, _ = _gpu_rollout(torch, case, _pa_bodies(pa, case["make"]()), envs_per_wave=1)
     _check_grad_vs_oracle(case, ret, ga, gd)
 
 

@@ -109,3 +109,24 @@ def test_asan_box_world_rollout_backward(emu_mod, tmp_path, E):
     ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, 21, case["actions"], case["ab"], case["w"], E=E)
     want = np.concatenate([x.reshape(-1).view(np.uint8) for x in (d, k, err, ret, ga, gd)])
     assert np.array_equal(raw, want)
+
+
+@pytest.mark.parametrize("scene", ["lunar", "poly_box"])
+def test_asan_polygon_rollout_backward(emu_mod, tmp_path, scene):
+    """The polygon gradients (phase GE's GJK/EPA contact VJPs, the joints in
+    phase G) under the sanitizers."""
+    emu, lib = emu_mod
+    if scene == "lunar":
+        case, stages = GC.lunar_case(4, 8, seed=1), 1 | 2 | 4 | 8 | 16 | 32
+    else:
+        case, stages = GC.poly_box_case(4, 8, seed=1), 1 | 4 | 16
+    B, T = case["S0"].shape[0], case["actions"].shape[0]
+    dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
+    raw, _ = _run_driver(tmp_path, case["make"](), dyn, case["keys"], T, stages, 4, mode=1,
+                         actions=case["actions"], ab=case["ab"], w=case["w"])
+    h, geom = emu.oracle_scene(lib, case["make"]())
+    d, k, err = dyn.copy(), np.array(case["keys"], np.uint32, copy=True), np.zeros(B, np.uint32)
+    ret, sd, sk = emu.rollout(lib, h, d, k, err, geom, 0, stages, case["actions"], case["ab"], case["w"], E=4)
+    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, stages, case["actions"], case["ab"], case["w"], E=4)
+    want = np.concatenate([x.reshape(-1).view(np.uint8) for x in (d, k, err, ret, ga, gd)])
+    assert np.array_equal(raw, want)

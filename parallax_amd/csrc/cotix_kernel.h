@@ -2533,10 +2533,52 @@ CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e) {
 #ifdef COTIX_STATS
 CX_DEV int L_rp_(const Ctx& c) { return c.L.rp; }
 #endif
+// the rollout's return terms (stage_ret_terms' compact list, launch
+// constants) in the registers of the env's lane, read once per launch
+constexpr int RT = 8;
+CX_DEV int ret_terms_cap(const Ctx& c) {
+  const int cap = (c.nb * 6 - 1) / 2;
+  return cap < RT ? cap : RT;
+}
+struct RetRegs {
+  int n = 0;
+  int k[RT];
+  float w[RT];
+};
+template <int EW>
+CX_DEV void ret_fetch(const Ctx& c, Tile<EW> t, int lane, RetRegs& r) {
+  const int e = lane < EW ? lane : 0;
+  r.n = (int)t.w(c.L.rst, e);
+#pragma unroll
+  for (int j = 0; j < RT; ++j) {
+    r.k[j] = j < r.n ? (int)t.w(c.L.rst + 1 + 2 * j, e) : 0;
+    r.w[j] = j < r.n ? t.f(c.L.rst + 2 + 2 * j, e) : 0.0f;
+  }
+}
+// return accumulation after a step (env e's lane): ret += sum_k w_k * state_k
+// (w_k != 0), k ascending
+template <int EW>
+CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const RetRegs& r) {
+  float acc = t.f(c.L.ret, e);
+  if (r.n <= ret_terms_cap(c)) {
+    float sv[RT];
+#pragma unroll
+    for (int j = 0; j < RT; ++j) sv[j] = t.f(c.L.dyn + r.k[j], e);
+#pragma unroll
+    for (int j = 0; j < RT; ++j) acc = j < r.n ? acc + r.w[j] * sv[j] : acc;
+  } else {  // more terms than the list holds: every weight from the kernel arguments
+    for (int k = 0; k < c.nb * 6; ++k)
+      if (a.ret_w[k] != 0.0f) acc = acc + a.ret_w[k] * t.f(c.L.dyn + k, e);
+  }
+  t.f(c.L.ret, e) = acc;
+}
+
 // REC (backward re-play only): record, per resolution, whether the impulses
 // were applied and the pre-resolution velocities of the two bodies.
-template <int EW, bool REC = false>
-CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso) {
+// RET (rollout forward): the return accumulation after the step, on the
+// env's lane (ret_accum), in the same phase.
+template <int EW, bool REC = false, bool RET = false>
+CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso, const RetRegs* rr = nullptr) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int nb = c.nb;
@@ -2616,6 +2658,7 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
       t.w(L.err, e) = 0u;
       t.w(L.nres, e) = t.w(L.nres, e) + r;
     }
+    if (RET) ret_accum<EW>(a, c, t, e, *rr);  // (the rollout never restarts: after phase R's place)
   }
 }
 
@@ -2817,14 +2860,9 @@ CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
 // The forward's return sums only the nonzero terms, compacted in k order
 // (ballots): word 0 the count n, then (k, w) pairs -- two LDS round trips per
 // step for up to RT terms (the return of config 5 has one).
-constexpr int RT = 8;
 template <int EW>
 CX_DEV void stage_ret_w(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) {
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) t.f(c.L.rst + w / EW, w % EW) = a.ret_w[w / EW];
-}
-CX_DEV int ret_terms_cap(const Ctx& c) {
-  const int cap = (c.nb * 6 - 1) / 2;
-  return cap < RT ? cap : RT;
 }
 template <int EW>
 CX_DEV void stage_ret_terms(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) {
@@ -2847,33 +2885,6 @@ CX_DEV void stage_ret_terms(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) 
   }
   if (lane < EW) t.w(c.L.rst, lane) = (uint32_t)n;
 }
-// return accumulation after a step: ret += sum_k w_k * state_k (w_k != 0), k ascending
-template <int EW>
-CX_DEV void ph_ret(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
-  for (int e = lane; e < EW; e += WAVE) {
-    if (env0 + e >= a.B) continue;
-    float acc = t.f(c.L.ret, e);
-    const int n = (int)t.w(c.L.rst, e);
-    if (n <= ret_terms_cap(c)) {
-      int kk[RT];
-      float ww[RT], sv[RT];
-#pragma unroll
-      for (int j = 0; j < RT; ++j) {
-        kk[j] = j < n ? (int)t.w(c.L.rst + 1 + 2 * j, e) : 0;
-        ww[j] = j < n ? t.f(c.L.rst + 2 + 2 * j, e) : 0.0f;
-      }
-#pragma unroll
-      for (int j = 0; j < RT; ++j) sv[j] = t.f(c.L.dyn + kk[j], e);
-#pragma unroll
-      for (int j = 0; j < RT; ++j) acc = j < n ? acc + ww[j] * sv[j] : acc;
-    } else {  // more terms than the list holds: every weight from the kernel arguments
-      for (int k = 0; k < c.nb * 6; ++k)
-        if (a.ret_w[k] != 0.0f) acc = acc + a.ret_w[k] * t.f(c.L.dyn + k, e);
-    }
-    t.f(c.L.ret, e) = acc;
-  }
-}
-
 // backward: the saved state of step `step`, read into registers one step
 // ahead (restore_fetch in the previous step's restore phase), so the global
 // reads are in flight while that step re-plays and differentiates
@@ -3364,6 +3375,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   MConst mc;  // the fused scan's launch-constant owner words
   if ((a.stages & COTIX_STAGE_COLLIDER) && c.nl > 0 && c.nl * EW <= 2 * WAVE)
     run(PH_C1, [&](int l) { mc_fetch<EW>(c, t, l, mc); });
+  RetRegs rr;  // the rollout's return terms
+  if (ROLL) run(PH_RET, [&](int l) { ret_fetch<EW>(c, t, l, rr); });
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
@@ -3405,10 +3418,14 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {
-      run(PH_E1, [&](int l) { ph_E<EW>(a, c, t, env0, l, kso); });
+      run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
       if (a.dyn_reset != nullptr && a.reset_mode == 1) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
+    } else if (ROLL) {
+      run(PH_RET, [&](int l) {
+        for (int e = l; e < EW; e += WAVE)
+          if (env0 + e < a.B) ret_accum<EW>(a, c, t, e, rr);
+      });
     }
-    if (ROLL) run(PH_RET, [&](int l) { ph_ret<EW>(a, c, t, env0, l); });
     if (EVAL && a.judge.on) {  // cotix_eval: NFE bookkeeping (cotix/_envs.py:77-117)
       run(PH_J, [&](int l) { ph_J<EW>(a, c, t, env0, l); });
       run(PH_J, [&](int l) { ph_JS<EW>(c, t, l); });

@@ -157,14 +157,19 @@ int cotix_scene_geom_floats(const cotix_scene* scene);
 /* introspection for tests: counts of distinct contacts / cells / candidates / type keys */
 int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, int* n_candidates, int* n_types);
 /* Kernel variant of the scene's launches (no reference counterpart: a tiling
- * choice; every variant computes the same bits).  envs_per_wave: 0 (default,
- * 4) | 1 | 2 | 4 | 8; specialize: 1 (default) lets the two reference scenes
+ * choice; every variant computes the same bits).  envs_per_wave: 0 (the
+ * scene's default) | 1 | 2 | 4 | 8; specialize: 1 (default) lets the two reference scenes
  * under the default constants use kernels with their whole scene header as a
  * compile-time constant, 0 forces the generic kernel.
  * cotix_scene_variant reports what a step launch uses: the tiling and the
  * specialization id (0 generic, 1 RoboCup, 2 LunarLander, 3 RoboCup and 4
  * LunarLander in the partitionable PRNG layout, 5 the box world's structure:
- * 3 AABB walls and 4 circles, legacy layout). */
+ * 3 AABB walls and 4 circles, legacy layout).
+ * The tiling is a scene property: cotix_scene_create(_ex) sets the default to
+ * 4 envs per wave, or the largest of 2 and 1 whose workgroup (the hot tables
+ * + 4 wave tiles and scratches) fits the CU's 160 KiB of LDS, and rejects a
+ * scene that fits at no tiling (the message gives the bytes);
+ * cotix_scene_set_variant rejects an explicit tiling that does not fit. */
 int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specialize);
 int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec);
 
@@ -310,6 +315,27 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
                            int geom_stride, int B, int n_steps, float dt, int stages, const float* action,
                            int action_body, const float* ret_weights, float* grad_action, float* grad_dyn0,
                            cotix_stream_t stream);
+/* The same with the forward's decision tape (no reference counterpart: the
+ * saved outcome of the forward's discrete work).  cotix_rollout_ex also writes
+ *   tape device u32 [n_steps][cotix_rollout_tape_words(scene)][B] (nullable):
+ *        per step and body the resolution RandomizedCollider.resolve applied
+ *        (cotix/_colliders.py:274-336: the chosen partner j*, the contact of
+ *        cell (i, j*)) and, in polygon scenes, the final EPA edge of every
+ *        contact EPA ran for (cotix/_collisions.py:115-273)
+ * and cotix_rollout_backward_ex, given that tape (nullable: the re-play of
+ * cotix_rollout_backward), restores those decisions instead of re-running the
+ * key splits, the narrowphase, the RNG scan and the choice, and starts the
+ * VJP of a GJK/EPA contact from the recorded edge.  The gradients are
+ * bit-identical to the re-play's. */
+int cotix_rollout_tape_words(const cotix_scene* scene);
+int cotix_rollout_ex(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
+                     int geom_stride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                     const float* ret_weights, float* ret, float* saved_dyn, uint32_t* saved_keys, uint32_t* tape,
+                     cotix_stream_t stream);
+int cotix_rollout_backward_ex(cotix_scene* scene, const float* saved_dyn, const uint32_t* saved_keys,
+                              const uint32_t* tape, const float* geom, int geom_stride, int B, int n_steps, float dt,
+                              int stages, const float* action, int action_body, const float* ret_weights,
+                              float* grad_action, float* grad_dyn0, cotix_stream_t stream);
 
 /* Body-level operators (UniversalShape, cotix/_universal_shape.py:87-132), per env:
  * cotix_body_penetration: collides_with (GJK over every part pair of the two

@@ -5,7 +5,7 @@ mirroring the reference's body/shape/operator surface.
 """
 from . import _ffi  # noqa: F401  (raises ImportError when the HIP library is missing)
 from . import random  # noqa: F401
-from . import contracts, render  # noqa: F401
+from . import contracts, pytree, render  # noqa: F401
 from .bodies import AnyBody, BodyView  # noqa: F401
 from .env import BatchedEnv, StepResult  # noqa: F401
 from .envs import (AbstractEnvironment, AffineControl, LinearJudge, PhysicsWorld, VelocityImpulse,  # noqa: F401

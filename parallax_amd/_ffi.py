@@ -57,6 +57,9 @@ SIGNATURES = {
                         ctypes.POINTER(CotixControl), _P, _I, _P, _P, _I, _P, _P, _P, _P]),
     "cotix_rollout": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P, _P]),
     "cotix_rollout_backward": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P]),
+    "cotix_rollout_tape_words": (_I, [_P]),
+    "cotix_rollout_ex": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "cotix_rollout_backward_ex": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P, _P, _P, _P]),
     "cotix_body_penetration": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cotix_body_aabb": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "cotix_physics_euler": (_I, [_P, _I, _I, _F, _P]),

@@ -987,9 +987,11 @@ static __device__ unsigned long long g_dev_sub[4];  // phase-timing build: GJK /
 #define CX_CLOCK() 0ull
 #define CX_DSUB_ADD(k, t0) ((void)(t0))
 #endif
+// edge (nullable): EPA's final edge (e0, e1), when EPA ran (the rollout
+// forward records it for the backward's VJP, cotix_grad.h)
 template <class SA, class SB, class MakeStore>
 CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen,
-                      v2* pen, MakeStore make) {
+                      v2* pen, MakeStore make, v2* edge = nullptr) {
   static_assert(2 * MAXV + 1 + 3 <= 20, "EPA buffer bound");
   v2 simplex[3];
   *pen = v2{0.0f, 0.0f};
@@ -1011,20 +1013,27 @@ CX_DEV bool gjk_epa_t(const SA& a, const SB& b, const Shape& A, const Shape& B, 
     unsigned long long t0;
     CX_MF ~EpaTimer() { CX_DSUB_ADD(1, t0); }
   } cx_epa_timer{cx_epa_t0};
+  v2 e0, e1;  // epa() = epa_edge + its closest point
   if (iters + 3 <= 14) {
     auto es = make.template get<14>();
-    *pen = epa<14, decltype(es)>(a, b, simplex, iters, es);
+    epa_edge<14, decltype(es)>(a, b, simplex, iters, es, &e0, &e1);
   } else {
     auto es = make.template get<20>();
-    *pen = epa<20, decltype(es)>(a, b, simplex, iters, es);
+    epa_edge<20, decltype(es)>(a, b, simplex, iters, es, &e0, &e1);
+  }
+  *pen = closest_on_edge_to_origin(e0, e1);
+  if (edge != nullptr) {
+    edge[0] = e0;
+    edge[1] = e1;
   }
   return true;
 }
 // POLY: both shapes are polygons (supports without the kind dispatch)
 template <bool POLY, class MakeStore>
-CX_DEV bool gjk_epa(const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen, v2* pen, MakeStore make) {
-  if constexpr (POLY) return gjk_epa_t(PolyRef{A}, PolyRef{B}, A, B, np, need_pen, pen, make);
-  else return gjk_epa_t(A, B, A, B, np, need_pen, pen, make);
+CX_DEV bool gjk_epa(const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen, v2* pen, MakeStore make,
+                    v2* edge = nullptr) {
+  if constexpr (POLY) return gjk_epa_t(PolyRef{A}, PolyRef{B}, A, B, np, need_pen, pen, make, edge);
+  else return gjk_epa_t(A, B, A, B, np, need_pen, pen, make, edge);
 }
 struct MakeRegs {
   template <int NE>
@@ -1044,8 +1053,8 @@ CX_DEV bool convex_vs_polygon_pen(const Shape& A, const Shape& B, const NarrowPa
 // (POLY: both shapes are polygons)
 template <bool POLY>
 CX_DEV bool convex_vs_polygon_pen_col(const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen, v2* pen,
-                                      float* col, int stride) {
-  return gjk_epa<POLY>(A, B, np, need_pen, pen, MakeCol{col, stride});
+                                      float* col, int stride, v2* edge = nullptr) {
+  return gjk_epa<POLY>(A, B, np, need_pen, pen, MakeCol{col, stride}, edge);
 }
 CX_DEV Contact convex_vs_polygon(const Shape& A, const Shape& B, const NarrowParams& np, bool need_pen = true) {
   Contact c;

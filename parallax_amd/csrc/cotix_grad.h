@@ -355,6 +355,19 @@ CX_DEV void convex_contact_vjp(const Shape& A, const Shape& B, const NarrowParam
   }
   if (gcp.x != 0.0f || gcp.y != 0.0f) contact_from_edges_vjp(A, B, gcp, ga, gb);
 }
+// the same from EPA's final edge (e0, e1) as the forward recorded it (the
+// rollout's tape, cotix_kernel.h): no GJK / EPA re-run -- the edge is the one
+// convex_contact_vjp's re-run would find (the same code on the same shapes)
+CX_DEV void convex_contact_vjp_edge(const Shape& A, const Shape& B, v2 e0, v2 e1, v2 gpen, v2 gcp, VGrad& ga,
+                                    VGrad& gb) {
+  if (gpen.x != 0.0f || gpen.y != 0.0f) {
+    v2 g0 = v2{0.0f, 0.0f}, g1 = v2{0.0f, 0.0f};
+    closest_vjp(e0, e1, gpen, &g0, &g1);
+    minkowski_vjp(A, B, e0, g0, ga, gb);
+    minkowski_vjp(A, B, e1, g1, ga, gb);
+  }
+  if (gcp.x != 0.0f || gcp.y != 0.0f) contact_from_edges_vjp(A, B, gcp, ga, gb);
+}
 
 // ---------------------------------------------------------------------------
 // LunarLander joints (LunarLander.step, cotix/_lunar_lander.py:176-212; the

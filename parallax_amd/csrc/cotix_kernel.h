@@ -228,6 +228,11 @@ struct KArgs {
   float* grad_action;      // backward: [n_steps][B][2] d ret / d action
   float* grad_dyn;         // backward: [nb*6][B] d ret / d initial state, or null
   float ret_w[MAXB * 6];
+  // the rollout's decision tape (cotix_rollout_ex / cotix_rollout_backward_ex;
+  // null = off): [n_steps][tw][B] words, written by the forward, read by the
+  // backward instead of re-playing the collider (tape_words below)
+  uint32_t* tape;
+  int tw;
   // cotix_eval (AbstractEnvironment.eval, cotix/_envs.py:37-132, fused):
   int reset_mode;          // 1: restart on error bits after a step (dyn_reset); 2: restart envs finished at entry
   int action_held;         // 1: action is [B][2], the same impulse every step (a held control signal)
@@ -237,6 +242,27 @@ struct KArgs {
   int nfe_len;             // env-steps per NFE (WFE_scale); n_steps is a multiple of it (judge on)
   JudgeArgs judge;         // device AbstractJudge (judge.on == 0: off)
   CtlArgs ctl;             // device AbstractControl (ctl.on == 0: off)
+};
+
+// The rollout's decision tape, per env-step (word w of step s, env g at
+// tape[(s * tw + w) * B + g]):
+//   5 i        body i's resolution (cotix/_colliders.py:310-336): its partner
+//              j* | the distinct contact id of cell (i, j*) << 8, or RP_NONE
+//              when the body resolves nothing this step
+//   5 i + 1..4 that contact (pen.x, pen.y, cp.x, cp.y) -- written only for a
+//              resolution
+//   5 nb + 4 c (polygon scenes) EPA's final edge (e0, e1) of distinct contact
+//              c, written by phase B when EPA ran for it
+// Every value is the forward's own; the backward (MODE 4) restores them
+// instead of re-running the key splits, the narrowphase, the RNG scan and the
+// choice, and the VJP of a GJK/EPA contact starts from the recorded edge.
+CX_HD int tape_words(int nb, int nc, int poly) { return 5 * nb + (poly ? 4 * nc : 0); }
+// the backward's tape words in registers (tape_fetch): per (body, env) item
+// its resolution word + contact, and the recorded EPA edge
+constexpr int TQ = (MAXB * 8 + WAVE - 1) / WAVE;  // items per lane: nb * EW over 64 lanes (EW <= 8)
+struct TapeRegs {
+  uint32_t d[TQ][5];
+  float ed[TQ][4];
 };
 
 // per-wave tile layout (words, each x EW envs)
@@ -404,11 +430,11 @@ CX_DEV void lunar_constraints(cx::Dyn& lander, cx::Dyn& rleg, cx::Dyn& lleg, con
 enum : int { FNS_ANALYTIC = 1, FNS_CONVEX = 2, FNS_CIRCLE_POLY = 4, FNS_AABB_POLY = 8 };
 // the FNSET instantiation of the step kernel for a scene's function set
 // (launcher and host emulation): analytic scenes get the analytic program,
-// modes 1 (rollout), 2 (its backward) and 3 (eval with a judge or control) the
-// full one
+// modes 1 (rollout), 2 / 4 (its backward: re-play / tape) and 3 (eval with a
+// judge or control) the full one
 CX_HD int launch_fnset(int fs, int mode) {
   if ((fs & ~FNS_ANALYTIC) == 0) return FNS_ANALYTIC;
-  if (mode == 1 || mode == 2 || mode == 3) return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
+  if (mode >= 1 && mode <= 4) return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
   if ((fs & ~(FNS_ANALYTIC | FNS_CONVEX)) == 0) return FNS_ANALYTIC | FNS_CONVEX;
   if ((fs & FNS_CIRCLE_POLY) == 0) return FNS_ANALYTIC | FNS_CONVEX | FNS_AABB_POLY;
   return FNS_ANALYTIC | FNS_CONVEX | FNS_CIRCLE_POLY | FNS_AABB_POLY;
@@ -1191,8 +1217,10 @@ CX_DEV bool self_cp_finite(const cx::Shape& P) {
   return ok & any;
 }
 
-template <int EW, int FNSET>
-CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int w) {
+// TAPE (rollout forward with a tape): EPA's final edge of the item to the
+// tape (step `step`)
+template <int EW, int FNSET, bool TAPE = false>
+CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int w, int step = 0) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const NarrowParams np = narrow_of(sc);
@@ -1222,10 +1250,17 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
       // GJK (+EPA); the contact point is deferred to phase F (wave-cooperative)
       const bool self = ((d0w >> 27) & 1u) != 0u;
       float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
+      v2 edge[2];
       const bool hit = CXK_SKIP(a, 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
                        : (FNSET & FNS_AABB_POLY) == 0
-                           ? convex_vs_polygon_pen_col<true>(A, Bs, np, !self, &ct.pen, col, WAVE)
-                           : convex_vs_polygon_pen_col<false>(A, Bs, np, !self, &ct.pen, col, WAVE);
+                           ? convex_vs_polygon_pen_col<true>(A, Bs, np, !self, &ct.pen, col, WAVE, TAPE ? edge : nullptr)
+                           : convex_vs_polygon_pen_col<false>(A, Bs, np, !self, &ct.pen, col, WAVE, TAPE ? edge : nullptr);
+      if (TAPE && a.tape != nullptr && hit && !self) {  // (a tape only with the polygon words, tape_words)
+        const int o = 5 * c.nb + 4 * ci;
+        const float ev[4] = {edge[0].x, edge[0].y, edge[1].x, edge[1].y};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a.tape[((size_t)step * a.tw + o + q) * a.B + g] = __float_as_uint(ev[q]);
+      }
       ct.cp = v2{qnan(), qnan()};
       // a part paired with itself: only the NaN-ness of its contact point is
       // observable (such a cell is only ever chosen as j == i, which
@@ -1484,15 +1519,15 @@ CX_DEV void ph_B_const(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int l
     ab_item<EW>(a, c, t, e, ci, r.dw[q], r.ga[q], r.gb[q], px[q][0][0], px[q][0][1], px[q][1][0], px[q][1][1]);
   }
 }
-template <int EW, int FNSET>
-CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+template <int EW, int FNSET, bool TAPE = false>
+CX_DEV void ph_B(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step = 0) {
   if constexpr (FNSET == FNS_ANALYTIC) {
     ph_B_analytic<EW>(a, c, t, env0, lane);
     return;
   }
   for (int w = lane; w < c.nc * EW; w += WAVE) {
     if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly) t.ws[c.W.cf_flag + w] = 0u;
-    b_item<EW, FNSET>(a, c, t, env0, lane, w);
+    b_item<EW, FNSET, TAPE>(a, c, t, env0, lane, w, step);
   }
 }
 
@@ -1792,8 +1827,8 @@ constexpr bool b_pairs() {
   return PAIR_GJK && FNSET == (FNS_ANALYTIC | FNS_CONVEX);
 }
 // item w on the lane pair (lane, lane ^ 1); h = lane & 1
-template <int EW, int FNSET>
-CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int w) {
+template <int EW, int FNSET, bool TAPE = false>
+CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int w, int step = 0) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int h = lane & 1;
@@ -1802,7 +1837,7 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
   const uint32_t d0w = t.tb[sc.o_cdesc + 2 * ci], d1w = t.tb[sc.o_cdesc + 2 * ci + 1];
   const int fn = (int)((d0w >> 20) & 7u);
   if (fn != FN_POLY_POLY) {  // (not in the reference scenes) the one-lane form on lane 0
-    if (h == 0) b_item<EW, FNSET>(a, c, t, env0, lane, w);
+    if (h == 0) b_item<EW, FNSET, TAPE>(a, c, t, env0, lane, w, step);
     return;
   }
   CXK_STAT(b_items, h == 0 ? 1 : 0);
@@ -1833,14 +1868,14 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
 // BP2: round r of the B list, one item per lane (lane pairs: b_pairs)
 // pairs: the step's mode (lane pairs pay off when EPA runs -- landers on the
 // terrain -- and cost a little on GJK-only lists, e.g. the self pairs in flight)
-template <int EW, int FNSET>
-CX_DEV void ph_BP2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int r, bool pairs) {
-  if (b_pairs<FNSET>() && pairs) {
+template <int EW, int FNSET, bool TAPE = false>
+CX_DEV void ph_BP2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int r, bool pairs, int step = 0) {
+  if (b_pairs<FNSET>() && pairs && !TAPE) {  // (the tape's edge words come from the one-lane form)
     const int k = r * (WAVE / 2) + (lane >> 1);
     if (k < (int)t.ws[c.W.bl_n]) b_item_pair<EW, FNSET>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k]);
   } else {
     const int k = r * WAVE + lane;
-    if (k < (int)t.ws[c.W.bl_n]) b_item<EW, FNSET>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k]);
+    if (k < (int)t.ws[c.W.bl_n]) b_item<EW, FNSET, TAPE>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k], step);
   }
 }
 
@@ -2395,6 +2430,46 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   }
 }
 
+// phase D of the backward with a tape (MODE 4): the forward's resolution of
+// body i -- partner, cell, contact, and for a GJK/EPA contact EPA's final
+// edge (into ge_edge's words, read by phase GE) -- from the tape registers,
+// then the resolution operands as phase D computes them (e0_item); the tile
+// words written are exactly those the re-play's phases B-D leave for E, GE
+// and G (the chosen cell's candidate word carries only its contact id, the
+// one field they read)
+CX_HD bool ge_edges_fit(const Ctx& c) { return 28 * c.nb <= KWIN * c.L.kww; }
+CX_DEV int ge_edge_word(const Ctx& c, int i) { return c.L.kw + 24 * c.nb + 4 * i; }
+template <int EW>
+CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, const TapeRegs& r) {
+  const Lay& L = c.L;
+  const int nb = c.nb, ni = nb * EW;
+  const bool edges = c.sh.poly && ge_edges_fit(c);
+#pragma unroll
+  for (int q = 0; q < TQ; ++q) {
+    if (q * WAVE >= ni) break;  // uniform
+    const int w = q * WAVE + lane, e = w % EW, i = w / EW;
+    if (w >= ni || env0 + e >= a.B) continue;
+    const uint32_t dec = r.d[q][0];
+    const bool res = dec != RP_NONE;
+    const int j = res ? (int)(dec & 255u) : i, cid = res ? (int)((dec >> 8) & 511u) : -1;
+    t.w(L.ch + i, e) = (uint32_t)j;
+    if (res) {
+      t.w(L.m + i * nb + j, e) = (uint32_t)cid << 18;
+      const int co = L.con + 4 * cid;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t.w(co + k, e) = r.d[q][k + 1];
+      if (edges) {
+        const int eo = ge_edge_word(c, i);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t.f(eo + k, e) = r.ed[q][k];
+      }
+    }
+    if (c.sh.rcp_all)
+      e0_item<EW, true>(c, t, e, i, j, cid);
+    else
+      e0_item<EW, false>(c, t, e, i, j, cid);
+  }
+}
 
 // phase E: sequential resolution (:310-336), joints, key update, restarts.
 // E0 (item = (body i, env), all lanes): everything of resolution i that does
@@ -2577,12 +2652,38 @@ CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const Ret
 // were applied and the pre-resolution velocities of the two bodies.
 // RET (rollout forward): the return accumulation after the step, on the
 // env's lane (ret_accum), in the same phase.
+// the rollout forward's tape words of step `step` (tape_words): per (body i,
+// env) item, on the lanes E1 leaves idle (lane >= EW), from phase D's
+// results -- disjoint from every word E1 touches
+template <int EW>
+CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+  const Lay& L = c.L;
+  const int nb = c.nb;
+  for (int w = lane - EW; w >= 0 && w < nb * EW; w += WAVE - EW) {
+    const int e = w % EW, i = w / EW, g = env0 + e;
+    if (g >= a.B) continue;
+    const uint32_t j = t.w(L.rp + RP_W * i + RP_J, e);
+    uint32_t* o = a.tape + ((size_t)step * a.tw + 5 * i) * a.B + g;
+    if (j == RP_NONE) {
+      o[0] = RP_NONE;
+      continue;
+    }
+    const uint32_t cid = (t.w(L.m + i * nb + (int)j, e) >> 18) & 511u;
+    const int co = L.con + 4 * (int)cid;
+    o[0] = j | (cid << 8);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[(size_t)(q + 1) * a.B] = t.w(co + q, e);
+  }
+}
+
 template <int EW, bool REC = false, bool RET = false>
-CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso, const RetRegs* rr = nullptr) {
+CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso, const RetRegs* rr = nullptr,
+                 int step = 0) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int nb = c.nb;
   const Lay& L = c.L;
+  if (RET && a.tape != nullptr && (a.stages & COTIX_STAGE_COLLIDER)) tape_save<EW>(a, c, t, env0, lane, step);
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g >= a.B) continue;
@@ -2924,6 +3025,39 @@ CX_DEV void restore_apply(const Ctx& c, Tile<EW> t, int lane, const RestoreRegs&
   }
 }
 
+// the backward's tape words of step `step` (MODE 4), read into registers one
+// step ahead like the saved state: per (body i, env) item (lane mapping of
+// phase D), the resolution word and its contact; the recorded EPA edge of the
+// resolution's contact (polygon scenes) is read once the step's resolution
+// words are current (tape_edge_fetch)
+template <int EW>
+CX_DEV void tape_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step, TapeRegs& r) {
+  const int ni = c.nb * EW;
+#pragma unroll
+  for (int q = 0; q < TQ; ++q) {
+    if (q * WAVE >= ni) break;  // uniform
+    const int w = q * WAVE + lane, e = w % EW, i = w / EW, g = env0 + e;
+    const bool ok = w < ni && g < a.B;
+    const uint32_t* p = a.tape + ((size_t)step * a.tw + 5 * (ok ? i : 0)) * a.B + (ok ? g : 0);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) r.d[q][k] = ok ? p[(size_t)k * a.B] : RP_NONE;
+  }
+}
+template <int EW>
+CX_DEV void tape_edge_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step, TapeRegs& r) {
+  const int ni = c.nb * EW;
+#pragma unroll
+  for (int q = 0; q < TQ; ++q) {
+    if (q * WAVE >= ni) break;  // uniform
+    const int w = q * WAVE + lane, g = env0 + w % EW;
+    const bool ok = w < ni && g < a.B && r.d[q][0] != RP_NONE;
+    const int cid = ok ? (int)((r.d[q][0] >> 8) & 511u) : 0;
+    const uint32_t* p = a.tape + ((size_t)step * a.tw + 5 * c.nb + 4 * cid) * a.B + (ok ? g : 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r.ed[q][k] = ok ? __uint_as_float(p[(size_t)k * a.B]) : 0.0f;
+  }
+}
+
 template <int EW>
 CX_DEV void ph_adj_init(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
@@ -3093,7 +3227,9 @@ template <int EW>
 CX_DEV int ge_word(const Ctx& c, int i, int k) {
   return c.L.kw + 24 * i + 6 * k;
 }
-template <int EW>
+// EDGES (MODE 4): EPA's final edge from the tape (ge_edge_word) instead of a
+// GJK + EPA re-run
+template <int EW, bool EDGES = false>
 CX_DEV void ph_GE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
@@ -3112,7 +3248,13 @@ CX_DEV void ph_GE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
     va.zero();
     vb.zero();
     const v2 gpen = v2{k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f}, gcp = v2{k == 2 ? 1.0f : 0.0f, k == 3 ? 1.0f : 0.0f};
-    convex_contact_vjp(WA, WB, narrow_of(sc), gpen, gcp, va, vb, MakeCol{col, WAVE});
+    if (EDGES) {
+      const int eo = ge_edge_word(c, i);
+      const v2 e0 = v2{t.f(eo, e), t.f(eo + 1, e)}, e1 = v2{t.f(eo + 2, e), t.f(eo + 3, e)};
+      convex_contact_vjp_edge(WA, WB, e0, e1, gpen, gcp, va, vb);
+    } else {
+      convex_contact_vjp(WA, WB, narrow_of(sc), gpen, gcp, va, vb, MakeCol{col, WAVE});
+    }
     float o[6];
     part_pose_vjp<EW>(c, t, pa, e, WA, va, o);
     part_pose_vjp<EW>(c, t, pb, e, WB, vb, o + 3);
@@ -3266,10 +3408,10 @@ enum : int { PH_LOAD, PH_SAVE, PH_A, PH_T, PH_B, PH_C0, PH_C0B, PH_C1, PH_C2, PH
 // kso: tile offset of this step's sk0 (skt follows): the key window slot, or
 // L.sk0 where phase A splits the keys (backward re-play)
 // AB: phases A, T and B ran as one (ab_fetch / ph_A / ab_contacts, analytic forward programs)
-template <int EW, int FNSET, bool PRE, class R, bool AB = false>
-CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso,
-                            const MConst& mc) {
-  if (!AB && !CXK_SKIP(a, 1)) {
+// phase T and (polygon scenes) TV0-TV4: the world parts of the step
+template <int EW, int FNSET, class R>
+CX_DEV void transform_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
+  {
     run(PH_T, [&](int l) { ph_T<EW, FNSET>(a, c, t, env0, l); });
     if (FNSET != FNS_ANALYTIC && c.sh.nvt > 0) {
       // the rebuild flags of TV0 and the chunks they make run, wave-uniform:
@@ -3297,15 +3439,22 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
 #endif
     }
   }
+}
+// TAPE: the rollout forward with a tape (phase B records EPA's edges)
+template <int EW, int FNSET, bool PRE, class R, bool AB = false, bool TAPE = false>
+CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int slot, int kso,
+                            const MConst& mc, int step = 0) {
+  if (!AB && !CXK_SKIP(a, 1)) transform_phases<EW, FNSET>(a, c, t, env0, run);
   if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && (a.stages & COTIX_STAGE_BROADPHASE) && !CXK_SKIP(a, 2)) {
     run(PH_BP0, [&](int l) { ph_BP0<EW>(a, c, t, env0, l); });
     const int n = (int)t.ws[c.W.bl_n];  // uniform: read after the phase barrier
     CXK_STAT(b_items, 0);
-    const bool pairs = b_pairs<FNSET>() && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the phase barrier
+    const bool pairs = b_pairs<FNSET>() && !TAPE && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the barrier
     const int per_round = pairs ? WAVE / 2 : WAVE;
-    for (int r = 0; r * per_round < n; ++r) run(PH_B, [&](int l) { ph_BP2<EW, FNSET>(a, c, t, env0, l, r, pairs); });
+    for (int r = 0; r * per_round < n; ++r)
+      run(PH_B, [&](int l) { ph_BP2<EW, FNSET, TAPE>(a, c, t, env0, l, r, pairs, step); });
   } else if (!AB && !CXK_SKIP(a, 2)) {
-    run(PH_B, [&](int l) { ph_B<EW, FNSET>(a, c, t, env0, l); });
+    run(PH_B, [&](int l) { ph_B<EW, FNSET, TAPE>(a, c, t, env0, l, step); });
   }
   if ((FNSET & FNS_CONVEX) != 0 && c.sh.poly && !CXK_SKIP(a, 2)) {
     for (int ch = 0; ch * WAVE < c.nc * EW; ++ch) run(PH_F0, [&](int l) { ph_F0<EW>(c, t, l, ch); });
@@ -3413,12 +3562,13 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
           a, c, t, env0, run, slot, kso, mc);
     } else {
       run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
-      if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true>(a, c, t, env0, run, slot, kso, mc);
+      if (a.stages & COTIX_STAGE_COLLIDER)
+        collider_phases<EW, FNSET, true, R, false, ROLL>(a, c, t, env0, run, slot, kso, mc, step);
     }
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {
-      run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
+      run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr, step); });
       if (a.dyn_reset != nullptr && a.reset_mode == 1) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     } else if (ROLL) {
       run(PH_RET, [&](int l) {
@@ -3439,6 +3589,65 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     }
   }
   run(PH_STORE, [&](int l) { ph_store<EW, ROLL, EVAL>(a, c, t, env0, l); });
+}
+
+// backward with the forward's tape (MODE 4): steps n_steps-1 .. 0, each
+// restored from the saved state and the tape -- Euler (+ action), the world
+// parts, the recorded resolutions (ph_D_tape) -- and reversed by phases E
+// (recording the pre-resolution velocities), GE and G as in the re-play.
+// No key split, narrowphase, RNG scan or choice runs: the tape holds their
+// outcome, and every value the VJPs read is bit-identical to the re-play's
+template <int EW, int FNSET, class R>
+CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run) {
+  run(PH_ADJ, [&](int l) {
+    ws_poly_init<EW>(c, t, l);
+    ph_geo<EW>(a, c, t, env0, l);
+    ph_adj_init<EW>(a, c, t, env0, l);
+    stage_ret_w<EW>(a, c, t, l);
+    for (int e = l; e < EW; e += WAVE) t.w(c.L.pcv, e) = 0u;  // phase T's pose entries
+  });
+  const bool col = (a.stages & COTIX_STAGE_COLLIDER) != 0;
+  const bool edges = FNSET != FNS_ANALYTIC && c.sh.poly && ge_fits(c) && ge_edges_fit(c);
+  RestoreRegs rr;
+  TapeRegs tn, tr;  // the next (earlier) step's tape words, the current step's
+  if (a.n_steps > 0)
+    run(PH_RESTORE, [&](int l) {
+      restore_fetch<EW>(a, c, env0, l, a.n_steps - 1, rr);
+      if (col) tape_fetch<EW>(a, c, env0, l, a.n_steps - 1, tn);
+    });
+  for (int step = a.n_steps - 1; step >= 0; --step) {
+    run(PH_RESTORE, [&](int l) {
+      restore_apply<EW>(c, t, l, rr);
+      if (col) {
+        tr = tn;
+        if (edges) tape_edge_fetch<EW>(a, c, env0, l, step, tr);
+      }
+      if (step > 0) {  // the next (earlier) step, in flight
+        restore_fetch<EW>(a, c, env0, l, step - 1, rr);
+        if (col) tape_fetch<EW>(a, c, env0, l, step - 1, tn);
+      }
+    });
+    run(PH_A, [&](int l) {  // Euler (+ gravity, + action); no key split, no collider scratch
+      if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
+        for (int w = l; w < c.nb * EW; w += WAVE) {
+          const int e = w % EW, b = w / EW;
+          if (env0 + e < a.B) euler_item<EW>(a, c, t, env0, e, b, step);
+        }
+    });
+    if (col) {
+      transform_phases<EW, FNSET>(a, c, t, env0, run);
+      run(PH_D, [&](int l) { ph_D_tape<EW>(a, c, t, env0, l, tr); });
+    }
+    run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
+    if (FNSET != FNS_ANALYTIC && col && ge_fits(c)) {
+      if (edges)
+        run(PH_GE, [&](int l) { ph_GE<EW, true>(a, c, t, env0, l); });
+      else
+        run(PH_GE, [&](int l) { ph_GE<EW>(a, c, t, env0, l); });
+    }
+    run(PH_G, [&](int l) { ph_G<EW, FNSET>(a, c, t, env0, l, step); });
+  }
+  run(PH_ADJ, [&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });
 }
 
 // backward: steps n_steps-1 .. 0, each re-played from the saved state (so

@@ -42,10 +42,26 @@ struct cotix_scene {
   int fnset = 0;
   // kernel variant (cotix_scene_set_variant): envs per wave and whether the
   // reference scenes' specializations may be used -- every variant computes
-  // the same bits; the defaults are the measured best
+  // the same bits; the defaults are the measured best (envs per wave: 4, or
+  // the largest tiling whose LDS fits, lds_default_ew)
   int envs_per_wave = 4;
   int specialize = 1;
 };
+// a workgroup's LDS at `ew` envs per wave (cxk::lds_bytes: the hot tables +
+// WPB tiles and wave scratches) and the hardware's 160 KiB per CU
+constexpr size_t LDS_CAP = 160 * 1024;
+static size_t scene_lds(const cotix_scene* sc, int ew) { return cxk::lds_bytes(sc->host, cxl::WPB, ew); }
+// the default tiling of a scene: 4 envs per wave (the measured best), else
+// the largest of 2, 1 whose workgroup fits the LDS; 0: none fits
+static int lds_default_ew(const cotix_scene* sc) {
+#ifdef COTIX_EW4_ONLY
+  return scene_lds(sc, 4) <= LDS_CAP ? 4 : 0;
+#else
+  for (int ew : {4, 2, 1})
+    if (scene_lds(sc, ew) <= LDS_CAP) return ew;
+  return 0;
+#endif
+}
 // the specialization a launch of this scene uses (cxk::SPEC_*)
 static int scene_spec(const cotix_scene* scene) {
   return scene->specialize ? cxk::spec_of(scene->host) : cxk::SPEC_GENERIC;
@@ -254,6 +270,15 @@ int cotix_scene_create_ex(int n_bodies, const float* body_params, int n_parts, c
     delete sc;
     return -1;
   }
+  // the tiling is a property of the scene: a scene whose tile does not fit
+  // the LDS even at one env per wave is rejected here, not at its first launch
+  sc->envs_per_wave = lds_default_ew(sc);
+  if (sc->envs_per_wave == 0) {
+    const size_t need = scene_lds(sc, 1);
+    delete sc;
+    return fail("scene too large for the LDS tile: " + std::to_string(need) + " bytes per workgroup at one env per "
+                "wave (" + std::to_string(cxl::WPB) + " waves), the CU has " + std::to_string(LDS_CAP));
+  }
   *out = sc;
   return 0;
 }
@@ -278,12 +303,16 @@ int cotix_scene_destroy(cotix_scene* scene) {
 
 int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specialize) {
   if (!scene) return fail("null scene");
-  if (envs_per_wave == 0) envs_per_wave = 4;
+  if (envs_per_wave == 0) envs_per_wave = lds_default_ew(scene);
   if (envs_per_wave != 1 && envs_per_wave != 2 && envs_per_wave != 4 && envs_per_wave != 8)
     return fail("envs_per_wave must be 0 (default), 1, 2, 4 or 8");
 #ifdef COTIX_EW4_ONLY
   if (envs_per_wave != 4) return fail("this build carries the 4-envs-per-wave tiling only");
 #endif
+  if (scene_lds(scene, envs_per_wave) > LDS_CAP)
+    return fail("envs_per_wave " + std::to_string(envs_per_wave) + ": the scene's workgroup needs " +
+                std::to_string(scene_lds(scene, envs_per_wave)) + " bytes of LDS, the CU has " +
+                std::to_string(LDS_CAP));
   scene->envs_per_wave = envs_per_wave;
   scene->specialize = specialize ? 1 : 0;
   return 0;
@@ -292,8 +321,13 @@ int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specializ
 int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec) {
   if (!scene) return fail("null scene");
   if (envs_per_wave) *envs_per_wave = scene->envs_per_wave;
-  // the step program's specialization: instantiated at 4 and 2 envs per wave
-  if (spec) *spec = (scene->envs_per_wave == 4 || scene->envs_per_wave == 2) ? scene_spec(scene) : cxk::SPEC_GENERIC;
+  // the step program's specialization, as the launcher has it
+  // (cotix_step_kernel.hip): the reference scenes at 4 and 2 envs per wave,
+  // the box world's structure at 4 only
+  if (spec) {
+    const int ew = scene->envs_per_wave, s = scene_spec(scene);
+    *spec = (ew == 4 || (ew == 2 && s != cxk::SPEC_BOX)) ? s : cxk::SPEC_GENERIC;
+  }
   return 0;
 }
 
@@ -336,8 +370,8 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
 #else
   const int EW = scene->envs_per_wave;
 #endif
-  const size_t lds = cxk::lds_bytes(scene->host, cxl::WPB, EW);
-  if (lds > 160 * 1024) return fail("scene too large for the LDS tile");
+  const size_t lds = scene_lds(scene, EW);
+  if (lds > LDS_CAP) return fail("scene too large for the LDS tile");  // (not reached: checked at create / set_variant)
   cxk::KArgs ka = ka0;
   ka.sc = scene->dev;
   ka.sh = scene->host;  // the header by value (kernel arguments)
@@ -455,9 +489,22 @@ int cotix_step_ex(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err,
                    resets, chosen, cells, stream);
 }
 
+int cotix_rollout_tape_words(const cotix_scene* scene) {
+  if (!scene) return fail("null scene");
+  return cxk::tape_words(scene->host.nb, scene->host.nc, scene->host.poly);
+}
+
 int cotix_rollout(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int geom_stride,
                   int B, int n_steps, float dt, int stages, const float* action, int action_body,
                   const float* ret_weights, float* ret, float* saved_dyn, uint32_t* saved_keys, cotix_stream_t stream) {
+  return cotix_rollout_ex(scene, dyn, keys, err, geom, geom_stride, B, n_steps, dt, stages, action, action_body,
+                          ret_weights, ret, saved_dyn, saved_keys, nullptr, stream);
+}
+
+int cotix_rollout_ex(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom,
+                     int geom_stride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
+                     const float* ret_weights, float* ret, float* saved_dyn, uint32_t* saved_keys, uint32_t* tape,
+                     cotix_stream_t stream) {
   if (check_step_args(scene, dyn, keys, geom, geom_stride, B, n_steps, stages, action, action_body)) return -1;
   if (!err || !ret_weights || !ret || !saved_dyn || !saved_keys) return fail("null argument");
   if (B == 0 || n_steps == 0) return 0;
@@ -475,6 +522,8 @@ int cotix_rollout(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err,
   ka.action_body = action_body;
   ka.save_dyn = saved_dyn;
   ka.save_keys = saved_keys;
+  ka.tape = tape;
+  ka.tw = cxk::tape_words(scene->host.nb, scene->host.nc, scene->host.poly);
   ka.ret = ret;
   for (int k = 0; k < scene->host.nb * 6; ++k) ka.ret_w[k] = ret_weights[k];
   return launch(scene, ka, 1, stream);
@@ -484,6 +533,14 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
                            int geom_stride, int B, int n_steps, float dt, int stages, const float* action,
                            int action_body, const float* ret_weights, float* grad_action, float* grad_dyn0,
                            cotix_stream_t stream) {
+  return cotix_rollout_backward_ex(scene, saved_dyn, saved_keys, nullptr, geom, geom_stride, B, n_steps, dt, stages,
+                                   action, action_body, ret_weights, grad_action, grad_dyn0, stream);
+}
+
+int cotix_rollout_backward_ex(cotix_scene* scene, const float* saved_dyn, const uint32_t* saved_keys,
+                              const uint32_t* tape, const float* geom, int geom_stride, int B, int n_steps, float dt,
+                              int stages, const float* action, int action_body, const float* ret_weights,
+                              float* grad_action, float* grad_dyn0, cotix_stream_t stream) {
   if (check_step_args(scene, saved_dyn, saved_keys, geom, geom_stride, B, n_steps, stages, action, action_body))
     return -1;
   if (!ret_weights) return fail("null argument");
@@ -510,10 +567,12 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
   ka.action_body = action_body;
   ka.save_dyn = const_cast<float*>(saved_dyn);
   ka.save_keys = const_cast<uint32_t*>(saved_keys);
+  ka.tape = const_cast<uint32_t*>(tape);
+  ka.tw = cxk::tape_words(scene->host.nb, scene->host.nc, scene->host.poly);
   ka.grad_action = grad_action;
   ka.grad_dyn = grad_dyn0;
   for (int k = 0; k < scene->host.nb * 6; ++k) ka.ret_w[k] = ret_weights[k];
-  return launch(scene, ka, 2, stream);
+  return launch(scene, ka, tape ? 4 : 2, stream);
 }
 
 int cotix_physics_euler(float* dyn, int n_bodies, int B, float dt, cotix_stream_t stream) {

@@ -72,8 +72,9 @@ struct WaveRun {
   }
 #endif
 };
-// MODE 0: step, 1: rollout forward (saves + return), 2: rollout backward,
-// 3: eval with the device judge / control (cotix_eval);
+// MODE 0: step, 1: rollout forward (saves + return, + tape), 2: rollout
+// backward re-playing the forward, 3: eval with the device judge / control
+// (cotix_eval), 4: rollout backward from the forward's tape;
 // SPEC: scene specialization (cxk::SPEC_*, compile-time dimensions)
 template <int EW, int FNSET, int MODE, int SPEC = cxk::SPEC_GENERIC>
 __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   // the forward programs load the wave's state before the barrier: it writes
   // only the wave's own tile (disjoint from the tables), so its global reads
   // overlap the table copy's (a launch's fixed cost, K = 1 RL loops)
-  if (MODE != 2 && env0 < a.B) {
+  if (MODE != 2 && MODE != 4 && env0 < a.B) {
     if (MODE == 3)
       cxk::ph_load_fwd<EW, false, true>(a, c, t, env0, lane);
     else
@@ -120,7 +121,9 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
 #else
   const WaveRun run{lane};
 #endif
-  if (MODE == 2)
+  if (MODE == 4)
+    cxk::run_wave_backward_tape<EW, FNSET>(a, c, t, env0, run);
+  else if (MODE == 2)
     cxk::run_wave_backward<EW, FNSET>(a, c, t, env0, run);
   else if (MODE == 3)
     cxk::run_wave<EW, FNSET, false, true>(a, c, t, env0, run, true);
@@ -147,11 +150,12 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
 #if COTIX_EW == 4 || COTIX_EW == 2
   // the reference-scene specializations: every program of RoboCup at the
   // default tiling, the step programs (mode 0) at 4 and 2 envs per wave
-  if (spec == cxk::SPEC_ROBOCUP && F == F_AN && (mode == 0 || COTIX_EW == 4)) {
+  // (the re-play backward, mode 2, is the tape backward's check: generic only)
+  if (spec == cxk::SPEC_ROBOCUP && F == F_AN && mode != 2 && (mode == 0 || COTIX_EW == 4)) {
     if (mode == 3)
       COTIX_LAUNCH_SPEC(F_AN, 3, cxk::SPEC_ROBOCUP);
-    else if (mode == 2)
-      COTIX_LAUNCH_SPEC(F_AN, 2, cxk::SPEC_ROBOCUP);
+    else if (mode == 4)
+      COTIX_LAUNCH_SPEC(F_AN, 4, cxk::SPEC_ROBOCUP);
     else if (mode == 1)
       COTIX_LAUNCH_SPEC(F_AN, 1, cxk::SPEC_ROBOCUP);
     else
@@ -164,9 +168,9 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
   }
 #if COTIX_EW == 4
   // the box world's structure: the step and rollout programs (finite_scene, grad_box)
-  if (spec == cxk::SPEC_BOX && F == F_AN && mode <= 2) {
-    if (mode == 2)
-      COTIX_LAUNCH_SPEC(F_AN, 2, cxk::SPEC_BOX);
+  if (spec == cxk::SPEC_BOX && F == F_AN && (mode <= 1 || mode == 4)) {
+    if (mode == 4)
+      COTIX_LAUNCH_SPEC(F_AN, 4, cxk::SPEC_BOX);
     else if (mode == 1)
       COTIX_LAUNCH_SPEC(F_AN, 1, cxk::SPEC_BOX);
     else
@@ -192,6 +196,11 @@ hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_
       COTIX_LAUNCH(F_AN, 2);
     else
       COTIX_LAUNCH(F_ALL, 2);  // polygon scenes (the host rejects circle x polygon contacts)
+  } else if (mode == 4) {
+    if (F == F_AN)
+      COTIX_LAUNCH(F_AN, 4);
+    else
+      COTIX_LAUNCH(F_ALL, 4);
   } else if (mode == 3) {
     if (F == F_AN)
       COTIX_LAUNCH(F_AN, 3);

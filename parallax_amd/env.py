@@ -37,8 +37,6 @@ class BatchedEnv:
         self.resets = torch.zeros(w.B, dtype=torch.int32, device=w.device)
         self._keys0 = w.keys.clone()
         self.judge, self.control = judge, control
-        self._judge_c = judge.c_struct() if judge is not None else None
-        self._control_c = control.c_struct() if control is not None else None
         nb = len(w.bodies)
         self._obs = torch.empty(w.B, nb, 6, dtype=torch.float32, device=w.device)
         self.reward = torch.zeros(w.B, dtype=torch.float32, device=w.device)
@@ -101,11 +99,17 @@ class BatchedEnv:
         configuration, built on first use: an RL loop's per-step host work is
         then one ctypes call (the launch checks only a new action's shape)."""
         w = self.world
-        # (object identities: a buffer swapped in by the caller gets its own launch)
-        key = (n_steps, body, id(obs), id(w.dyn), id(w.keys), id(w.err), id(w.geom), id(self.scenario.dyn_reset))
+        # everything the prepared launch copies: the public attributes by
+        # value (dt, autoreset, the scenario's stages) and the judge / control
+        # and the buffers by identity (a buffer swapped in by the caller, or a
+        # new judge, gets its own launch)
+        key = (n_steps, body, float(self.dt), bool(self.autoreset), int(self.scenario.stages), id(self.judge),
+               id(self.control), id(obs), id(w.dyn), id(w.keys), id(w.err), id(w.geom), id(self.scenario.dyn_reset))
         launch = self._launchers.get(key)
         if launch is not None:
             return launch
+        judge_c = self.judge.c_struct() if self.judge is not None else None
+        control_c = self.control.c_struct() if self.control is not None else None
         if obs is not self._obs and (tuple(obs.shape) != tuple(self._obs.shape) or obs.dtype != torch.float32
                                      or not obs.is_contiguous() or obs.device != self._obs.device):
             raise ValueError("obs_out must be a contiguous f32 [B, n_bodies, 6] tensor on the env's device")
@@ -113,12 +117,12 @@ class BatchedEnv:
             self._launchers.clear()
         if self.judge is None:
             launch = w.eval_launcher(w.dyn, w.keys, w.err, 1, n_steps, self.dt, self.scenario.stages,
-                                     action_body=body, control=self._control_c, reset_mode=1 if self.autoreset else 0,
+                                     action_body=body, control=control_c, reset_mode=1 if self.autoreset else 0,
                                      dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
                                      resets=self.resets if self.autoreset else None, obs=obs)
         else:
             launch = w.eval_launcher(w.dyn, w.keys, w.err, 1, n_steps, self.dt, self.scenario.stages,
-                                     judge=self._judge_c, control=self._control_c, reward=self.reward,
+                                     judge=judge_c, control=control_c, reward=self.reward,
                                      finished=self.done, action_body=body, reset_mode=2 if self.autoreset else 0,
                                      dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
                                      resets=self.resets if self.autoreset else None, obs=obs)

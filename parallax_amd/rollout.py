@@ -1,6 +1,10 @@
 """Differentiable fused rollout (BASELINE config 5): grad(return)/d(action)
 through an n-step rollout, forward and backward as HIP kernels
-(cotix_rollout / cotix_rollout_backward, include/cotix_amd.h).
+(cotix_rollout_ex / cotix_rollout_backward_ex, include/cotix_amd.h).  The
+forward writes a decision tape (each step's resolutions and, for polygon
+contacts, EPA's final edge) and the backward restores those decisions instead
+of re-playing the collider; tape=False runs the re-play instead (the same
+bits, the check of the tape path).
 
 The reference defines neither action nor return (cotix/_envs.py:9-28 is
 abstract); SURVEY.md 8(d) fixes them: action[t] (f32[B,2]) is added to the
@@ -41,37 +45,44 @@ def _check_actions(world, actions):
     return actions
 
 
-def rollout_forward(world, actions, action_body=None, ret_weights=None, dt=1e-2, stages=_ffi.STAGES_ROBOCUP):
+def rollout_forward(world, actions, action_body=None, ret_weights=None, dt=1e-2, stages=_ffi.STAGES_ROBOCUP,
+                    tape=True):
     """Run T = actions.shape[0] fused steps (world state advanced in place)
-    and save the trajectory.  Returns (ret [B], saved) for rollout_backward."""
+    and save the trajectory (and the decision tape).  Returns (ret [B],
+    saved) for rollout_backward."""
     actions = _check_actions(world, actions)
     nb, B, T = len(world.bodies), world.B, actions.shape[0]
     action_body = nb - 1 if action_body is None else int(action_body)
     w = _weights(world, ret_weights)
     saved_dyn = torch.empty(T, nb, 6, B, device=world.device, dtype=torch.float32)
     saved_keys = torch.empty(T, B, 2, device=world.device, dtype=torch.int32)
+    tw = _ffi.lib.cotix_rollout_tape_words(world.scene.handle)
+    tp = torch.empty(T, tw, B, device=world.device, dtype=torch.int32) if tape else None
     ret = torch.zeros(B, device=world.device, dtype=torch.float32)
-    _ffi.check(_ffi.lib.cotix_rollout(
+    _ffi.check(_ffi.lib.cotix_rollout_ex(
         world.scene.handle, _ffi.ptr(world.dyn), _ffi.ptr(world.keys), _ffi.ptr(world.err), _ffi.ptr(world.geom),
         world.geom_stride, B, T, float(dt), int(stages), _ffi.ptr(actions), action_body,
-        w.ctypes.data_as(_ffi._P), _ffi.ptr(ret), _ffi.ptr(saved_dyn), _ffi.ptr(saved_keys),
-        _ffi.stream_ptr(world.device)), "cotix_rollout")
-    saved = dict(dyn=saved_dyn, keys=saved_keys, actions=actions, action_body=action_body, w=w, dt=float(dt),
-                 stages=int(stages))
+        w.ctypes.data_as(_ffi._P), _ffi.ptr(ret), _ffi.ptr(saved_dyn), _ffi.ptr(saved_keys), _ffi.ptr(tp),
+        _ffi.stream_ptr(world.device)), "cotix_rollout_ex")
+    saved = dict(dyn=saved_dyn, keys=saved_keys, tape=tp, actions=actions, action_body=action_body, w=w,
+                 dt=float(dt), stages=int(stages))
     return ret, saved
 
 
-def rollout_backward(world, saved, want_dyn0=False):
-    """d ret / d actions [T, B, 2] (and d ret / d initial state [nb, 6, B])."""
+def rollout_backward(world, saved, want_dyn0=False, replay=False):
+    """d ret / d actions [T, B, 2] (and d ret / d initial state [nb, 6, B]):
+    from the forward's tape, or (replay=True, or no tape saved) re-playing
+    the forward's steps."""
     nb, B = len(world.bodies), world.B
     T = saved["actions"].shape[0]
     ga = torch.empty(T, B, 2, device=world.device, dtype=torch.float32)
     gd = torch.empty(nb, 6, B, device=world.device, dtype=torch.float32) if want_dyn0 else None
-    _ffi.check(_ffi.lib.cotix_rollout_backward(
-        world.scene.handle, _ffi.ptr(saved["dyn"]), _ffi.ptr(saved["keys"]), _ffi.ptr(world.geom),
+    tp = None if replay else saved.get("tape")
+    _ffi.check(_ffi.lib.cotix_rollout_backward_ex(
+        world.scene.handle, _ffi.ptr(saved["dyn"]), _ffi.ptr(saved["keys"]), _ffi.ptr(tp), _ffi.ptr(world.geom),
         world.geom_stride, B, T, saved["dt"], saved["stages"], _ffi.ptr(saved["actions"]), saved["action_body"],
         saved["w"].ctypes.data_as(_ffi._P), _ffi.ptr(ga), _ffi.ptr(gd), _ffi.stream_ptr(world.device)),
-        "cotix_rollout_backward")
+        "cotix_rollout_backward_ex")
     return ga, gd
 
 

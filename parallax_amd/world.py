@@ -89,6 +89,16 @@ class Scene:
 
 
 class World:
+    @classmethod
+    def from_bodies(cls, bodies, batch=None, device="cuda", keys=None, params=None):
+        """A World from the reference's own body pytrees (a list of AnyBody
+        objects, or an env object with ``.bodies``), read by the reference's
+        class and field names (parallax_amd.pytree); leaves with a leading
+        batch dimension (a vmapped pytree) give the env axis."""
+        from .pytree import bodies_from_reference
+        pb, B = bodies_from_reference(bodies, batch)
+        return cls(pb, B, device, keys, params)
+
     def __init__(self, bodies, batch=1, device="cuda", keys=None, params=None):
         if not all(isinstance(b, AnyBody) for b in bodies):
             raise TypeError("bodies must be AnyBody")

@@ -62,3 +62,16 @@ def pytest_sessionfinish(session, exitstatus):
     elif tr is not None:
         tr.write_line("native library check: %s mapped (%s), %d gpu tests"
                       % (want, _ffi.lib.cotix_version().decode(), len(_GPU_TESTS_RUN)))
+
+
+def pytest_terminal_summary(terminalreporter):
+    """The gradient checks' measured errors (tests/grad_cases.py close): per
+    workload, the floor its compared blocks needed at rtol 1e-5 -- the
+    numbers DESIGN.md section 5 records against the tolerances."""
+    gc = sys.modules.get("grad_cases")
+    if gc is None or not getattr(gc, "MEASURED", None):
+        return
+    terminalreporter.write_line("gradient checks, floor needed at rtol 1e-5 (allowed: analytic %g, polygon %g):"
+                                % (gc.ANALYTIC_TOL[1], gc.POLYGON_TOL[1]))
+    for k in sorted(gc.MEASURED):
+        terminalreporter.write_line("  %-22s %.3g" % (k, gc.MEASURED[k]))

@@ -5,19 +5,23 @@
 // then f32 body_params[nb*4], int32 part_body[np], part_type[np],
 // part_nverts[np], f32 geom[gstride ? B*gstride : G], f32 dyn[nb*6*B],
 // u32 keys[B*2]; mode 1 adds f32 actions[T*B*2], f32 ret_w[nb*6].
-// OUT: mode 0: dyn, keys, err; mode 1: dyn, keys, err, ret, grad_action, grad_dyn0.
+// OUT: mode 0: dyn, keys, err; mode 1: dyn, keys, err, ret, grad_action, grad_dyn0
+// (the backward from the forward's tape; the re-play backward must give the
+// same bits, else exit 6).
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 extern "C" {
 int emu_scene_create(int, const float*, int, const int*, const int*, const int*, void**);
 int emu_step(void*, float*, uint32_t*, uint32_t*, const float*, int, int, int, float, int, const float*, int,
              const float*, uint32_t*, int);
+int emu_rollout_tape_words(void*);
 int emu_rollout(void*, float*, uint32_t*, uint32_t*, const float*, int, int, int, float, int, const float*, int,
-                const float*, float*, float*, uint32_t*, int);
-int emu_rollout_backward(void*, const float*, const uint32_t*, const float*, int, int, int, float, int, const float*,
-                         int, const float*, float*, float*, int);
+                const float*, float*, float*, uint32_t*, uint32_t*, int);
+int emu_rollout_backward(void*, const float*, const uint32_t*, const uint32_t*, const float*, int, int, int, float, int,
+                         const float*, int, const float*, float*, float*, int);
 const char* emu_last_error(void);
 int emu_scene_destroy(void*);
 }
@@ -63,13 +67,20 @@ int main(int argc, char** argv) {
     wr(o, err);
   } else {
     std::vector<float> ret(B, 0.0f), sd((size_t)T * nb * 6 * B), ga((size_t)T * B * 2), gd((size_t)nb * 6 * B);
-    std::vector<uint32_t> sk((size_t)T * B * 2);
+    std::vector<uint32_t> sk((size_t)T * B * 2), tape((size_t)T * emu_rollout_tape_words(sc) * B, 0x7FBADBADu);
     emu_rollout(sc, dyn.data(), keys.data(), err.data(), geom.data(), gs, B, T, 1e-2f, stages, act.data(), ab,
-                rw.data(), ret.data(), sd.data(), sk.data(), E);
-    if (emu_rollout_backward(sc, sd.data(), sk.data(), geom.data(), gs, B, T, 1e-2f, stages, act.data(), ab, rw.data(),
-                             ga.data(), gd.data(), E)) {
+                rw.data(), ret.data(), sd.data(), sk.data(), tape.data(), E);
+    std::vector<float> ra(ga.size()), rd_(gd.size());
+    if (emu_rollout_backward(sc, sd.data(), sk.data(), tape.data(), geom.data(), gs, B, T, 1e-2f, stages, act.data(),
+                             ab, rw.data(), ga.data(), gd.data(), E) ||
+        emu_rollout_backward(sc, sd.data(), sk.data(), nullptr, geom.data(), gs, B, T, 1e-2f, stages, act.data(), ab,
+                             rw.data(), ra.data(), rd_.data(), E)) {
       fprintf(stderr, "%s\n", emu_last_error());
       return 5;
+    }
+    if (memcmp(ga.data(), ra.data(), ga.size() * 4) != 0 || memcmp(gd.data(), rd_.data(), gd.size() * 4) != 0) {
+      fprintf(stderr, "tape backward != re-play backward\n");
+      return 6;
     }
     wr(o, dyn);
     wr(o, keys);

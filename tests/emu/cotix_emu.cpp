@@ -68,7 +68,10 @@ void run_blocks(const cxk::KArgs& a, int mode) {
     const int env0 = wv * EW;
     cxk_simt::run([&](int lane) {
       const HostRun run{lane};
-      if (mode == 2)
+      if (mode == 4)
+        F == 1 ? cxk::run_wave_backward_tape<EW, 1>(a, c, t, env0, run)
+               : cxk::run_wave_backward_tape<EW, 15>(a, c, t, env0, run);
+      else if (mode == 2)
         F == 1 ? cxk::run_wave_backward<EW, 1>(a, c, t, env0, run) : cxk::run_wave_backward<EW, 15>(a, c, t, env0, run);
       else if (mode == 1)
         F == 1 ? cxk::run_wave<EW, 1, true>(a, c, t, env0, run) : cxk::run_wave<EW, 15, true>(a, c, t, env0, run);
@@ -205,9 +208,13 @@ int emu_eval(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float
   return 0;
 }
 
+int emu_rollout_tape_words(void* scene) {
+  const cxk::SceneDev& s = static_cast<EmuScene*>(scene)->s;
+  return cxk::tape_words(s.nb, s.nc, s.poly);
+}
 int emu_rollout(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
                 int n_steps, float dt, int stages, const float* action, int action_body, const float* ret_w, float* ret,
-                float* saved_dyn, uint32_t* saved_keys, int E) {
+                float* saved_dyn, uint32_t* saved_keys, uint32_t* tape, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
   cxk::KArgs a{};
   a.sc = &s->s;
@@ -224,15 +231,17 @@ int emu_rollout(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const fl
   a.action_body = action_body;
   a.save_dyn = saved_dyn;
   a.save_keys = saved_keys;
+  a.tape = tape;
+  a.tw = emu_rollout_tape_words(scene);
   a.ret = ret;
   for (int k = 0; k < s->s.nb * 6; ++k) a.ret_w[k] = ret_w[k];
   run_any(a, E, 1);
   return 0;
 }
 
-int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* saved_keys, const float* geom,
-                         int gstride, int B, int n_steps, float dt, int stages, const float* action, int action_body,
-                         const float* ret_w, float* grad_action, float* grad_dyn0, int E) {
+int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* saved_keys, const uint32_t* tape,
+                         const float* geom, int gstride, int B, int n_steps, float dt, int stages, const float* action,
+                         int action_body, const float* ret_w, float* grad_action, float* grad_dyn0, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
   if (s->fnset & cxk::FNS_CIRCLE_POLY) {  // (the library's admission, cotix_step.hip)
     g_err = "differentiable rollout: circle x polygon contacts are not differentiated";
@@ -254,10 +263,12 @@ int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* sa
   a.action_body = action_body;
   a.save_dyn = const_cast<float*>(saved_dyn);
   a.save_keys = const_cast<uint32_t*>(saved_keys);
+  a.tape = const_cast<uint32_t*>(tape);
+  a.tw = emu_rollout_tape_words(scene);
   a.grad_action = grad_action;
   a.grad_dyn = grad_dyn0;
   for (int k = 0; k < s->s.nb * 6; ++k) a.ret_w[k] = ret_w[k];
-  run_any(a, E, 2);
+  run_any(a, E, tape ? 4 : 2);
   return 0;
 }
 

@@ -30,9 +30,10 @@ def load(asan=False):
     lib.emu_body_penetration.argtypes = [P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_]
     lib.emu_body_aabb.argtypes = [P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_]
     lib.emu_rollout.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
-                                ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, ctypes.c_int]
-    lib.emu_rollout_backward.argtypes = [P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, P_, ctypes.c_int]
+    lib.emu_rollout_backward.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                          ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.c_int]
+    lib.emu_rollout_tape_words.argtypes = [P_]
     lib.emu_eval.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_float, ctypes.c_int, P_, P_, P_, ctypes.c_int, P_, P_, ctypes.c_int, P_, P_, P_,
                              ctypes.c_int]
@@ -106,26 +107,31 @@ def step_ex(lib, h, dyn, keys, err, geom, gstride, n_steps, stages, nb, dt=1e-2,
 
 def rollout(lib, h, dyn, keys, err, geom, gstride, stages, actions, action_body, w, dt=1e-2, E=4):
     """Forward of the differentiable rollout; returns (ret [B], saved_dyn
-    [T,nb,6,B], saved_keys [T,B,2]); dyn/keys/err advanced in place."""
+    [T,nb,6,B], saved_keys [T,B,2], tape [T,tape_words,B]); dyn/keys/err
+    advanced in place.  The tape is poisoned first (words the forward leaves
+    unwritten are never read)."""
     T, B = actions.shape[0], dyn.shape[2]
     ret = np.zeros(B, np.float32)
     sd = np.zeros((T,) + dyn.shape, np.float32)
     sk = np.zeros((T, B, 2), np.uint32)
+    tape = np.full((T, lib.emu_rollout_tape_words(h), B), 0x7FBADBAD, np.uint32)
     actions = np.ascontiguousarray(actions, np.float32)
     w = np.ascontiguousarray(w, np.float32)
     lib.emu_rollout(h, _p(dyn), _p(keys), _p(err), _p(geom), gstride, B, T, dt, stages, _p(actions), action_body,
-                    _p(w), _p(ret), _p(sd), _p(sk), E)
-    return ret, sd, sk
+                    _p(w), _p(ret), _p(sd), _p(sk), _p(tape), E)
+    return ret, sd, sk, tape
 
 
-def rollout_backward(lib, h, sd, sk, geom, gstride, stages, actions, action_body, w, dt=1e-2, E=4):
+def rollout_backward(lib, h, sd, sk, geom, gstride, stages, actions, action_body, w, dt=1e-2, E=4, tape=None):
+    """The backward: from the forward's tape (MODE 4), or re-playing the
+    forward (tape None, MODE 2)."""
     T, B = actions.shape[0], sd.shape[3]
     ga = np.zeros((T, B, 2), np.float32)
     gd = np.zeros(sd.shape[1:], np.float32)
     actions = np.ascontiguousarray(actions, np.float32)
     w = np.ascontiguousarray(w, np.float32)
-    rc = lib.emu_rollout_backward(h, _p(sd), _p(sk), _p(geom), gstride, B, T, dt, stages, _p(actions), action_body,
-                                  _p(w), _p(ga), _p(gd), E)
+    rc = lib.emu_rollout_backward(h, _p(sd), _p(sk), _p(tape), _p(geom), gstride, B, T, dt, stages, _p(actions),
+                                  action_body, _p(w), _p(ga), _p(gd), E)
     if rc:
         raise RuntimeError(lib.emu_last_error().decode())
     return ga, gd

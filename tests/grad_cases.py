@@ -36,7 +36,8 @@ def box_case(B, T, seed=0):
     w = np.zeros(7 * 6, np.float32)
     w[6 * 6 + 0] = 1.0   # ball 6: x
     w[5 * 6 + 3] = 0.5   # ball 5: vy
-    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=6, step=P.robocup_step)
+    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=6, step=P.robocup_step,
+                tol=ANALYTIC_TOL, name="box")
 
 
 def robocup_case(B, T, seed=0):
@@ -47,7 +48,7 @@ def robocup_case(B, T, seed=0):
     w = np.zeros(5 * 6, np.float32)
     w[4 * 6 + 0] = 1.0   # return = sum_t ball x
     return dict(make=P.robocup_bodies, S0=np.ascontiguousarray(dyn.transpose(2, 0, 1)), keys=keys,
-                actions=actions, w=w, ab=4, step=P.robocup_step)
+                actions=actions, w=w, ab=4, step=P.robocup_step, tol=ANALYTIC_TOL, name="robocup")
 
 
 def lunar_case(B, T, seed=0, drop=-0.02):
@@ -75,7 +76,7 @@ def lunar_case(B, T, seed=0, drop=-0.02):
     w[4] = 2.0          # lander angle
     w[2 * 6 + 3] = 0.25  # left leg vy
     return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=0,
-                step=P.lunar_lander_step)
+                step=P.lunar_lander_step, tol=POLYGON_TOL, name="lunar")
 
 
 def poly_box_bodies(octagons=False):
@@ -122,7 +123,8 @@ def poly_box_case(B, T, seed=0, octagons=False):
     w[2 * 6 + 0] = 1.0   # box x
     w[3 * 6 + 1] = 0.5   # hexagon y
     w[3 * 6 + 4] = 1.0   # hexagon angle
-    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=2, step=P.robocup_step)
+    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=2, step=P.robocup_step,
+                tol=POLYGON_TOL, name="octagons" if octagons else "poly_box")
 
 
 def quad_row_case(B, T, seed=0):
@@ -152,23 +154,47 @@ def quad_row_case(B, T, seed=0):
     w = np.zeros(9 * 6, np.float32)
     w[4 * 6 + 0] = 1.0
     w[5 * 6 + 4] = 0.5
-    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=4, step=P.robocup_step)
+    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=4, step=P.robocup_step,
+                tol=POLYGON_TOL, name="quad_row")
 
 
-def oracle(case, envs=None):
-    """Per env: (ret, grad_actions [T,2], grad_S0 [nb,6]) from the torch VJP chain."""
+def oracle(case, envs=None, params=None):
+    """Per env: (ret, grad_actions [T,2], grad_S0 [nb,6]) from the torch VJP
+    chain, under the oracle parameter block `params` (None: the defaults)."""
+    from cotix_oracle import params as _params
     B = case["S0"].shape[0]
     envs = range(B) if envs is None else envs
     out = {}
-    for e in envs:
-        ret, ga, gS, _ = G.rollout_grad(case["make"], case["S0"][e], case["keys"][e], case["actions"][:, e],
-                                        case["w"], case["ab"], D0, step=case["step"])
-        out[e] = (ret, ga, gS)
+    with _params.use(params):
+        d0 = prng.gjk_initial_direction()  # random_direction(PRNGKey(1)) in the block's PRNG layout
+        for e in envs:
+            ret, ga, gS, _ = G.rollout_grad(case["make"], case["S0"][e], case["keys"][e], case["actions"][:, e],
+                                            case["w"], case["ab"], d0, step=case["step"])
+            out[e] = (ret, ga, gS)
     return out
 
 
-def close(got, want, rtol=2e-4):
-    """Gradient agreement: same NaN pattern, |got-want| <= rtol*(|want| + max|want|*0.1)."""
+# Gradient tolerances, measured (DESIGN.md section 5): the kernel's
+# hand-written f32 VJPs against the oracle's torch-f32 autograd of the same
+# forward differ by rounding only, so the check is north_star's 1e-5
+# relative, elementwise.  Scenes with GJK/EPA contacts add an absolute part,
+# FLOOR * max|want| of the gradient block: their gradient entries are sums of
+# large terms of both signs (contact_from_edges' terms, the polygon vertex
+# chains), whose f32 rounding is relative to the terms, not to the small sum.
+# Measured (tests/test_grad_cpu.py, host emulation == GPU bit for bit; the
+# floor each case needs at rtol 1e-5): box world, RoboCup 0; LunarLander
+# 1.3e-10; quad row 8.1e-8; polygon box 5.0e-7; octagon pair 1.19e-6 --
+# POLYGON_TOL's 4e-6 is 3.4x the largest.
+ANALYTIC_TOL = (1e-5, 0.0)
+POLYGON_TOL = (1e-5, 4e-6)
+MEASURED = {}  # name -> the floor the compared blocks needed at rtol 1e-5 (reported by conftest)
+
+
+def close(got, want, tol=ANALYTIC_TOL, name=None):
+    """Gradient agreement: the same NaN pattern, and for every entry
+    |got - want| <= rtol |want| + floor max|want| (tol = (rtol, floor), the
+    max over the finite entries of this block)."""
+    rtol, floor = tol
     got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
     ng, nw = np.isnan(got), np.isnan(want)
     if not np.array_equal(ng, nw):
@@ -176,6 +202,11 @@ def close(got, want, rtol=2e-4):
     g, w = got[~nw], want[~nw]
     if g.size == 0:
         return True, ""
-    scale = np.abs(w) + 0.1 * np.max(np.abs(w)) + 1e-12
-    err = np.max(np.abs(g - w) / scale)
-    return err <= rtol, "max scaled err %.3g" % err
+    mx = np.max(np.abs(w))
+    d = np.abs(g - w)
+    need = float(np.max(np.maximum(d - rtol * np.abs(w), 0.0)) / mx) if mx > 0 else float(np.max(d))
+    if name is not None:
+        MEASURED[name] = max(MEASURED.get(name, 0.0), need)
+    ok = bool(np.all(d <= rtol * np.abs(w) + floor * mx))
+    rel = float(np.max(d / np.maximum(np.abs(w), 1e-300)))
+    return ok, "needs floor %.3g at rtol %g (allowed %g); max relative error %.3g" % (need, rtol, floor, rel)

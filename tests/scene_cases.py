@@ -42,3 +42,21 @@ def mixed_scene(circle):
         bodies.insert(2, P.Body([G.Circle(0.3, (0.0, 0.0))], position=(-0.75, 0.25), velocity=(0.3, -0.2),
                                 elasticity=0.5, friction_coefficient=0.2))
     return bodies
+
+
+def octagon_row(n):
+    """n octagon bodies in a row, neighbours overlapping (every pair of
+    neighbours in contact), body 0 static: a polygon scene whose step tile
+    needs more LDS than 4 envs per wave give (n = 9: one env per wave fits,
+    n = 12: nothing fits -- rejected at cotix_scene_create)."""
+    from cotix_oracle import geometry as G
+    from cotix_oracle import physics as P
+    a = np.arange(8) * (2 * np.pi / 8)
+    octa = [(float(np.float32(0.25 * np.cos(t))), float(np.float32(0.25 * np.sin(t)))) for t in a]
+    out = [P.Body([G.Polygon(octa, kind="Polygon")], mass=float("inf"), inertia=float("inf"), elasticity=0.5,
+                  friction_coefficient=0.2)]
+    for i in range(1, n):
+        out.append(P.Body([G.Polygon(octa, kind="Polygon")], position=(0.46 * i, 0.02 * i), angle=0.1 * i,
+                          velocity=(0.1 * (i % 3) - 0.1, -0.2), angular_velocity=0.05 * i, elasticity=0.5,
+                          friction_coefficient=0.2))
+    return out

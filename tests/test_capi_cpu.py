@@ -125,6 +125,14 @@ def test_scene_variant_api():
     assert s.variant()["specialization"] == "robocup_partitionable"
     s = pa.Scene(pa.scenarios.robocup_bodies(), params=pa.Params(contact_p=0.25))
     assert s.variant()["specialization"] == "generic"
+    # the box world's structure is specialized at 4 envs per wave only (the
+    # launcher's table): at 2 the generic kernel runs and is reported
+    s = pa.Scene(pa.scenarios.box_world_bodies())
+    assert s.variant()["specialization"] == "box"
+    s.set_variant(2)
+    assert s.variant() == {"envs_per_wave": 2, "specialization": "generic"}
+    s.set_variant(1)
+    assert s.variant()["specialization"] == "generic"
 
 
 def test_eval_rejects_reset_mode2_without_judge_and_overflow():
@@ -212,3 +220,25 @@ def test_prepared_eval_launch_marshals_every_argument(monkeypatch):
         with pytest.raises(ValueError, match="action"):
             env.step(1, action=torch.ones(Scen.world.B, 3))
     assert isinstance(calls[0][-1], ctypes.c_void_p)
+
+
+def test_tiling_is_a_scene_property():
+    """cotix_scene_create picks the default envs per wave from the scene's LDS
+    need (4, else the largest of 2 and 1 that fits the CU's 160 KiB) and
+    rejects a scene that fits at no tiling, with the byte count; an explicit
+    tiling that does not fit is rejected by cotix_scene_set_variant."""
+    import parallax_amd as pa
+    import grad_cases as GC
+    import scene_cases
+    from test_gpu_parity import _pa_bodies
+    quad_row = pa.Scene(_pa_bodies(pa, GC.quad_row_case(1, 1)["make"]()))
+    assert quad_row.variant()["envs_per_wave"] == 2
+    with pytest.raises(RuntimeError, match="bytes of LDS"):
+        quad_row.set_variant(4)
+    quad_row.set_variant(1)
+    quad_row.set_variant(0)
+    assert quad_row.variant()["envs_per_wave"] == 2
+    assert pa.Scene(_pa_bodies(pa, scene_cases.octagon_row(9))).variant()["envs_per_wave"] == 1
+    with pytest.raises(RuntimeError, match=r"scene too large for the LDS tile: \d+ bytes"):
+        pa.Scene(_pa_bodies(pa, scene_cases.octagon_row(12)))
+    assert pa.Scene(pa.scenarios.lunar_lander_bodies(torch.zeros(1, 7, 4, 2))).variant()["envs_per_wave"] == 4

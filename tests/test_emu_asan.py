@@ -105,8 +105,9 @@ def test_asan_box_world_rollout_backward(emu_mod, tmp_path, E):
                          ab=case["ab"], w=case["w"])
     h, geom = emu.oracle_scene(lib, case["make"]())
     d, k, err = dyn.copy(), np.array(case["keys"], np.uint32, copy=True), np.zeros(B, np.uint32)
-    ret, sd, sk = emu.rollout(lib, h, d, k, err, geom, 0, 21, case["actions"], case["ab"], case["w"], E=E)
-    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, 21, case["actions"], case["ab"], case["w"], E=E)
+    ret, sd, sk, tape = emu.rollout(lib, h, d, k, err, geom, 0, 21, case["actions"], case["ab"], case["w"], E=E)
+    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, 21, case["actions"], case["ab"], case["w"], E=E,
+                                  tape=tape)
     want = np.concatenate([x.reshape(-1).view(np.uint8) for x in (d, k, err, ret, ga, gd)])
     assert np.array_equal(raw, want)
 
@@ -126,7 +127,8 @@ def test_asan_polygon_rollout_backward(emu_mod, tmp_path, scene):
                          actions=case["actions"], ab=case["ab"], w=case["w"])
     h, geom = emu.oracle_scene(lib, case["make"]())
     d, k, err = dyn.copy(), np.array(case["keys"], np.uint32, copy=True), np.zeros(B, np.uint32)
-    ret, sd, sk = emu.rollout(lib, h, d, k, err, geom, 0, stages, case["actions"], case["ab"], case["w"], E=4)
-    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, stages, case["actions"], case["ab"], case["w"], E=4)
+    ret, sd, sk, tape = emu.rollout(lib, h, d, k, err, geom, 0, stages, case["actions"], case["ab"], case["w"], E=4)
+    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, stages, case["actions"], case["ab"], case["w"], E=4,
+                                  tape=tape)
     want = np.concatenate([x.reshape(-1).view(np.uint8) for x in (d, k, err, ret, ga, gd)])
     assert np.array_equal(raw, want)

@@ -433,6 +433,39 @@ def test_emu_static_part_straddling_chunks_vs_cport(emu_lib, EW, bp):
         assert np.array_equal(g, w)
 
 
+def test_emu_octagon_row_one_env_per_wave_vs_cport(emu_lib):
+    """A scene whose tile fits the LDS at one env per wave only (9 octagon
+    bodies, scene_cases.octagon_row; the library picks that tiling at
+    cotix_scene_create): the kernel logic at EW 1 == the C port over 16 steps,
+    4 envs, contact choices included."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    _build_cport()
+    clib = cport.load()
+    import scene_cases
+    bodies = scene_cases.octagon_row(9)
+    h, geom = emu.oracle_scene(lib, bodies)
+    lib.emu_lds_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.emu_lds_bytes.restype = ctypes.c_long
+    assert lib.emu_lds_bytes(h, 1) <= 160 * 1024 < lib.emu_lds_bytes(h, 2)
+    sc = cport.Scene(clib, bodies)
+    B, T = 4, 16
+    base = np.array([b.dyn() for b in bodies], np.float32)
+    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
+    dyn[1:, 2, :] += np.linspace(-0.2, 0.2, B).astype(np.float32)
+    keys = np.ascontiguousarray(np.stack([np.arange(B) + 9, np.arange(B) * 3 + 2], 1).astype(np.uint32))
+    got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    gch, gcl = emu.step_ex(lib, h, *got, geom, 0, T, 1 | 4 | 16, len(bodies), E=1)
+    wch, wcl = sc.step_ex(*want, T, 1 | 4 | 16, trace=True)
+    assert (wcl >= 0).sum() > 4 * T  # neighbours in contact
+    assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)
+
+
 @pytest.mark.parametrize("EW", [1, 4, 8])
 def test_emu_robocup_moving_static_bodies_vs_cport(emu_lib, EW):
     """The analytic program with infinite-mass bodies that do move: restarts

@@ -180,3 +180,30 @@ def test_step_obs_from_kernel_equals_observe(torch_cuda):
     assert bool((outs[0] == 7.0).all())  # never written
     with pytest.raises(ValueError):
         a.step(1, obs_out=torch.empty(999, 5, 6, device="cuda"))
+
+
+def test_step_launch_follows_env_attributes(torch_cuda):
+    """BatchedEnv.step's prepared launch is rebuilt when a public attribute it
+    copies changes between steps (dt, autoreset, the scenario's stages): each
+    step equals the same step of a twin env driven through World.step with
+    the attribute's current value."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    from parallax_amd import _ffi
+    a = pa.BatchedEnv(pa.RoboCupEnv(batch=512, device="cuda", perturb=True), autoreset=True)
+    b = pa.BatchedEnv(pa.RoboCupEnv(batch=512, device="cuda", perturb=True), autoreset=True)
+    a.reset()
+    b.reset()
+    plan = [(1e-2, True, None), (5e-3, True, None), (5e-3, False, None), (2e-2, True, _ffi.STAGE_EULER),
+            (1e-2, True, None)]
+    stages0 = a.scenario.stages
+    for dt, ar, st in plan:
+        a.dt, a.autoreset = dt, ar
+        a.scenario.stages = stages0 if st is None else st
+        o = a.step(2)
+        kw = dict(dyn_reset=b.scenario.dyn_reset, resets=b.resets) if ar else {}
+        b.world.step(2, dt, stages0 if st is None else st, **kw)
+        ob = b.observation()
+        torch.cuda.synchronize()
+        assert torch.equal(o.view(torch.int32), ob.view(torch.int32)), (dt, ar, st)
+    a.scenario.stages = stages0

@@ -552,8 +552,20 @@ def _gpu_rollout(torch, case, bodies_pa, want_dyn0=True, stages=None, world=None
     ret, saved = pa.rollout_forward(w, acts, case["ab"], case["w"],
                                     stages=pa._ffi.STAGES_ROBOCUP if stages is None else stages)
     ga, gd = pa.rollout_backward(w, saved, want_dyn0=want_dyn0)
-    torch.cuda.synchronize()
+    _check_tape_vs_replay(pa, w, saved, ga, gd)
     return w, ret.cpu().numpy(), ga.cpu().numpy(), (gd.cpu().numpy() if gd is not None else None), saved
+
+
+def _check_tape_vs_replay(pa, world, saved, ga, gd):
+    """The backward from the forward's tape (what the library runs) equals the
+    re-play of the forward (MODE 2) bit for bit, NaN patterns included."""
+    import torch
+    assert saved["tape"] is not None
+    ra, rd = pa.rollout_backward(world, saved, want_dyn0=gd is not None, replay=True)
+    torch.cuda.synchronize()
+    assert same_f32(ga.cpu().numpy(), ra.cpu().numpy()), diff_report(ga.cpu().numpy(), ra.cpu().numpy())
+    if gd is not None:
+        assert same_f32(gd.cpu().numpy(), rd.cpu().numpy()), diff_report(gd.cpu().numpy(), rd.cpu().numpy())
 
 
 def _pa_part(pa, p):
@@ -585,9 +597,9 @@ def test_rollout_grad_box_world_vs_oracle(torch_cuda):
     for e in orc:
         r, oga, ogS = orc[e]
         assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)
-        ok, msg = GC.close(ga[:, e], oga)
+        ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d grad_action %s" % (e, msg)
-        ok, msg = GC.close(gd[:, :, e], ogS)
+        ok, msg = GC.close(gd[:, :, e], ogS, case["tol"], case["name"])
         assert ok, "env %d grad_dyn0 %s" % (e, msg)
 
 
@@ -597,9 +609,9 @@ def _check_grad_vs_oracle(case, ret, ga, gd):
     for e in orc:
         r, oga, ogS = orc[e]
         assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)
-        ok, msg = GC.close(ga[:, e], oga)
+        ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d grad_action %s" % (e, msg)
-        ok, msg = GC.close(gd[:, :, e], ogS)
+        ok, msg = GC.close(gd[:, :, e], ogS, case["tol"], case["name"])
         assert ok, "env %d grad_dyn0 %s" % (e, msg)
 
 
@@ -641,11 +653,13 @@ def test_rollout_grad_lunar_settled_full_size_sampled(torch_cuda):
     acts = torch.tensor(actions, device="cuda")
     ret, saved = pa.rollout_forward(ll.world, acts, 0, w, stages=st)
     ga, gd = pa.rollout_backward(ll.world, saved, want_dyn0=True)
+    _check_tape_vs_replay(pa, ll.world, saved, ga, gd)
     ret, ga, gd = ret.cpu().numpy(), ga.cpu().numpy(), gd.cpu().numpy()
     assert np.isfinite(ga).all(axis=(0, 2)).mean() > 0.9
     envs = list(range(0, B, B // 8))
     case = dict(make=lambda: P.lunar_lander_bodies(prng.PRNGKey(0)), S0=S0[envs], keys=keys[envs],
-                actions=actions[:, envs], w=w, ab=0, step=P.lunar_lander_step)
+                actions=actions[:, envs], w=w, ab=0, step=P.lunar_lander_step, tol=GC.POLYGON_TOL,
+                name="lunar_settled_4096")
     _check_grad_vs_oracle(case, ret[envs], ga[:, envs], gd[:, :, envs])
 
 
@@ -660,13 +674,15 @@ def test_rollout_grad_polygon_box_vs_oracle(torch_cuda):
 
 
 def test_rollout_grad_quad_row_vs_oracle(torch_cuda):
-    """Nine polygons of one contact type: the contact VJPs inside phase G
-    (one env per wave: the scene's tile exceeds the LDS at the default four)."""
+    """Nine polygons of one contact type: the contact VJPs inside phase G, at
+    the scene's default tiling (2 envs per wave: its tile exceeds the LDS at
+    4, so cotix_scene_create picks 2)."""
     torch = torch_cuda
     import parallax_amd as pa
     import grad_cases as GC
     case = GC.quad_row_case(8, 6, seed=0)
-    _, ret, ga, gd, _ = _gpu_rollout(torch, case, _pa_bodies(pa, case["make"]()), envs_per_wave=1)
+    w, ret, ga, gd, _ = _gpu_rollout(torch, case, _pa_bodies(pa, case["make"]()))
+    assert w.scene.variant()["envs_per_wave"] == 2
     _check_grad_vs_oracle(case, ret, ga, gd)
 
 
@@ -681,7 +697,7 @@ def test_rollout_grad_robocup_vs_oracle(torch_cuda):
         r, oga, _ = orc[e]
         assert (np.isnan(ret[e]) and np.isnan(r)) or np.float32(ret[e]).view(np.uint32) == np.float32(r).view(
             np.uint32), (e, ret[e], r)
-        ok, msg = GC.close(ga[:, e], oga)
+        ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d %s" % (e, msg)
 
 
@@ -705,7 +721,7 @@ def test_rollout_config5_full_size_vs_vjp_oracle(torch_cuda):
         r, oga, _ = orc[e]
         assert (np.isnan(ret[e]) and np.isnan(r)) or np.float32(ret[e]).view(np.uint32) == np.float32(r).view(
             np.uint32), (e, ret[e], r)
-        ok, msg = GC.close(ga[:, e], oga)
+        ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d %s" % (e, msg)
         finite += int(np.isfinite(oga).all())
     assert finite > 0
@@ -731,8 +747,9 @@ def test_rollout_config5_full_size_vs_emulation(torch_cuda):
     dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
     keys = np.array(case["keys"], np.uint32, copy=True)
     err = np.zeros(B, np.uint32)
-    eret, esd, esk = emu.rollout(lib, h, dyn, keys, err, geom, 0, 21, case["actions"], case["ab"], case["w"])
-    ega, egd = emu.rollout_backward(lib, h, esd, esk, geom, 0, 21, case["actions"], case["ab"], case["w"])
+    eret, esd, esk, etape = emu.rollout(lib, h, dyn, keys, err, geom, 0, 21, case["actions"], case["ab"], case["w"])
+    ega, egd = emu.rollout_backward(lib, h, esd, esk, geom, 0, 21, case["actions"], case["ab"], case["w"],
+                                    tape=etape)
     assert same_f32(w.dyn.cpu().numpy(), dyn)
     assert same_f32(saved["dyn"].cpu().numpy(), esd)
     assert same_f32(ret, eret)
@@ -994,6 +1011,36 @@ def test_rank_shards_concatenate_to_single_run(torch_cuda):
     assert not torch.equal(parts[0][0][4], parts[1][0][4])
 
 
+def test_config4_global_size_shards_concatenate(torch_cuda):
+    """BASELINE config 4 at its full global size on one GPU: the 8 rank shards
+    of 8192 envs, each BUILT from its global env ids 0..65535 as bench.py's
+    rank r does (RoboCupEnv(env_offset=8192 r, total_envs=65536), restarts on
+    the error trip), stepped 2 x 8 fused steps, concatenate to ONE
+    65,536-env launch bit for bit: state, keys, errors, restart counts and
+    every collider choice (chosen partner per body, winning candidate per
+    cell) of the second launch."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    N, R, T = 65536, 8, 8
+    n = N // R
+
+    def run(env):
+        resets = torch.zeros(env.world.B, dtype=torch.int32, device="cuda")
+        env.world.step(T, 1e-2, env.stages, dyn_reset=env.dyn_reset, resets=resets)
+        tr = {}
+        env.world.step(T, 1e-2, env.stages, dyn_reset=env.dyn_reset, resets=resets, trace=tr)
+        return env.world.dyn, env.world.keys, env.world.err, resets, tr["chosen"], tr["cells"]
+
+    full = run(pa.RoboCupEnv(batch=N, device="cuda", perturb=True))
+    shards = [run(pa.RoboCupEnv(batch=n, device="cuda", perturb=True, env_offset=r * n, total_envs=N))
+              for r in range(R)]
+    torch.cuda.synchronize()
+    for q, cat_dim in enumerate((2, 0, 0, 0, 2, 3)):
+        got = torch.cat([sh[q] for sh in shards], cat_dim)
+        assert torch.equal(got.view(torch.int32), full[q].view(torch.int32)), q
+    assert int(full[3].sum()) > N  # the restarts ran (most envs trip within 2 steps)
+
+
 def test_contracts_and_check_state_vs_oracle(torch_cuda):
     """Row f4 as a parity row: the device state check (cotix_check_state, the
     invariant "NaN or invalid value encountered", cotix/_design_by_contract.py:
@@ -1161,24 +1208,31 @@ def _world_from_oracle(pa, torch, bodies, B, keys):
     return pa.World(out, B, "cuda", torch.tensor(u32_to_i32(keys), device="cuda"))
 
 
-@pytest.mark.parametrize("scene", ["aabb_poly", "aabb_circle_poly", "straddle", "straddle_ew1"])
+@pytest.mark.parametrize("scene", ["aabb_poly", "aabb_circle_poly", "straddle", "straddle_ew1", "octagons9"])
 def test_generic_polygon_scenes_vs_cport(torch_cuda, cport_lib, scene):
     """The generic step programs on the GPU (cxk::launch_fnset: polygon-only
     GJK/EPA for the straddling-part scene, AABB x polygon, circle x polygon)
     against the C port: 512 envs x 24 steps, state, keys, errors and every
     contact choice.  straddle_ew1: one env per wave, where the static floor
-    straddles phase T's first two vertex-item chunks."""
+    straddles phase T's first two vertex-item chunks.  octagons9: nine
+    octagon bodies, whose tile fits the LDS at one env per wave only -- the
+    tiling the library picks at scene creation."""
     torch = torch_cuda
     import parallax_amd as pa
     cport, lib = cport_lib
     import scene_cases
-    bodies = scene_cases.straddle_scene(4.0) if scene.startswith("straddle") else scene_cases.mixed_scene(
-        scene == "aabb_circle_poly")
+    if scene == "octagons9":
+        bodies = scene_cases.octagon_row(9)
+    else:
+        bodies = scene_cases.straddle_scene(4.0) if scene.startswith("straddle") else scene_cases.mixed_scene(
+            scene == "aabb_circle_poly")
     B, T = 512, 24
     keys = np.ascontiguousarray(np.stack([np.arange(B) + 3, np.arange(B) * 5 + 1], 1).astype(np.uint32))
     w = _world_from_oracle(pa, torch, bodies, B, keys)
     if scene == "straddle_ew1":
         w.set_variant(1)
+    if scene == "octagons9":
+        assert w.scene.variant()["envs_per_wave"] == 1
     base = np.array([b.dyn() for b in bodies], np.float32)
     dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
     dyn[0, 0, :] += np.linspace(-0.6, 0.6, B).astype(np.float32)

@@ -22,14 +22,25 @@ def emu_lib():
     return emu, emu.load()
 
 
+def _both_backwards(emu, lib, h, sd, sk, tape, geom, stages, case, E):
+    """The tape backward (MODE 4, what the library runs) and the re-play
+    (MODE 2): bit for bit the same gradients, NaN patterns included."""
+    args = (geom, 0, stages, case["actions"], case["ab"], case["w"])
+    ga, gd = emu.rollout_backward(lib, h, sd, sk, *args, E=E, tape=tape)
+    ra, rd = emu.rollout_backward(lib, h, sd, sk, *args, E=E)
+    assert np.array_equal(ga.view(np.uint32), ra.view(np.uint32)), "grad_action: tape != re-play"
+    assert np.array_equal(gd.view(np.uint32), rd.view(np.uint32)), "grad_dyn0: tape != re-play"
+    return ga, gd
+
+
 def _emu_run(emu, lib, case, E=4):
     h, geom = emu.oracle_scene(lib, case["make"]())
     dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
     keys = np.array(case["keys"], np.uint32, copy=True)  # the kernel advances keys in place
     err = np.zeros(dyn.shape[2], np.uint32)
-    ret, sd, sk = emu.rollout(lib, h, dyn, keys, err, geom, 0, 1 | 4 | 16, case["actions"], case["ab"], case["w"],
-                              E=E)
-    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, 1 | 4 | 16, case["actions"], case["ab"], case["w"], E=E)
+    ret, sd, sk, tape = emu.rollout(lib, h, dyn, keys, err, geom, 0, 1 | 4 | 16, case["actions"], case["ab"],
+                                    case["w"], E=E)
+    ga, gd = _both_backwards(emu, lib, h, sd, sk, tape, geom, 1 | 4 | 16, case, E)
     return ret, ga, gd, dyn
 
 
@@ -69,9 +80,9 @@ def test_emu_rollout_box_world(emu_lib, E):
     for e in range(B):
         r, oga, ogS = orc[e]
         assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)  # bit-exact
-        ok, msg = GC.close(ga[:, e], oga)
+        ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d grad_action: %s" % (e, msg)
-        ok, msg = GC.close(gd[:, :, e], ogS)
+        ok, msg = GC.close(gd[:, :, e], ogS, case["tol"], case["name"])
         assert ok, "env %d grad_dyn0: %s" % (e, msg)
     assert np.abs(ga).max() > 0
 
@@ -90,7 +101,7 @@ def test_emu_rollout_robocup(emu_lib):
         same = (np.isnan(ret[e]) and np.isnan(r)) or np.float32(ret[e]).view(np.uint32) == np.float32(r).view(
             np.uint32)
         assert same, (e, ret[e], r)
-        ok, msg = GC.close(ga[:, e], oga)
+        ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d: %s" % (e, msg)
         finite += int(np.isfinite(oga).all())
     assert finite >= 1
@@ -137,24 +148,28 @@ def test_oracle_grad_polygons_vs_finite_differences(scene):
     assert nontrivial >= 8
 
 
-def _emu_run_st(emu, lib, case, stages, E=4):
-    h, geom = emu.oracle_scene(lib, case["make"]())
+def _emu_run_st(emu, lib, case, stages, E=4, params=None):
+    from cotix_oracle import params as _params
+    with _params.use(params):  # (the scene's own draws, LunarLander's terrain, in the block's layout)
+        bodies = case["make"]()
+    h, geom = emu.oracle_scene(lib, bodies, params)
     dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
     keys = np.array(case["keys"], np.uint32, copy=True)
     err = np.zeros(dyn.shape[2], np.uint32)
-    ret, sd, sk = emu.rollout(lib, h, dyn, keys, err, geom, 0, stages, case["actions"], case["ab"], case["w"], E=E)
-    ga, gd = emu.rollout_backward(lib, h, sd, sk, geom, 0, stages, case["actions"], case["ab"], case["w"], E=E)
+    ret, sd, sk, tape = emu.rollout(lib, h, dyn, keys, err, geom, 0, stages, case["actions"], case["ab"], case["w"],
+                                    E=E)
+    ga, gd = _both_backwards(emu, lib, h, sd, sk, tape, geom, stages, case, E)
     return ret, ga, gd
 
 
-def _check_vs_oracle(case, ret, ga, gd):
-    orc = GC.oracle(case)
+def _check_vs_oracle(case, ret, ga, gd, params=None):
+    orc = GC.oracle(case, params=params)
     for e in orc:
         r, oga, ogS = orc[e]
         assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)  # bit-exact
-        ok, msg = GC.close(ga[:, e], oga)
+        ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d grad_action: %s" % (e, msg)
-        ok, msg = GC.close(gd[:, :, e], ogS)
+        ok, msg = GC.close(gd[:, :, e], ogS, case["tol"], case["name"])
         assert ok, "env %d grad_dyn0: %s" % (e, msg)
 
 
@@ -226,5 +241,24 @@ def test_emu_rollout_return_terms(emu_lib, nterms):
     for e in range(B):
         r, oga, ogS = orc[e]
         assert np.float32(ret[e]).view(np.uint32) == np.float32(r).view(np.uint32), (e, ret[e], r)
-        ok, msg = GC.close(ga[:, e], oga)
+        ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d grad_action: %s" % (e, msg)
+
+
+@pytest.mark.parametrize("sfx", ["_part", "_alt"])
+@pytest.mark.parametrize("scene", ["box", "lunar", "poly_box"])
+def test_emu_rollout_under_param_sets(emu_lib, scene, sfx):
+    """The differentiable rollout under a non-default parameter block
+    (tests/param_sets.py: the partitionable PRNG layout; Baumgarte 0.2 / 0.02,
+    bernoulli p 0.3, GJK capped at 1 step, EPA at 3 iterations): the backward
+    reads the scene's Baumgarte constants, narrowphase caps and (re-play) PRNG
+    layout -- emulation (tape == re-play) against the VJP oracle run under the
+    same block, returns bit for bit."""
+    from param_sets import oracle_params
+    emu, lib = emu_lib
+    prm = oracle_params(sfx)
+    case, stages = {"box": (GC.box_case(4, 12, seed=4), 1 | 4 | 16),
+                    "lunar": (GC.lunar_case(4, 8, seed=1), LUNAR_STAGES),
+                    "poly_box": (GC.poly_box_case(4, 8, seed=2), 1 | 4 | 16)}[scene]
+    ret, ga, gd = _emu_run_st(emu, lib, case, stages, params=prm)
+    _check_vs_oracle(case, ret, ga, gd, params=prm)

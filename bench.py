@@ -262,10 +262,27 @@ def roofline(scenario, B, substeps, launch_ms, nb, layout="legacy"):
 # CPU baselines (oracle C port: test infrastructure, timed here as the
 # reported non-target baseline; never on the product path)
 # ---------------------------------------------------------------------------
+def host_cpu():
+    """The host CPU the baselines ran on (model name from /proc/cpuinfo; the
+    box's logical CPU count -- the threads used are each baseline's cores)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.lower().startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "host_logical_cpus": os.cpu_count()}
+
+
 def cpu_baseline(scenario, seconds):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from cotix_oracle import cport
-    return cport.time_baseline(scenario, seconds)
+    out = cport.time_baseline(scenario, seconds)
+    out.update(host_cpu())
+    return out
 
 
 def cpu_config1(seconds=3.0):
@@ -287,8 +304,9 @@ def cpu_config1(seconds=3.0):
         sc.step(dyn, keys, err, 10000, cport.STAGES_LUNAR, geom, nthreads=1)
         n += 10000
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "%d x the 10,000-step trajectory, C oracle port, 1 thread, %.1f s" % (n // 10000, dt)}
+    return dict({"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                 "sample": "%d x the 10,000-step trajectory, C oracle port, 1 thread, %.1f s" % (n // 10000, dt)},
+                **host_cpu())
 
 
 def cpu_baseline_grad(T, seconds):
@@ -314,28 +332,32 @@ def cpu_baseline_grad(T, seconds):
     while dt < 0.5 * seconds and B < 4096:
         B = int(min(4096, max(2 * B, B * seconds / max(dt, 1e-3))))
         dt = run(B)
-    return {"value": B * T / dt, "unit": "env-steps/s (with d ret/d action)", "cores": nthreads, "kind": "port",
-            "sample": "%d RoboCup envs x %d-step rollout, gradient by central differences (%d perturbed rollouts "
-                      "per env) of the C oracle port, OpenMP %d threads, %.1f s" % (B, T, 4 * T, nthreads, dt)}
+    return dict({"value": B * T / dt, "unit": "env-steps/s (with d ret/d action)", "cores": nthreads, "kind": "port",
+                 "sample": "%d RoboCup envs x %d-step rollout, gradient by central differences (%d perturbed "
+                           "rollouts per env) of the C oracle port, OpenMP %d threads, %.1f s"
+                           % (B, T, 4 * T, nthreads, dt)}, **host_cpu())
 
 
 # ---------------------------------------------------------------------------
 # secondary figures (rank 0, after the headline)
 # ---------------------------------------------------------------------------
-def sub_step(pa, dev, name, B, substeps, steps, warmup, key=None):
+def sub_step(pa, dev, name, B, substeps, steps, warmup, key=None, layout="legacy"):
     """A secondary figure; `key` names its committed PMC pass
     (profiles/latest_pmc_<key>.json, default the scenario name), which must be
     of the same stretch of the trajectory (warm-up launches) for LunarLander,
-    whose cost changes when the landers touch down."""
+    whose cost changes when the landers touch down.  layout: the scene's PRNG
+    layout (cotix_params; the partitionable one is JAX >= 0.5's default)."""
     key = key or name
-    scen = make_scenario(pa, name, dev, B)
+    params = pa.Params(prng_layout=layout)
+    scen = make_scenario(pa, name, dev, B, params=params)
     env = pa.BatchedEnv(scen, autoreset=True)
     env.reset()
     wall, ev_ms = timed_launches(lambda: env.step(substeps), steps, warmup, separate=substeps == 1)
     out = {"workload": WORKLOAD[name] % B, "substeps_per_launch": substeps, "launches": steps,
            "value": B * substeps * steps / wall, "unit": "env-steps/s", "launch_ms": ev_ms,
-           "hbm_GBs": bytes_per_env(name, len(scen.bodies)) * B / (ev_ms * 1e-3) / 1e9}
-    v = valu_roofline(key, B, substeps, ev_ms, warmup if name == "lunar" else None)
+           "hbm_GBs": bytes_per_env(name, len(scen.bodies)) * B / (ev_ms * 1e-3) / 1e9, "prng_layout": layout,
+           "kernel_variant": scen.world.scene.variant()}
+    v = valu_roofline(key, B, substeps, ev_ms, warmup if name == "lunar" else None, layout)
     if v is not None:  # the committed PMC pass of this workload (profiles/latest_pmc_<key>.json)
         out["valu"] = {"achieved": v["valu_instr_per_launch"] / (ev_ms * 1e-3) / 1e9,
                        "frac": v["valu_instr_per_launch"] / (ev_ms * 1e-3) / VALU_PEAK_WAVE_INSTR_S,
@@ -347,7 +369,7 @@ def sub_step(pa, dev, name, B, substeps, steps, warmup, key=None):
         ch = tr["chosen"]  # [step][body][B], j* of body i (cotix/_colliders.py:274-295; i itself: none)
         own = torch.arange(ch.shape[1], device=ch.device, dtype=ch.dtype)[None, :, None]
         out["contact_env_fraction"] = float((ch != own).any(1).any(0).float().mean().item())
-    out.update(finite_stats(pa, make_scenario(pa, name, dev, B), 1, 64))
+    out.update(finite_stats(pa, make_scenario(pa, name, dev, B, params=params), 1, 64))
     return out
 
 
@@ -558,10 +580,15 @@ def main():
     # the CPU baseline and the secondary figures: one-GPU runs only (an N-GPU
     # line carries the headline; the other ranks would idle in the barrier)
     single = world_size == 1
-    if rank == 0 and single and a.extras == "auto":
-        out["workload_stats"] = finite_stats(pa, make_scenario(pa, a.scenario, dev, B), 1, 64)
+    if rank == 0 and single and a.extras == "auto":  # (the headline's own workload: its PRNG layout)
+        out["workload_stats"] = finite_stats(pa, make_scenario(pa, a.scenario, dev, B, params=params), 1, 64)
+        out["workload_stats"]["prng_layout"] = a.prng_layout
     if rank == 0 and single and a.extras == "auto" and a.scenario == "robocup":
         out["k1"] = sub_step(pa, dev, "robocup", B, 1, 2000, 50)
+        # the headline scene in JAX >= 0.5's partitionable threefry layout (the
+        # reference pins no JAX version, pyproject.toml:16)
+        out["robocup_partitionable"] = sub_step(pa, dev, "robocup", B, a.substeps, 10, 2, key="robocup_part",
+                                                layout="partitionable")
         out["finite_scene"] = sub_step(pa, dev, "box", B, a.substeps, 10, 2)
         out["lunar"] = sub_step(pa, dev, "lunar", B, a.substeps, 10, 2)  # airborne: driver steps 128-768
         # the landers settled on the terrain (first touch-down ~770, a bounce, settled from
@@ -576,6 +603,9 @@ def main():
     # host thread that launches the GPU figures (the K = 1 loop is launch-bound)
     if rank == 0 and single and a.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline(a.scenario if a.scenario != "box" else "robocup", a.cpu_seconds)
+        if a.extras == "auto" and a.scenario == "robocup":  # the sub-figures' own baselines (configs 2 and 5)
+            out["lunar"]["cpu_baseline"] = cpu_baseline("lunar", a.cpu_seconds / 2)
+            out["grad"]["cpu_baseline"] = cpu_baseline_grad(64, a.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
@@ -691,8 +721,9 @@ def main_grad(a):
     nb = 7 if box else (4 if lunar else 5)
     key = "grad_box" if box else ("grad_lunar" if lunar else "grad")
     # algorithmic HBM bytes of the backward launch per env-step: saved state
-    # (nb x 6 f32) + key (2 u32) + action (2 f32) read, grad_action (2 f32) written
-    bwd_bytes = (nb * 6 * 4 + 8 + 8 + 8) * B * T
+    # (nb x 6 f32) + key (2 u32) + action (2 f32) + the tape's resolution words
+    # (5 per body) read, grad_action (2 f32) written
+    bwd_bytes = (nb * 6 * 4 + 8 + 8 + nb * 5 * 4 + 8) * B * T
     achieved = bwd_bytes / (r["bwd_ms"] * 1e-3) / 1e9
     out = {
         "metric": "differentiable %d-step %s rollout, %d envs/GPU: env-steps/s with d(return)/d(action)"
@@ -734,11 +765,11 @@ def main_grad(a):
             "unit": "G wave-instr/s",
             "frac": None,
             "traffic": None,
-            "kernel": "step_kernel<4,1,2> (backward re-play)",
+            "kernel": "step_kernel<4,F,4> (backward from the forward's tape)",
             "launch_ms": r["bwd_ms"],
             "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                     "alg_bytes_per_launch": bwd_bytes},
-            "note": "VALU/latency-bound (the backward re-plays each step's forward)",
+            "note": "VALU/latency-bound (per step: Euler, world parts, the tape's resolutions, the VJP chain)",
         },
     }
     v = grad_valu(key, B, T, r["fwd_ms"], r["bwd_ms"])

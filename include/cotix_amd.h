@@ -218,6 +218,8 @@ int cotix_step_ex(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err,
  * kernel evaluates after every env-step.  s = the env's state words
  * [n_bodies*6] (body-major: px, py, vx, vy, angle, angular_velocity):
  *   judge(s)      = sum_k rate_w[k] * s[k]                       (reward rate)
+ *                   (+ piece_r(s) while rate region r is the first rate region
+ *                   holding s: piecewise linear, below)
  *   end_reward(s) = sum_k end_w[k] * s[k]  (+ region_reward[r] for the first
  *                   region r that holds s)
  *   is_done(s)    = some region holds s, or (done_on_error and the env's
@@ -237,6 +239,18 @@ typedef struct cotix_judge {
   float region_hi[COTIX_JUDGE_REGIONS][6];
   float region_reward[COTIX_JUDGE_REGIONS];
   int done_on_error;
+  /* piecewise-linear reward rate: n_rate_regions boxes over one body's state
+   * (held as the done regions are; they do not end the episode).  While rate
+   * region r is the first holding s, piece_r(s) = sum_k rate_region_w[r][k] *
+   * s[k] (nonzero weights in k order, from the first term, at most 8) +
+   * rate_region_bias[r] (if nonzero) is added: judge(s) = base + piece_r when
+   * both have terms, else whichever has one (none: 0) */
+  int n_rate_regions;
+  int rate_region_body[COTIX_JUDGE_REGIONS];
+  float rate_region_lo[COTIX_JUDGE_REGIONS][6];
+  float rate_region_hi[COTIX_JUDGE_REGIONS][6];
+  float rate_region_w[COTIX_JUDGE_REGIONS][COTIX_MAX_STATE_WORDS];
+  float rate_region_bias[COTIX_JUDGE_REGIONS];
 } cotix_judge;
 
 /* Device control: AbstractControl (cotix/_controls.py:16-27) whose dense
@@ -244,12 +258,18 @@ typedef struct cotix_judge {
  * from that body's state s[6] and added after Euler (world.forward(state,
  * signal), cotix/_envs.py:72-75):
  *   dv[i] = sum_q gain[i][q] * (target[i][q] - s[q])  (nonzero gains, q order,
- *           from the first term)  + bias[i] (if nonzero) */
+ *           from the first term)  + bias[i] (if nonzero)
+ * and with saturate != 0 the saturating (clipped) form
+ *   dv[i] = clip(dv[i], clip_lo[i], clip_hi[i])  (jnp.clip: min(hi, max(lo, x)),
+ *           NaN propagates) */
 typedef struct cotix_control {
   int body;
   float gain[2][6];
   float target[2][6];
   float bias[2];
+  int saturate;
+  float clip_lo[2];
+  float clip_hi[2];
 } cotix_control;
 
 /* AbstractEnvironment.eval (cotix/_envs.py:37-132) fused into ONE launch:

@@ -64,11 +64,15 @@ class LinearJudge:
     first term; a region holds the state when it is strictly inside every
     bound."""
 
-    def __init__(self, rate_w=None, end_w=None, regions=(), done_on_error=False):
+    def __init__(self, rate_w=None, end_w=None, regions=(), done_on_error=False, rate_regions=()):
         self.rate_terms = sorted((int(k), F(w)) for k, w in dict(rate_w or {}).items() if F(w) != 0)
         self.end_terms = sorted((int(k), F(w)) for k, w in dict(end_w or {}).items() if F(w) != 0)
         self.regions = [(int(b), [F(v) for v in lo], [F(v) for v in hi], F(r)) for b, lo, hi, r in regions]
         self.done_on_error = bool(done_on_error)
+        # the rate's pieces over non-terminal boxes (body, lo, hi, rate_w, bias): piecewise linear
+        self.rate_regions = [(int(b), [F(v) for v in lo], [F(v) for v in hi],
+                              sorted((int(k), F(w)) for k, w in dict(pw or {}).items() if F(w) != 0), F(pb))
+                             for b, lo, hi, pw, pb in rate_regions]
 
     @staticmethod
     def _s(state, k):
@@ -82,15 +86,27 @@ class LinearJudge:
                 acc = t if acc is None else F(acc + t)
         return F(0.0) if acc is None else acc
 
-    def region(self, state):
-        for r, (b, lo, hi, _) in enumerate(self.regions):
+    def region(self, state, boxes=None):
+        for r, (b, lo, hi) in enumerate(x[:3] for x in (self.regions if boxes is None else boxes)):
             d = state[0][b].dyn()
             if all(bool(F(lo[q]) < F(d[q])) and bool(F(d[q]) < F(hi[q])) for q in range(6)):
                 return r
         return -1
 
     def rate(self, state, sig):
-        return self._lin(state, self.rate_terms)
+        """base (+ the piece of the first rate region holding the state): each
+        a sum from its first term; base + piece when both have terms"""
+        acc = self._lin(state, self.rate_terms) if self.rate_terms else None
+        r = self.region(state, self.rate_regions)
+        if r >= 0:
+            terms, b = self.rate_regions[r][3:]
+            with np.errstate(all="ignore"):
+                pc = self._lin(state, terms) if terms else None
+                if b != 0:
+                    pc = b if pc is None else F(pc + b)
+                if pc is not None:
+                    acc = pc if acc is None else F(acc + pc)
+        return F(0.0) if acc is None else acc
 
     def is_done(self, state, sig):
         err = state[2] if len(state) > 2 else 0
@@ -109,12 +125,13 @@ class AffineControl:
     """Restatement of the device control (include/cotix_amd.h cotix_control):
     dv[i] = sum_q gain[i][q] * (target[i][q] - s[q]) (+ bias[i]) on `body`."""
 
-    def __init__(self, body, gain=None, target=None, bias=(0.0, 0.0)):
+    def __init__(self, body, gain=None, target=None, bias=(0.0, 0.0), clip=None):
         z = [[0.0] * 6, [0.0] * 6]
         self.body = int(body)
         self.gain = [[F(v) for v in row] for row in (gain or z)]
         self.target = [[F(v) for v in row] for row in (target or z)]
         self.bias = [F(v) for v in bias]
+        self.clip = None if clip is None else [(F(lo), F(hi)) for lo, hi in clip]  # the saturating form
 
     def dv(self, state):
         s = state[0][self.body].dyn()
@@ -128,7 +145,12 @@ class AffineControl:
                         acc = t if acc is None else F(acc + t)
                 if self.bias[i] != 0:
                     acc = self.bias[i] if acc is None else F(acc + self.bias[i])
-                out.append(F(0.0) if acc is None else acc)
+                acc = F(0.0) if acc is None else acc
+                if self.clip is not None:  # jnp.clip (jax 0.4.x): minimum(hi, maximum(lo, x))
+                    from .geometry import clip as _clip
+                    lo, hi = self.clip[i]
+                    acc = F(_clip(acc, lo, hi))
+                out.append(acc)
         return tuple(out)
 
     def __call__(self, state):

@@ -32,12 +32,16 @@ class CotixJudge(ctypes.Structure):
     _fields_ = [("rate_w", _F * MAX_STATE_WORDS), ("end_w", _F * MAX_STATE_WORDS), ("n_regions", _I),
                 ("region_body", _I * JUDGE_REGIONS), ("region_lo", (_F * 6) * JUDGE_REGIONS),
                 ("region_hi", (_F * 6) * JUDGE_REGIONS), ("region_reward", _F * JUDGE_REGIONS),
-                ("done_on_error", _I)]
+                ("done_on_error", _I), ("n_rate_regions", _I), ("rate_region_body", _I * JUDGE_REGIONS),
+                ("rate_region_lo", (_F * 6) * JUDGE_REGIONS), ("rate_region_hi", (_F * 6) * JUDGE_REGIONS),
+                ("rate_region_w", (_F * MAX_STATE_WORDS) * JUDGE_REGIONS),
+                ("rate_region_bias", _F * JUDGE_REGIONS)]
 
 
 class CotixControl(ctypes.Structure):
     """struct cotix_control (include/cotix_amd.h)."""
-    _fields_ = [("body", _I), ("gain", (_F * 6) * 2), ("target", (_F * 6) * 2), ("bias", _F * 2)]
+    _fields_ = [("body", _I), ("gain", (_F * 6) * 2), ("target", (_F * 6) * 2), ("bias", _F * 2),
+                ("saturate", _I), ("clip_lo", _F * 2), ("clip_hi", _F * 2)]
 
 
 SIGNATURES = {

@@ -185,17 +185,23 @@ CX_HD SceneHdr spec_hdr(const SceneHdr& h) {
 // cotix_control), compacted by the host: the nonzero weights as (word, w)
 // terms in word order -- the sums run over them in that order, starting from
 // the first term
-constexpr int JT = 16, JR = 4;
+constexpr int JT = 16, JR = 4, JRT = 8;
 struct JudgeArgs {
   int on, nrate, nend, nreg, doe;
   uint8_t rate_k[JT], end_k[JT];
   float rate_w[JT], end_w[JT];
   int rbody[JR];
   float lo[JR][6], hi[JR][6], rrew[JR];
+  // the reward rate's pieces (cotix_judge rate regions): region r over body
+  // prbody[r], npr[r] terms (k, w), then the bias when hasb[r]
+  int nrr, prbody[JR], npr[JR], hasb[JR];
+  float prlo[JR][6], prhi[JR][6];
+  uint8_t pr_k[JR][JRT];
+  float pr_w[JR][JRT], pr_b[JR];
 };
 struct CtlArgs {
-  int on, body;
-  float gain[2][6], target[2][6], bias[2];
+  int on, body, sat;
+  float gain[2][6], target[2][6], bias[2], lo[2], hi[2];
 };
 
 // kernel arguments (passed by value)
@@ -833,6 +839,7 @@ CX_DEV cx::v2 control_dv(const KArgs& a, Tile<EW> t, int o, int e) {
         any = true;
       }
     if (a.ctl.bias[i] != 0.0f) acc = any ? acc + a.ctl.bias[i] : a.ctl.bias[i];
+    if (a.ctl.sat) acc = cx::clip_(acc, a.ctl.lo[i], a.ctl.hi[i]);  // the saturating form (jnp.clip)
     dv[i] = acc;
   }
   return cx::v2{dv[0], dv[1]};
@@ -2653,13 +2660,14 @@ CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const Ret
 // RET (rollout forward): the return accumulation after the step, on the
 // env's lane (ret_accum), in the same phase.
 // the rollout forward's tape words of step `step` (tape_words): per (body i,
-// env) item, on the lanes E1 leaves idle (lane >= EW), from phase D's
-// results -- disjoint from every word E1 touches
+// env) item, from the tile's phase-D words of that step -- they live until
+// the next step's phase A resets the collider scratch, so the save runs in
+// the next step's save phase (ph_save) or, for the last step, after the loop
 template <int EW>
 CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   const Lay& L = c.L;
   const int nb = c.nb;
-  for (int w = lane - EW; w >= 0 && w < nb * EW; w += WAVE - EW) {
+  for (int w = lane; w < nb * EW; w += WAVE) {
     const int e = w % EW, i = w / EW, g = env0 + e;
     if (g >= a.B) continue;
     const uint32_t j = t.w(L.rp + RP_W * i + RP_J, e);
@@ -2677,13 +2685,11 @@ CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
 }
 
 template <int EW, bool REC = false, bool RET = false>
-CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso, const RetRegs* rr = nullptr,
-                 int step = 0) {
+CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso, const RetRegs* rr = nullptr) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int nb = c.nb;
   const Lay& L = c.L;
-  if (RET && a.tape != nullptr && (a.stages & COTIX_STAGE_COLLIDER)) tape_save<EW>(a, c, t, env0, lane, step);
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g >= a.B) continue;
@@ -2810,19 +2816,45 @@ CX_DEV float judge_lin(Tile<EW> t, int o, int e, int n, const uint8_t* k, const 
   }
   return acc;
 }
-// the first region holding the env's state (strictly inside every bound), or -1
+// the first of n boxes holding the env's state (strictly inside every bound), or -1
 template <int EW>
-CX_DEV int judge_region(const JudgeArgs& j, Tile<EW> t, int o, int e) {
-  for (int r = 0; r < j.nreg; ++r) {
+CX_DEV int first_box(Tile<EW> t, int o, int e, int n, const int* body, const float (*lo)[6], const float (*hi)[6]) {
+  for (int r = 0; r < n; ++r) {
     bool in = true;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
-      const float v = t.f(o + 6 * j.rbody[r] + q, e);
-      in = in & (j.lo[r][q] < v) & (v < j.hi[r][q]);
+      const float v = t.f(o + 6 * body[r] + q, e);
+      in = in & (lo[r][q] < v) & (v < hi[r][q]);
     }
     if (in) return r;
   }
   return -1;
+}
+// the first (done) region holding the env's state, or -1
+template <int EW>
+CX_DEV int judge_region(const JudgeArgs& j, Tile<EW> t, int o, int e) {
+  return first_box<EW>(t, o, e, j.nreg, j.rbody, j.lo, j.hi);
+}
+// the reward rate: the base sum, plus the piece of the first rate region
+// holding the state -- piecewise linear over the rate regions
+template <int EW>
+CX_DEV float judge_rate(const JudgeArgs& j, Tile<EW> t, int o, int e) {
+  const float base = judge_lin<EW>(t, o, e, j.nrate, j.rate_k, j.rate_w);
+  const int r = j.nrr > 0 ? first_box<EW>(t, o, e, j.nrr, j.prbody, j.prlo, j.prhi) : -1;
+  float pc = 0.0f;  // the piece: its own sum from its first term, then base + piece
+  bool has = false;
+  for (int q = 0; q < JR; ++q) {
+    if (q != r) continue;
+    for (int m = 0; m < j.npr[q]; ++m) {
+      const float term = j.pr_w[q][m] * t.f(o + j.pr_k[q][m], e);
+      pc = has ? pc + term : term;
+      has = true;
+    }
+    if (j.hasb[q]) pc = has ? pc + j.pr_b[q] : j.pr_b[q];
+    has = has || j.hasb[q] != 0;
+  }
+  if (!has) return base;
+  return j.nrate > 0 ? base + pc : pc;
 }
 template <int EW>
 CX_DEV float judge_end(const JudgeArgs& j, Tile<EW> t, int o, int e, int r) {
@@ -2870,7 +2902,7 @@ CX_DEV void ph_J(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
       t.w(L.je, e) = t.w(L.err, e);
     }
     t.w(L.jsn, e) = now ? 1u : 0u;
-    t.f(L.jr, e) = R + judge_lin<EW>(t, L.dyn, e, a.judge.nrate, a.judge.rate_k, a.judge.rate_w) * a.dt;
+    t.f(L.jr, e) = R + judge_rate<EW>(a.judge, t, L.dyn, e) * a.dt;
   }
 }
 // the premature-out state words of the envs flagged by ph_JB / ph_J, item = (word, env)
@@ -2938,8 +2970,10 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
 // differentiable rollout: forward saves, return, backward re-play
 // ---------------------------------------------------------------------------
 // state before step `step` -> save_dyn[step], save_keys[step]
+// (+ the tape words of the step before it, tape_save)
 template <int EW>
 CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+  if (a.tape != nullptr && step > 0 && (a.stages & COTIX_STAGE_COLLIDER)) tape_save<EW>(a, c, t, env0, lane, step - 1);
   const size_t base = (size_t)step * c.nb * 6 * a.B;
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
@@ -3568,7 +3602,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {
-      run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr, step); });
+      run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
       if (a.dyn_reset != nullptr && a.reset_mode == 1) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     } else if (ROLL) {
       run(PH_RET, [&](int l) {
@@ -3588,6 +3622,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       }
     }
   }
+  if (ROLL && a.tape != nullptr && (a.stages & COTIX_STAGE_COLLIDER) && a.n_steps > 0)
+    run(PH_SAVE, [&](int l) { tape_save<EW>(a, c, t, env0, l, a.n_steps - 1); });  // the last step's
   run(PH_STORE, [&](int l) { ph_store<EW, ROLL, EVAL>(a, c, t, env0, l); });
 }
 

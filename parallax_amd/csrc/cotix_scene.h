@@ -384,6 +384,36 @@ inline int pack_judge(const cotix_judge* j, int nw, int nb, JudgeArgs& out, std:
     }
     out.rrew[r] = j->region_reward[r];
   }
+  // the rate's pieces over the rate regions (piecewise-linear reward rate)
+  if (j->n_rate_regions < 0 || j->n_rate_regions > JR) return scene_fail(err, "judge n_rate_regions outside [0, 4]");
+  out.nrr = j->n_rate_regions;
+  for (int r = 0; r < JR; ++r) {
+    const bool live = r < out.nrr;
+    if (live) {
+      if (j->rate_region_body[r] < 0 || j->rate_region_body[r] >= nb)
+        return scene_fail(err, "judge rate region body out of range");
+      out.prbody[r] = j->rate_region_body[r];
+      for (int q = 0; q < 6; ++q) {
+        out.prlo[r][q] = j->rate_region_lo[r][q];
+        out.prhi[r][q] = j->rate_region_hi[r][q];
+      }
+    }
+    for (int k = 0; k < COTIX_MAX_STATE_WORDS; ++k) {
+      const float w = j->rate_region_w[r][k];
+      if (w == 0.0f) continue;
+      if (!live) return scene_fail(err, "judge rate piece for a rate region past n_rate_regions");
+      if (k >= nw) return scene_fail(err, "judge rate piece on a state word beyond the scene's bodies");
+      if (std::isnan(w)) return scene_fail(err, "NaN judge rate piece weight");
+      if (out.npr[r] == JRT) return scene_fail(err, "more than 8 nonzero weights in a rate piece");
+      out.pr_k[r][out.npr[r]] = (uint8_t)k;
+      out.pr_w[r][out.npr[r]++] = w;
+    }
+    if (j->rate_region_bias[r] != 0.0f) {
+      if (!live) return scene_fail(err, "judge rate piece for a rate region past n_rate_regions");
+      out.hasb[r] = 1;
+      out.pr_b[r] = j->rate_region_bias[r];
+    }
+  }
   out.doe = j->done_on_error ? 1 : 0;
   return 0;
 }
@@ -399,7 +429,12 @@ inline int pack_control(const cotix_control* ct, int nb, CtlArgs& out, std::stri
       out.target[i][q] = ct->target[i][q];
     }
     out.bias[i] = ct->bias[i];
+    out.lo[i] = ct->clip_lo[i];
+    out.hi[i] = ct->clip_hi[i];
   }
+  out.sat = ct->saturate ? 1 : 0;
+  if (out.sat && (std::isnan(out.lo[0]) || std::isnan(out.lo[1]) || std::isnan(out.hi[0]) || std::isnan(out.hi[1])))
+    return scene_fail(err, "NaN control clip bound");
   return 0;
 }
 

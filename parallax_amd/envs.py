@@ -89,25 +89,34 @@ class LinearJudge(AbstractJudge):
     """A device AbstractJudge (include/cotix_amd.h cotix_judge): over the env's
     state words s[k] (k = 6 * body + {px, py, vx, vy, angle, angular_velocity})
 
-      judge(s)      = sum_k rate_w[k] * s[k]
+      judge(s)      = sum_k rate_w[k] * s[k]  (+ piece_r(s) in rate region r: piecewise linear)
       end_reward(s) = sum_k end_w[k] * s[k] (+ the reward of the first region holding s)
       is_done(s)    = some region holds s, or (done_on_error and err bits set)
 
     sums over the nonzero weights in k order, from the first term.
     regions: [(body, lo[6], hi[6], reward)], strictly inside every bound
     (NaN never inside, +-inf leaves a word free); at most 4, and at most 16
-    nonzero weights per sum.  The torch methods evaluate the same f32
-    expressions in the same order as the kernel, so the host loop and the
-    fused cotix_eval agree bit for bit."""
+    nonzero weights per sum.  rate_regions: [(body, lo[6], hi[6], rate_w,
+    bias)], boxes held like the regions but not terminal: while rate region r
+    is the first holding s, the reward rate gains piece_r(s) = sum_k w[k] *
+    s[k] (+ bias) (at most 8 nonzero weights, at most 4 rate regions); the
+    rate is base + piece when both have terms.  The torch methods evaluate the
+    same f32 expressions in the same order as the kernel, so the host loop and
+    the fused cotix_eval agree bit for bit."""
 
-    def __init__(self, rate_w=None, end_w=None, regions=(), done_on_error=False):
+    def __init__(self, rate_w=None, end_w=None, regions=(), done_on_error=False, rate_regions=()):
         self.rate = sorted((int(k), _f32(w)) for k, w in dict(rate_w or {}).items() if _f32(w) != 0.0)
         self.end = sorted((int(k), _f32(w)) for k, w in dict(end_w or {}).items() if _f32(w) != 0.0)
         self.regions = [(int(b), [_f32(v) for v in lo], [_f32(v) for v in hi], _f32(r)) for b, lo, hi, r in regions]
         self.done_on_error = bool(done_on_error)
+        self.rate_regions = [(int(b), [_f32(v) for v in lo], [_f32(v) for v in hi],
+                              sorted((int(k), _f32(w)) for k, w in dict(pw or {}).items() if _f32(w) != 0.0),
+                              _f32(pb)) for b, lo, hi, pw, pb in rate_regions]
         if len(self.rate) > 16 or len(self.end) > 16 or len(self.regions) > _ffi.JUDGE_REGIONS:
             raise ValueError("LinearJudge: at most 16 nonzero weights per sum and 4 regions")
-        if any(len(lo) != 6 or len(hi) != 6 for _, lo, hi, _ in self.regions):
+        if len(self.rate_regions) > _ffi.JUDGE_REGIONS or any(len(t) > 8 for *_, t, _ in self.rate_regions):
+            raise ValueError("LinearJudge: at most 4 rate regions of at most 8 nonzero weights")
+        if any(len(lo) != 6 or len(hi) != 6 for _, lo, hi, *_ in self.regions + self.rate_regions):
             raise ValueError("LinearJudge: region bounds are 6 words (one body's state)")
 
     def c_struct(self):
@@ -124,6 +133,15 @@ class LinearJudge(AbstractJudge):
                 j.region_hi[r][q] = hi[q]
             j.region_reward[r] = rew
         j.done_on_error = int(self.done_on_error)
+        j.n_rate_regions = len(self.rate_regions)
+        for r, (body, lo, hi, terms, b) in enumerate(self.rate_regions):
+            j.rate_region_body[r] = body
+            for q in range(6):
+                j.rate_region_lo[r][q] = lo[q]
+                j.rate_region_hi[r][q] = hi[q]
+            for k, w in terms:
+                j.rate_region_w[r][k] = w
+            j.rate_region_bias[r] = b
         return j
 
     @staticmethod
@@ -137,12 +155,14 @@ class LinearJudge(AbstractJudge):
             acc = t if acc is None else acc + t
         return torch.zeros_like(state.dyn[0, 0, :]) if acc is None else acc
 
-    def _region(self, state):
-        """index of the first region holding the state, -1 for none ([B] int)."""
+    def _region(self, state, boxes=None):
+        """index of the first region (or box of `boxes`) holding the state, -1
+        for none ([B] int)."""
+        boxes = self.regions if boxes is None else boxes
         B = state.dyn.shape[2]
         r_of = torch.full((B,), -1, dtype=torch.int64, device=state.dyn.device)
-        for r in reversed(range(len(self.regions))):
-            b, lo, hi, _ = self.regions[r]
+        for r in reversed(range(len(boxes))):
+            b, lo, hi = boxes[r][:3]
             inside = torch.ones(B, dtype=torch.bool, device=state.dyn.device)
             for q in range(6):
                 v = state.dyn[b, q, :]
@@ -152,7 +172,20 @@ class LinearJudge(AbstractJudge):
         return r_of
 
     def __call__(self, state, control_signal):
-        return self._lin(state, self.rate)
+        acc = None if not self.rate else self._lin(state, self.rate)
+        if not self.rate_regions:
+            return self._lin(state, self.rate)
+        r_of = self._region(state, self.rate_regions)
+        out = torch.zeros_like(state.dyn[0, 0, :]) if acc is None else acc
+        for r, (_, _, _, terms, b) in enumerate(self.rate_regions):
+            if not terms and b == 0.0:
+                continue
+            pc = None if not terms else self._lin(state, terms)
+            if b != 0.0:
+                bt = torch.tensor(b, dtype=torch.float32, device=out.device)
+                pc = bt.expand_as(out) if pc is None else pc + bt
+            out = torch.where(r_of == r, pc if acc is None else acc + pc, out)
+        return out
 
     def is_done(self, state, control_signal):
         d = self._region(state) >= 0
@@ -174,14 +207,18 @@ class AffineControl(AbstractControl):
     signal is the velocity impulse dv[i] = sum_q gain[i][q] * (target[i][q] -
     s[q]) (+ bias[i]) on `body`, from that body's state s before each
     env-step (nonzero gains in q order from the first term, bias last when
-    nonzero).  Stateless."""
+    nonzero).  clip = ((lo0, hi0), (lo1, hi1)): the saturating form dv[i] =
+    clip(dv[i], lo_i, hi_i) (jnp.clip: NaN propagates).  Stateless."""
 
-    def __init__(self, body, gain=None, target=None, bias=(0.0, 0.0)):
+    def __init__(self, body, gain=None, target=None, bias=(0.0, 0.0), clip=None):
         self.body = int(body)
         z = [[0.0] * 6, [0.0] * 6]
         self.gain = [[_f32(v) for v in row] for row in (gain or z)]
         self.target = [[_f32(v) for v in row] for row in (target or z)]
         self.bias = [_f32(v) for v in bias]
+        self.clip = None if clip is None else [(_f32(lo), _f32(hi)) for lo, hi in clip]
+        if self.clip is not None and (len(self.clip) != 2 or any(np.isnan(v) for p in self.clip for v in p)):
+            raise ValueError("AffineControl: clip is ((lo0, hi0), (lo1, hi1)), no NaN bound")
 
     def c_struct(self):
         c = _ffi.CotixControl()
@@ -191,6 +228,10 @@ class AffineControl(AbstractControl):
                 c.gain[i][q] = self.gain[i][q]
                 c.target[i][q] = self.target[i][q]
             c.bias[i] = self.bias[i]
+        if self.clip is not None:
+            c.saturate = 1
+            for i in range(2):
+                c.clip_lo[i], c.clip_hi[i] = self.clip[i]
         return c
 
     def dv(self, state):
@@ -207,7 +248,12 @@ class AffineControl(AbstractControl):
             if self.bias[i] != 0.0:
                 bt = torch.tensor(self.bias[i], dtype=torch.float32, device=state.dyn.device)
                 acc = bt.expand(state.dyn.shape[2]).clone() if acc is None else acc + bt
-            out.append(torch.zeros_like(state.dyn[0, 0, :]) if acc is None else acc)
+            acc = torch.zeros_like(state.dyn[0, 0, :]) if acc is None else acc
+            if self.clip is not None:  # jnp.clip = min(hi, max(lo, x)): ties keep the bound, NaN propagates
+                lo, hi = (torch.tensor(v, dtype=torch.float32, device=acc.device) for v in self.clip[i])
+                acc = torch.where(lo >= acc, lo, acc)
+                acc = torch.where(hi <= acc, hi, acc)
+            out.append(acc)
         return torch.stack(out, 1).contiguous()
 
     def __call__(self, state):

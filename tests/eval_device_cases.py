@@ -47,6 +47,16 @@ def judges(name, ab):
         j = dict(rate_w={o + 2: 0.1}, regions=[(ab, yl[0], yl[1], -1.0), (ab, bl[0], bl[1], 1.0)], done_on_error=True)
         c = dict(body=ab, gain=[[0, 0, 0.1, 0, 0, 0], [0, 0, 0, 0.1, 0, 0]], target=[[0, 0, 2.0, 0, 0, 0], [0] * 6])
         return j, c
+    if name == "piecewise":  # a piecewise-linear reward rate over rate regions and a saturating control
+        r0 = _region(ab, px=(1.2, INF))
+        q0 = _region(ab, px=(-INF, 0.0))
+        q1 = _region(ab, vx=(0.0, INF), vy=(-INF, 0.2))
+        j = dict(rate_w={o: 0.5}, end_w={o + 1: 1.0}, regions=[(ab, r0[0], r0[1], 2.0)],
+                 rate_regions=[(ab, q0[0], q0[1], {o + 2: -2.0, o + 5: 0.25}, 1.5), (ab, q1[0], q1[1], {}, -0.75)])
+        c = dict(body=ab, gain=[[0.4, 0, 0.3, 0, 0, 0], [0, 0.5, 0, 0.2, 0, 0]],
+                 target=[[0.0, 0, 1.5, 0, 0, 0], [0, 0.5, 0, 0, 0, 0]], bias=(0.01, 0.0),
+                 clip=((-0.02, 0.03), (-0.05, 0.01)))
+        return j, c
     raise KeyError(name)
 
 

@@ -54,6 +54,8 @@ def _check_vs_oracle(dyn, keys, err, reward, fin, want):
     ("box", "x_done", 3, 10, 0.6),
     ("box", "multi", 4, 6, 0.5),
     ("robocup", "goal", 3, 4, 0.24),
+    ("box", "piecewise", 4, 8, 0.64),
+    ("robocup", "piecewise", 3, 5, 0.3),
     ("robocup", "x_done", 2, 5, 0.2),
 ])
 @pytest.mark.parametrize("EW", [1, 4])
@@ -78,18 +80,20 @@ def test_fused_eval_vs_oracle(emu_lib, scene, name, nfe, wfe, period, EW):
         assert fin.sum() >= 1  # the error trip ends episodes (done_on_error)
 
 
-def test_fused_eval_equals_product_host_loop(emu_lib):
+@pytest.mark.parametrize("name", ["multi", "piecewise"])
+def test_fused_eval_equals_product_host_loop(emu_lib, name):
     """The product's generic eval loop (one launch per env-step, judge and
     control evaluated by their torch methods) == the fused launch, bit for
     bit: the LinearJudge / AffineControl torch methods are the kernel's
-    expressions."""
+    expressions (piecewise: the rate's pieces per region, the clipped
+    control)."""
     emu, lib = emu_lib
     from parallax_amd import envs as E
     from test_envs_cpu import EmuWorld
     B = 8
     case = EDC.case("box", B, seed=5)
     ab = case["ab"]
-    j, c = EDC.device("multi", ab)
+    j, c = EDC.device(name, ab)
     world = EmuWorld(emu, lib, case["make"](), 1 | 4 | 16)
     dyn, keys, err = _state(case)
     state = E.WorldState(torch.from_numpy(dyn.copy()), torch.from_numpy(keys.view(np.int32).copy()),

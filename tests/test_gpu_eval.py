@@ -56,6 +56,8 @@ def _world(torch, case):
     ("box", "x_done", 3, 10, 0.6),
     ("box", "multi", 4, 6, 0.5),
     ("robocup", "goal", 3, 4, 0.24),
+    ("box", "piecewise", 4, 8, 0.64),
+    ("robocup", "piecewise", 3, 5, 0.3),
 ])
 def test_fused_eval_vs_oracle(torch_cuda, scene, name, nfe, wfe, period):
     torch = torch_cuda

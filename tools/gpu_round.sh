@@ -17,7 +17,8 @@ rc=$?; echo "bench rc=$rc"; cut -c1-200 $O/bench.json; [ $rc -eq 0 ] || { tail $
 fi
 # workload key : bench arguments (lunar_contact: the landers on the terrain,
 # driver steps 2560-3200, the stretch of the bench line's lunar_contact figure)
-ALL=("robocup:--scenario robocup --warmup 2" "lunar:--scenario lunar --warmup 2" \
+ALL=("robocup:--scenario robocup --warmup 2" "robocup_part:--scenario robocup --prng-layout partitionable --warmup 2" \
+     "lunar:--scenario lunar --warmup 2" \
      "lunar_contact:--scenario lunar --warmup 40" "box:--scenario box --warmup 2" \
      "grad:--mode grad --scenario robocup --warmup 1" "grad_box:--mode grad --scenario box --warmup 1" \
      "grad_lunar:--mode grad --scenario lunar --warmup 1")

@@ -54,7 +54,7 @@ def pmc(d, n=None):
 
 
 if scen.startswith("grad"):
-    # config 5: the forward (MODE 1) and backward (MODE 2) step kernels, per kernel
+    # config 5: the forward (MODE 1) and backward (MODE 4 / 2) step kernels, per kernel
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     bench = json.load(open(os.path.join(src, "trace_bench.json")))
 
@@ -72,7 +72,9 @@ if scen.startswith("grad"):
         m = re.search(r"step_kernel<\d+, \d+, (\d+)", name)
         return int(m.group(1)) if m else -1
 
-    for part, mode in (("fwd", 1), ("bwd", 2)):
+    # the backward: MODE 4 (from the forward's tape), else the re-play (MODE 2)
+    bmode = 4 if any(K in r["Name"] and mode_of(r["Name"]) == 4 for r in stats) else 2
+    for part, mode in (("fwd", 1), ("bwd", bmode)):
         row = [r for r in stats if K in r["Name"] and mode_of(r["Name"]) == mode][0]
         c = {}
         for d in ("pmc_fetch", "pmc_write", "pmc_sq"):

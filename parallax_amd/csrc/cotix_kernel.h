@@ -703,6 +703,7 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
     t.w(c.L.err, e) = er;
     t.w(c.L.nres, e) = rc;
     t.w(c.L.pcv, e) = 0u;  // no world part built yet in this launch (phase T)
+    t.w(c.L.rflag, e) = 0u;  // no restart pending
     if (EVAL && a.judge.on) {
       t.w(c.L.jfin, e) = jf;
       t.f(c.L.jr, e) = jr;
@@ -845,11 +846,36 @@ CX_DEV cx::v2 control_dv(const KArgs& a, Tile<EW> t, int o, int e) {
   return cx::v2{dv[0], dv[1]};
 }
 
+// Restarts of the autoreset programs (reset_mode 1) are deferred: phase E
+// flags the env (rflag) and the restart state replaces the state where the
+// next reader takes it -- the next step's phase A (euler_item, ab_fetch), or
+// the store phase after the last step -- instead of a phase of its own after
+// every step (ph_R).  Every reader selects the restart state for a flagged
+// env, so the values are the ones the copy would have left.  Deferred when
+// phase A runs (Euler or gravity on), else ph_R runs as before.
+CX_DEV bool restart_deferred(const KArgs& a) {
+  return a.dyn_reset != nullptr && a.reset_mode == 1 && (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY)) != 0;
+}
+// env e's restart is pending (its flag, when deferred)
+template <int EW>
+CX_DEV bool restart_pending(const KArgs& a, const Ctx& c, Tile<EW> t, int e) {
+  return restart_deferred(a) && t.w(c.L.rflag, e) != 0u;
+}
+
 // EVAL: the cotix_eval program (device judge / control); the step programs
 // are compiled without them
 template <int EW, bool EVAL = false>
 CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int b, int step) {
   const int o = c.L.dyn + b * 6;
+  if (restart_deferred(a)) {  // (uniform) a pending restart: the body's restart state first
+    const bool rs = t.w(c.L.rflag, e) != 0u;
+    float r[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) r[q] = t.f(c.L.rst + b * 6 + q, e);
+    if (rs)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) t.f(o + q, e) = r[q];
+  }
   const bool ctl = EVAL && a.ctl.on && b == a.ctl.body;
   const cx::v2 dv = ctl ? control_dv<EW>(a, t, o, e) : cx::v2{0.0f, 0.0f};
   if (!(a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))) return;  // (ph_A calls only with either)
@@ -1397,7 +1423,10 @@ CX_DEV void ab_fetch(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, ABRegs&
     const int w0 = q * WAVE + lane, w = w0 < ni ? w0 : ni - 1, e = w % EW;
     // analytic scenes: a part's world offset is its local-geometry offset (4 words per part)
     const int la = c.L.geo + (int)(r.dw[q] & 1023u), lb = c.L.geo + (int)((r.dw[q] >> 10) & 1023u);
-    const int oa = c.L.dyn + 6 * (int)(r.bw[q] & 255u), ob = c.L.dyn + 6 * (int)((r.bw[q] >> 8) & 255u);
+    // the pre-Euler state, or the restart state of an env whose restart is pending
+    const int ba = 6 * (int)(r.bw[q] & 255u), bb = 6 * (int)((r.bw[q] >> 8) & 255u);
+    const bool rs = restart_pending<EW>(a, c, t, e);
+    const int oa = (rs ? c.L.rst : c.L.dyn) + ba, ob = (rs ? c.L.rst : c.L.dyn) + bb;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       r.ga[q][k] = t.f(la + k, e);
@@ -2935,11 +2964,13 @@ CX_DEV void ph_JE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
   }
 }
 
+// (the last step's deferred restarts taken here: restart_deferred)
 template <int EW, bool ROLL = false, bool EVAL = false>
 CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
-    if (g < a.B) a.dyn[(size_t)off * a.B + g] = t.f(c.L.dyn + off, e);
+    const int src = (restart_pending<EW>(a, c, t, e) ? c.L.rst : c.L.dyn) + off;
+    if (g < a.B) a.dyn[(size_t)off * a.B + g] = t.f(src, e);
   }
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
@@ -2961,7 +2992,8 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
     const int nw = c.nb * 6;
     for (int w = lane; w < nw * EW; w += WAVE) {
       const int e = w / nw, off = w % nw, g = env0 + e;
-      if (g < a.B) a.obs[(size_t)g * nw + off] = t.f(c.L.dyn + off, e);
+      const int src = (restart_pending<EW>(a, c, t, e) ? c.L.rst : c.L.dyn) + off;
+      if (g < a.B) a.obs[(size_t)g * nw + off] = t.f(src, e);
     }
   }
 }
@@ -3603,7 +3635,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {
       run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
-      if (a.dyn_reset != nullptr && a.reset_mode == 1) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
+      if (a.dyn_reset != nullptr && a.reset_mode == 1 && !restart_deferred(a))
+        run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     } else if (ROLL) {
       run(PH_RET, [&](int l) {
         for (int e = l; e < EW; e += WAVE)

@@ -847,34 +847,25 @@ CX_DEV cx::v2 control_dv(const KArgs& a, Tile<EW> t, int o, int e) {
 }
 
 // Restarts of the autoreset programs (reset_mode 1) are deferred: phase E
-// flags the env (rflag) and the restart state replaces the state where the
-// next reader takes it -- the next step's phase A (euler_item, ab_fetch), or
-// the store phase after the last step -- instead of a phase of its own after
-// every step (ph_R).  Every reader selects the restart state for a flagged
-// env, so the values are the ones the copy would have left.  Deferred when
-// phase A runs (Euler or gravity on), else ph_R runs as before.
+// flags the env (rflag) and the next step's phase A (euler_item, DEFER)
+// copies the flagged env's restart state before it reads the state -- one
+// restart phase (ph_R) after the last step instead of one after every step;
+// the values are the ones the copy after the step would have left (nothing
+// reads the state in between).  Deferred when phase A runs as a phase of its
+// own (Euler or gravity on; not the staged A/T/B phase, whose fetch reads the
+// pre-Euler state ahead of phase A: run_wave's `defer`).
 CX_DEV bool restart_deferred(const KArgs& a) {
   return a.dyn_reset != nullptr && a.reset_mode == 1 && (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY)) != 0;
 }
-// env e's restart is pending (its flag, when deferred)
-template <int EW>
-CX_DEV bool restart_pending(const KArgs& a, const Ctx& c, Tile<EW> t, int e) {
-  return restart_deferred(a) && t.w(c.L.rflag, e) != 0u;
-}
 
 // EVAL: the cotix_eval program (device judge / control); the step programs
-// are compiled without them
-template <int EW, bool EVAL = false>
+// are compiled without them.  DEFER: take a deferred restart first
+template <int EW, bool EVAL = false, bool DEFER = false>
 CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int b, int step) {
   const int o = c.L.dyn + b * 6;
-  if (restart_deferred(a)) {  // (uniform) a pending restart: the body's restart state first
-    const bool rs = t.w(c.L.rflag, e) != 0u;
-    float r[6];
+  if (DEFER && restart_deferred(a) && t.w(c.L.rflag, e) != 0u) {  // the body's restart state first
 #pragma unroll
-    for (int q = 0; q < 6; ++q) r[q] = t.f(c.L.rst + b * 6 + q, e);
-    if (rs)
-#pragma unroll
-      for (int q = 0; q < 6; ++q) t.f(o + q, e) = r[q];
+    for (int q = 0; q < 6; ++q) t.f(o + q, e) = t.f(c.L.rst + b * 6 + q, e);
   }
   const bool ctl = EVAL && a.ctl.on && b == a.ctl.body;
   const cx::v2 dv = ctl ? control_dv<EW>(a, t, o, e) : cx::v2{0.0f, 0.0f};
@@ -909,7 +900,7 @@ CX_DEV void reset_scratch(const Ctx& c, Tile<EW> t, int lane) {
   for (int w = lane; w < c.sh.nmw * EW; w += WAVE) t.u[c.L.vm * EW + w] = 0u;
 }
 
-template <int EW, bool PRE = false, bool EVAL = false>
+template <int EW, bool PRE = false, bool EVAL = false, bool DEFER = false>
 CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step, int slot = 0) {
   using namespace cx;
   const int nb = c.nb;
@@ -917,7 +908,7 @@ CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
     for (int w = lane; w < nb * EW; w += WAVE) {
       const int e = w % EW, b = w / EW;
-      if (env0 + e < a.B) euler_item<EW, EVAL>(a, c, t, env0, e, b, step);
+      if (env0 + e < a.B) euler_item<EW, EVAL, DEFER>(a, c, t, env0, e, b, step);
     }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
     if (!PRE && !CXK_SKIP(a, 16)) {
@@ -1423,10 +1414,7 @@ CX_DEV void ab_fetch(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, ABRegs&
     const int w0 = q * WAVE + lane, w = w0 < ni ? w0 : ni - 1, e = w % EW;
     // analytic scenes: a part's world offset is its local-geometry offset (4 words per part)
     const int la = c.L.geo + (int)(r.dw[q] & 1023u), lb = c.L.geo + (int)((r.dw[q] >> 10) & 1023u);
-    // the pre-Euler state, or the restart state of an env whose restart is pending
-    const int ba = 6 * (int)(r.bw[q] & 255u), bb = 6 * (int)((r.bw[q] >> 8) & 255u);
-    const bool rs = restart_pending<EW>(a, c, t, e);
-    const int oa = (rs ? c.L.rst : c.L.dyn) + ba, ob = (rs ? c.L.rst : c.L.dyn) + bb;
+    const int oa = c.L.dyn + 6 * (int)(r.bw[q] & 255u), ob = c.L.dyn + 6 * (int)((r.bw[q] >> 8) & 255u);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       r.ga[q][k] = t.f(la + k, e);
@@ -2964,13 +2952,11 @@ CX_DEV void ph_JE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
   }
 }
 
-// (the last step's deferred restarts taken here: restart_deferred)
 template <int EW, bool ROLL = false, bool EVAL = false>
 CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
-    const int src = (restart_pending<EW>(a, c, t, e) ? c.L.rst : c.L.dyn) + off;
-    if (g < a.B) a.dyn[(size_t)off * a.B + g] = t.f(src, e);
+    if (g < a.B) a.dyn[(size_t)off * a.B + g] = t.f(c.L.dyn + off, e);
   }
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
@@ -2992,8 +2978,7 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
     const int nw = c.nb * 6;
     for (int w = lane; w < nw * EW; w += WAVE) {
       const int e = w / nw, off = w % nw, g = env0 + e;
-      const int src = (restart_pending<EW>(a, c, t, e) ? c.L.rst : c.L.dyn) + off;
-      if (g < a.B) a.obs[(size_t)g * nw + off] = t.f(src, e);
+      if (g < a.B) a.obs[(size_t)g * nw + off] = t.f(c.L.dyn + off, e);
     }
   }
 }
@@ -3592,6 +3577,9 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     run(PH_C1, [&](int l) { mc_fetch<EW>(c, t, l, mc); });
   RetRegs rr;  // the rollout's return terms
   if (ROLL) run(PH_RET, [&](int l) { ret_fetch<EW>(c, t, l, rr); });
+  // restarts deferred into phase A (restart_deferred): not with the staged A/T/B phase
+  const bool staged = !bconst && FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE;
+  const bool defer = restart_deferred(a) && !staged;
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
@@ -3612,7 +3600,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     // phases A, T, B as one (circle / AABB scenes whose contact items fit the
     // phase's ABQ prefetched chunks; uniform)
     if (bconst) {  // phase A, then B from the launch-constant item words (no phase T)
-      run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
+      run(PH_A, [&](int l) { ph_A<EW, true, EVAL, true>(a, c, t, env0, l, step, slot); });
       if (a.stages & COTIX_STAGE_COLLIDER) {
         run(PH_B, [&](int l) { ph_B_const<EW>(a, c, t, env0, l, bc); });
         collider_phases<EW, FNSET, true, R, true>(a, c, t, env0, run, slot, kso, mc);
@@ -3627,7 +3615,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true, R, FNSET == FNS_ANALYTIC>(
           a, c, t, env0, run, slot, kso, mc);
     } else {
-      run(PH_A, [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); });
+      run(PH_A, [&](int l) { ph_A<EW, true, EVAL, true>(a, c, t, env0, l, step, slot); });
       if (a.stages & COTIX_STAGE_COLLIDER)
         collider_phases<EW, FNSET, true, R, false, ROLL>(a, c, t, env0, run, slot, kso, mc, step);
     }
@@ -3635,8 +3623,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {
       run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
-      if (a.dyn_reset != nullptr && a.reset_mode == 1 && !restart_deferred(a))
-        run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
+      if (a.dyn_reset != nullptr && a.reset_mode == 1 && !defer) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     } else if (ROLL) {
       run(PH_RET, [&](int l) {
         for (int e = l; e < EW; e += WAVE)
@@ -3657,6 +3644,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   }
   if (ROLL && a.tape != nullptr && (a.stages & COTIX_STAGE_COLLIDER) && a.n_steps > 0)
     run(PH_SAVE, [&](int l) { tape_save<EW>(a, c, t, env0, l, a.n_steps - 1); });  // the last step's
+  if (defer && a.n_steps > 0) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });  // the last step's
   run(PH_STORE, [&](int l) { ph_store<EW, ROLL, EVAL>(a, c, t, env0, l); });
 }
 

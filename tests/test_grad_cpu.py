@@ -70,10 +70,10 @@ def test_oracle_grad_vs_finite_differences():
             assert abs(fd - ga[t, c]) <= 2e-3 * (1 + abs(fd)), (e, t, c, fd, ga[t, c])
 
 
-@pytest.mark.parametrize("E", [1, 4])
-def test_emu_rollout_box_world(emu_lib, E):
+@pytest.mark.parametrize("E,T", [(1, 40), (4, 32)])  # (T 32: the GPU test's horizon)
+def test_emu_rollout_box_world(emu_lib, E, T):
     emu, lib = emu_lib
-    B, T = 6, 40
+    B = 6
     case = GC.box_case(B, T, seed=1)
     ret, ga, gd, dyn = _emu_run(emu, lib, case, E)
     orc = GC.oracle(case)

@@ -852,8 +852,9 @@ CX_DEV cx::v2 control_dv(const KArgs& a, Tile<EW> t, int o, int e) {
 // restart phase (ph_R) after the last step instead of one after every step;
 // the values are the ones the copy after the step would have left (nothing
 // reads the state in between).  Deferred when phase A runs as a phase of its
-// own (Euler or gravity on; not the staged A/T/B phase, whose fetch reads the
-// pre-Euler state ahead of phase A: run_wave's `defer`).
+// own (Euler or gravity on), and in the staged A/T/B phase where its fetch
+// reads the restart state of a pending env (run_wave's SDEFER: kept to the
+// RoboCup step, whose register budget holds the select; run_wave's `defer`).
 CX_DEV bool restart_deferred(const KArgs& a) {
   return a.dyn_reset != nullptr && a.reset_mode == 1 && (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY)) != 0;
 }
@@ -1396,8 +1397,9 @@ template <int EW>
 CX_DEV int ab_chunks(const KArgs& a, const Ctx& c) {
   return (a.stages & COTIX_STAGE_COLLIDER) ? (c.nc * EW + WAVE - 1) / WAVE : 0;
 }
-// stage 1: every LDS read of the phase (the pre-Euler state)
-template <int EW>
+// stage 1: every LDS read of the phase (the pre-Euler state; DEFER: an env's
+// restart state where its restart is pending, run_wave's SDEFER)
+template <int EW, bool DEFER = false>
 CX_DEV void ab_fetch(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, ABRegs& r) {
   const SceneHdr& sc = c.sh;
   const int ni = c.nc * EW, nch = ab_chunks<EW>(a, c);
@@ -1414,7 +1416,8 @@ CX_DEV void ab_fetch(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, ABRegs&
     const int w0 = q * WAVE + lane, w = w0 < ni ? w0 : ni - 1, e = w % EW;
     // analytic scenes: a part's world offset is its local-geometry offset (4 words per part)
     const int la = c.L.geo + (int)(r.dw[q] & 1023u), lb = c.L.geo + (int)((r.dw[q] >> 10) & 1023u);
-    const int oa = c.L.dyn + 6 * (int)(r.bw[q] & 255u), ob = c.L.dyn + 6 * (int)((r.bw[q] >> 8) & 255u);
+    const int base = DEFER && restart_deferred(a) && t.w(c.L.rflag, e) != 0u ? c.L.rst : c.L.dyn;
+    const int oa = base + 6 * (int)(r.bw[q] & 255u), ob = base + 6 * (int)((r.bw[q] >> 8) & 255u);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       r.ga[q][k] = t.f(la + k, e);
@@ -3555,7 +3558,7 @@ CX_DEV void ph_load_fwd(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
     stage_ret_terms<EW>(a, c, t, l);
   }
 }
-template <int EW, int FNSET, bool ROLL, bool EVAL = false, class R = void>
+template <int EW, int FNSET, bool ROLL, bool EVAL = false, bool SDEFER = false, class R = void>
 CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, bool loaded = false) {
   static_assert(!(ROLL && EVAL), "the rollout has no judge");
   if (!loaded) run(PH_LOAD, [&](int l) { ph_load_fwd<EW, ROLL, EVAL>(a, c, t, env0, l); });
@@ -3577,9 +3580,9 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     run(PH_C1, [&](int l) { mc_fetch<EW>(c, t, l, mc); });
   RetRegs rr;  // the rollout's return terms
   if (ROLL) run(PH_RET, [&](int l) { ret_fetch<EW>(c, t, l, rr); });
-  // restarts deferred into phase A (restart_deferred): not with the staged A/T/B phase
+  // restarts deferred into phase A (restart_deferred)
   const bool staged = !bconst && FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE;
-  const bool defer = restart_deferred(a) && !staged;
+  const bool defer = restart_deferred(a) && (!staged || SDEFER);
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
@@ -3609,8 +3612,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       // stage 1 reads the pre-Euler state: every read is issued before phase
       // A's writes (stage 2); stage 3 computes the contacts
       run.template staged<ABRegs>(
-          PH_B, [&](int l, ABRegs& r) { ab_fetch<EW>(a, c, t, l, r); },
-          [&](int l) { ph_A<EW, true, EVAL>(a, c, t, env0, l, step, slot); },
+          PH_B, [&](int l, ABRegs& r) { ab_fetch<EW, SDEFER>(a, c, t, l, r); },
+          [&](int l) { ph_A<EW, true, EVAL, SDEFER>(a, c, t, env0, l, step, slot); },
           [&](int l, const ABRegs& r) { ab_contacts<EW>(a, c, t, env0, l, r); });
       if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true, R, FNSET == FNS_ANALYTIC>(
           a, c, t, env0, run, slot, kso, mc);

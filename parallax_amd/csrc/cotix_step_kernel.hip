@@ -128,7 +128,8 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   else if (MODE == 3)
     cxk::run_wave<EW, FNSET, false, true>(a, c, t, env0, run, true);
   else
-    cxk::run_wave<EW, FNSET, MODE == 1>(a, c, t, env0, run, true);
+    cxk::run_wave<EW, FNSET, MODE == 1, false,
+                  MODE == 0 && (SPEC == cxk::SPEC_ROBOCUP || SPEC == cxk::SPEC_ROBOCUP_PART)>(a, c, t, env0, run, true);
 #ifdef COTIX_PHASE_PROF
   if (lane == 0)
     for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);

@@ -2955,11 +2955,21 @@ CX_DEV void ph_JE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
   }
 }
 
+// all ones where env e's restart is taken at the store (rs and its flag),
+// else 0: a mask on the word offset, not a select between the layout's
+// fields (which LLVM turns into an indexed read of a private copy)
+template <int EW>
+CX_DEV int rsel(const Ctx& c, Tile<EW> t, int e, bool rs) {
+  return -(int)(rs & (t.w(c.L.rflag, e) != 0u));
+}
 template <int EW, bool ROLL = false, bool EVAL = false>
-CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
+CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, bool rs = false) {
+  // rs: the last step's restarts are taken here (run_wave's `rstore`): a
+  // flagged env's state is its restart state
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
-    if (g < a.B) a.dyn[(size_t)off * a.B + g] = t.f(c.L.dyn + off, e);
+    const int src = c.L.dyn + ((c.L.rst - c.L.dyn) & rsel<EW>(c, t, e, rs));
+    if (g < a.B) a.dyn[(size_t)off * a.B + g] = t.f(src + off, e);
   }
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
@@ -2981,7 +2991,8 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
     const int nw = c.nb * 6;
     for (int w = lane; w < nw * EW; w += WAVE) {
       const int e = w / nw, off = w % nw, g = env0 + e;
-      if (g < a.B) a.obs[(size_t)g * nw + off] = t.f(c.L.dyn + off, e);
+      const int src = c.L.dyn + ((c.L.rst - c.L.dyn) & rsel<EW>(c, t, e, rs));
+      if (g < a.B) a.obs[(size_t)g * nw + off] = t.f(src + off, e);
     }
   }
 }
@@ -3583,6 +3594,9 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   // restarts deferred into phase A (restart_deferred)
   const bool staged = !bconst && FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE;
   const bool defer = restart_deferred(a) && (!staged || SDEFER);
+  // the last step's restarts taken by the store (ph_store's rs; nothing reads
+  // the state after the last phase E but the judge)
+  const bool rstore = a.dyn_reset != nullptr && a.reset_mode == 1 && !(EVAL && a.judge.on);
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
@@ -3626,7 +3640,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {
       run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
-      if (a.dyn_reset != nullptr && a.reset_mode == 1 && !defer) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
+      if (a.dyn_reset != nullptr && a.reset_mode == 1 && !defer && !(rstore && step == a.n_steps - 1))
+        run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     } else if (ROLL) {
       run(PH_RET, [&](int l) {
         for (int e = l; e < EW; e += WAVE)
@@ -3647,8 +3662,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   }
   if (ROLL && a.tape != nullptr && (a.stages & COTIX_STAGE_COLLIDER) && a.n_steps > 0)
     run(PH_SAVE, [&](int l) { tape_save<EW>(a, c, t, env0, l, a.n_steps - 1); });  // the last step's
-  if (defer && a.n_steps > 0) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });  // the last step's
-  run(PH_STORE, [&](int l) { ph_store<EW, ROLL, EVAL>(a, c, t, env0, l); });
+  if (defer && a.n_steps > 0 && !rstore) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });  // the last step's
+  run(PH_STORE, [&](int l) { ph_store<EW, ROLL, EVAL>(a, c, t, env0, l, rstore); });
 }
 
 // backward with the forward's tape (MODE 4): steps n_steps-1 .. 0, each

@@ -25,6 +25,14 @@ namespace {
 using cxl::WPB;
 #ifdef COTIX_PHASE_PROF
 __device__ unsigned long long g_phase_cycles[cxk::PH_COUNT];
+// per-wave timeline of the last launch (s_memrealtime, 100 MHz, chip-wide):
+// entry, state loaded (before the workgroup barrier), after the barrier, end
+// (after the stores completed) -- tools/k1_stamps.py
+constexpr int STAMP_WAVES = 4096;
+__device__ unsigned long long g_stamps[STAMP_WAVES * 4];
+#define CXK_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#else
+#define CXK_STAMP(v) ((void)0)
 #endif
 // one phase on this lane, then wave-local ordering before the next phase.
 // staged(ph, fetch, mid, finish): a phase of three stages whose per-lane
@@ -79,6 +87,7 @@ struct WaveRun {
 template <int EW, int FNSET, int MODE, int SPEC = cxk::SPEC_GENERIC>
 __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   extern __shared__ uint32_t lds[];
+  CXK_STAMP(st0);
   const SceneDev* sc = a.sc;
   const cxk::SceneHdr sh = cxk::spec_hdr<SPEC>(a.sh);  // a constant for SPEC > 0
   const int nhot = sh.nhot;
@@ -112,7 +121,12 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
     else
       cxk::ph_load_fwd<EW, MODE == 1>(a, c, t, env0, lane);
   }
+#ifdef COTIX_PHASE_PROF
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+  CXK_STAMP(st1);
   __syncthreads();
+  CXK_STAMP(st2);
   if (env0 >= a.B) return;  // whole wave idle (after the only workgroup barrier)
 #ifdef COTIX_PHASE_PROF
   unsigned long long acc[cxk::PH_COUNT];
@@ -133,6 +147,15 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
 #ifdef COTIX_PHASE_PROF
   if (lane == 0)
     for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  CXK_STAMP(st3);
+  const int gw = (int)blockIdx.x * WPB + wave;
+  if (lane == 0 && gw < STAMP_WAVES) {
+    g_stamps[4 * gw] = st0;
+    g_stamps[4 * gw + 1] = st1;
+    g_stamps[4 * gw + 2] = st2;
+    g_stamps[4 * gw + 3] = st3;
+  }
 #endif
 }
 
@@ -246,5 +269,12 @@ extern "C" int cotix_phase_cycles(unsigned long long* out, int n) {
   sub[5] = dsub[1];  // EPA
   for (int q = 0; q < 8 && cxk::PH_COUNT + q < n; ++q) out[cxk::PH_COUNT + q] = sub[q];
   return cxk::PH_COUNT + 8 < n ? cxk::PH_COUNT + 8 : n;
+}
+// profiling build only: the last launch's per-wave timeline (g_stamps), n words
+extern "C" int cotix_phase_stamps(unsigned long long* out, int n) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const int m = n < STAMP_WAVES * 4 ? n : STAMP_WAVES * 4;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * m) != hipSuccess) return -1;
+  return m;
 }
 #endif

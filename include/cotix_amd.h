@@ -173,16 +173,6 @@ int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, in
 int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specialize);
 int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec);
 
-/* One-step launches (n_steps == 1 in cotix_step / cotix_eval: the RL loop's
- * env.step(1)) keep a key-window cache per key array: the end of a launch
- * derives the next launch's key splits from each env's final key, and the
- * next launch's prologue takes them where the env's key is still that key
- * (else it runs the splits itself) -- the same bits either way, the splits
- * off the next launch's critical path.  The cache is device memory the scene
- * owns (3 + 2 * n_types + n_bodies u32 per env, per key array, at most 8
- * arrays; freed by cotix_scene_destroy).  on = 0 turns it off (default 1). */
-int cotix_scene_set_key_cache(cotix_scene* scene, int on);
-
 /* Fused step, n_steps times, in place.
  *   dyn   device f32 [n_bodies][6][B]  (px, py, vx, vy, angle, angular_velocity)
  *   keys  device u32 [B][2]            collider key per env (advanced when

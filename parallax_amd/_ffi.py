@@ -53,7 +53,6 @@ SIGNATURES = {
     "cotix_scene_geom_floats": (_I, [_P]),
     "cotix_scene_info": (_I, [_P, _P, _P, _P, _P]),
     "cotix_scene_set_variant": (_I, [_P, _I, _I]),
-    "cotix_scene_set_key_cache": (_I, [_P, _I]),
     "cotix_scene_variant": (_I, [_P, _P, _P]),
     "cotix_step": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _I, _P]),
     "cotix_step_autoreset": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),

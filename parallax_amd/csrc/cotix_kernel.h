@@ -239,11 +239,6 @@ struct KArgs {
   // backward instead of re-playing the collider (tape_words below)
   uint32_t* tape;
   int tw;
-  // one-step launches (the RL loop): the key-window cache, [kc_words][B] --
-  // the next launch's one-step window, derived at the end of this launch from
-  // the env's final key (kc_produce), taken by the next prologue instead of
-  // the key chain where the env's key is the key it was derived from (ph_load)
-  uint32_t* kcache;
   // cotix_eval (AbstractEnvironment.eval, cotix/_envs.py:37-132, fused):
   int reset_mode;          // 1: restart on error bits after a step (dyn_reset); 2: restart envs finished at entry
   int action_held;         // 1: action is [B][2], the same impulse every step (a held control signal)
@@ -626,14 +621,10 @@ template <int EW>
 CX_DEV void k_one_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, uint32_t k0, uint32_t k1);
 // the key chain of a one-step launch runs in the prologue, on the keys in
 // registers, while the batch of state reads is in flight (ph_load)
-CX_HD bool keys_on(const KArgs& a) {
+CX_DEV bool keys_on(const KArgs& a) {
   return (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) != 0 && !CXK_SKIP(a, 16);
 }
-CX_HD bool k_in_prologue(const KArgs& a) { return keys_on(a) && a.n_steps == 1; }
-// the key-window cache (kc_produce): flags word, words per env, whether on
-constexpr uint32_t KC_SET = 1u, KC_COLL = 2u;
-CX_HD int kc_words(int kww) { return 3 + kww; }
-CX_DEV bool kc_on(const KArgs& a) { return a.kcache != nullptr && k_in_prologue(a); }
+CX_DEV bool k_in_prologue(const KArgs& a) { return keys_on(a) && a.n_steps == 1; }
 // the polygon programs' wave-scratch words that live across steps (every
 // program's first phase: the forward's load, the backward's adjoint init)
 template <int EW>
@@ -662,11 +653,6 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
   // the restart counter, read here with the state (the store then writes it:
   // no read-modify-write round trip at the end of the launch)
   const uint32_t rc = ((le && a.resets != nullptr) ? a.resets[ge] : 0u) + (rs ? 1u : 0u);
-  // the cached key window's key and flags (kc_on)
-  const bool kc = kc_on(a);
-  const size_t Bz = (size_t)a.B;
-  const uint32_t c0 = (kc && le) ? a.kcache[ge] : 0u, c1 = (kc && le) ? a.kcache[Bz + ge] : 0u;
-  const uint32_t cf = (kc && le) ? a.kcache[2 * Bz + ge] : 0u;
   uint32_t jf = 0u;
   float jr = 0.0f;
   if (EVAL && a.judge.on) {
@@ -678,8 +664,7 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
   // round trip instead of one per loop iteration -- the K = 1 launch's
   // fixed cost), item w over [dyn | geo | rst]
   const int nd = c.nb * 6 * EW, ng = a.geom != nullptr ? c.sh.G * EW : 0;
-  const int nr = (a.dyn_reset != nullptr && a.reset_mode == 1) ? nd : 0, nk = kc ? c.L.kww * EW : 0;
-  const int n3 = nd + ng + nr, ntot = n3 + nk;
+  const int nr = (a.dyn_reset != nullptr && a.reset_mode == 1) ? nd : 0, ntot = nd + ng + nr;
   constexpr int LK = 12;
   for (int base = 0; base < ntot; base += LK * WAVE) {
     float r[LK];
@@ -693,17 +678,13 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
       } else if (w < nd + ng) {
         const int e = (w - nd) % EW, g = env0 + e;
         if (g < a.B) src = a.geom + (a.gstride ? (size_t)g * a.gstride : (size_t)0) + (w - nd) / EW;
-      } else if (w < n3) {
+      } else if (w < ntot) {
         const int e = (w - nd - ng) % EW, g = env0 + e;
         if (g < a.B) src = a.dyn_reset + (size_t)((w - nd - ng) / EW) * a.B + g;
-      } else if (w < ntot) {  // the cached window's words (bit patterns)
-        const int e = (w - n3) % EW, g = env0 + e;
-        if (g < a.B) src = reinterpret_cast<const float*>(a.kcache) + (size_t)(3 + (w - n3) / EW) * a.B + g;
       }
       r[q] = src != nullptr ? *src : 0.0f;
     }
-    // uniform; the reads in flight (with the cache: only where it misses, below)
-    if (base == 0 && k_in_prologue(a) && !kc) k_one_regs<EW>(a, c, t, lane, k0, k1);
+    if (base == 0 && k_in_prologue(a)) k_one_regs<EW>(a, c, t, lane, k0, k1);  // uniform; the reads in flight
 #pragma unroll
     for (int q = 0; q < LK; ++q) {
       const int w = base + q * WAVE + lane;
@@ -711,16 +692,9 @@ CX_DEV void ph_load(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
         t.f(c.L.dyn + w / EW, w % EW) = r[q];
       else if (w < nd + ng)
         t.f(c.L.geo + (w - nd) / EW, (w - nd) % EW) = r[q];
-      else if (w < n3)
-        t.f(c.L.rst + (w - nd - ng) / EW, (w - nd - ng) % EW) = r[q];
       else if (w < ntot)
-        t.w(c.L.kw + (w - n3) / EW, (w - n3) % EW) = __float_as_uint(r[q]);
+        t.f(c.L.rst + (w - nd - ng) / EW, (w - nd - ng) % EW) = r[q];
     }
-  }
-  if (kc) {  // an env whose cached window is not its key's: the chain, for the wave (uniform)
-    const bool hit = c0 == k0 && c1 == k1 && (cf & KC_SET) != 0u &&
-                     ((cf & KC_COLL) != 0u || (a.stages & COTIX_STAGE_COLLIDER) == 0);
-    if (ballot(le && !hit) != 0ull) k_one_regs<EW>(a, c, t, lane, k0, k1);
   }
   if (lane < EW) {
     const int e = lane;
@@ -812,66 +786,35 @@ CX_DEV void ph_K2(const Ctx& c, Tile<EW> t, int lane, int n) {
 // one-step launch runs this in its prologue (ph_load) while the state reads
 // are in flight.  Items ((body, env), half) on lane pairs (split_at_pair),
 // in uniform rounds of 64 (the permutes are wave-wide).
-// (the window's word j of env e goes to put(e, j, word): the tile's slot 0,
-// or the key-window cache, kc_produce)
-template <int EW, class P>
-CX_DEV void k_one_chain(const KArgs& a, const Ctx& c, int lane, uint32_t k0, uint32_t k1, const P& put) {
+template <int EW>
+CX_DEV void k_one_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, uint32_t k0, uint32_t k1) {
   using namespace cx;
+  const Lay& L = c.L;
   const int nb = c.nb;
   const bool coll = (a.stages & COTIX_STAGE_COLLIDER) != 0;
   const bool part = c.sh.prng != 0;
   const int ni = 2 * (coll ? nb : 1) * EW;
   for (int base = 0; base < ni; base += WAVE) {
-    const int w = base + lane, p = w >> 1, h = w & 1, e = p % EW, i = p / EW;
+    const int w = base + lane, p = w >> 1, h = w & 1, e = p % EW, i = p / EW, o = L.kw;
     const key2 kin = key2{bpermute(e, k0), bpermute(e, k1)};  // env e's collider key (lane e)
     if (w >= ni) continue;
     const bool wr = i == 0 && h == 0;
     key2 k = split_at_pair(kin, 2u, 0u, h, part);  // K0
     if (wr) {
-      put(e, 0, k.a);
-      put(e, 1, k.b);
+      t.w(o, e) = k.a;
+      t.w(o + 1, e) = k.b;
     }
     for (int q = 0; q < c.nt; ++q) {  // K1
       k = split_at_pair(k, 2u, 0u, h, part);
       if (wr) {
-        put(e, 2 + 2 * q, k.a);
-        put(e, 3 + 2 * q, k.b);
+        t.w(o + 2 + 2 * q, e) = k.a;
+        t.w(o + 3 + 2 * q, e) = k.b;
       }
     }
     if (coll) {  // K2
       const float u = unit_float(bits1_l(split_at_pair(k, (uint32_t)nb, (uint32_t)i, h, part), part));
-      if (h == 0) put(e, 2 + 2 * c.nt + i, __float_as_uint(u));
+      if (h == 0) t.f(o + 2 + 2 * c.nt + i, e) = u;
     }
-  }
-}
-template <int EW>
-CX_DEV void k_one_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, uint32_t k0, uint32_t k1) {
-  const int o = c.L.kw;
-  k_one_chain<EW>(a, c, lane, k0, k1, [&](int e, int j, uint32_t v) { t.w(o + j, e) = v; });
-}
-
-// The key-window cache (KArgs::kcache, one-step launches): per env g, word
-// q at kcache[q * B + g] -- 0, 1 the key the window was derived from, 2 the
-// flags (KC_SET: written; KC_COLL: with the collider's choice uniforms), 3 ..
-// 3 + kww - 1 the window's words (the tile's key-window slot 0).  The window
-// is a function of the key, the scene's type count, body count and PRNG
-// layout (the cache belongs to one scene) and the collider stage alone, so a
-// cached window equals the chain's output bit for bit wherever its key equals
-// the env's key; elsewhere (first launch, keys written by the caller,
-// collider turned on) the prologue runs the chain.
-// end of a one-step launch: the next launch's window from each env's final key
-template <int EW>
-CX_DEV void kc_produce(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) {
-  const uint32_t k0 = lane < EW ? t.w(c.L.key, lane) : 0u, k1 = lane < EW ? t.w(c.L.key + 1, lane) : 0u;
-  const size_t B = (size_t)a.B;
-  k_one_chain<EW>(a, c, lane, k0, k1, [&](int e, int j, uint32_t v) {
-    if (env0 + e < a.B) a.kcache[(3 + (size_t)j) * B + env0 + e] = v;
-  });
-  if (lane < EW && env0 + lane < a.B) {
-    const size_t g = (size_t)env0 + lane;
-    a.kcache[g] = k0;
-    a.kcache[B + g] = k1;
-    a.kcache[2 * B + g] = KC_SET | ((a.stages & COTIX_STAGE_COLLIDER) ? KC_COLL : 0u);
   }
 }
 
@@ -3721,8 +3664,6 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     run(PH_SAVE, [&](int l) { tape_save<EW>(a, c, t, env0, l, a.n_steps - 1); });  // the last step's
   if (defer && a.n_steps > 0 && !rstore) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });  // the last step's
   run(PH_STORE, [&](int l) { ph_store<EW, ROLL, EVAL>(a, c, t, env0, l, rstore); });
-  // the next launch's key window, while the stores drain
-  if (!ROLL && kc_on(a)) run(PH_STORE, [&](int l) { kc_produce<EW>(a, c, t, env0, l); });
 }
 
 // backward with the forward's tape (MODE 4): steps n_steps-1 .. 0, each

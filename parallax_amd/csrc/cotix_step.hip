@@ -10,7 +10,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
-#include <vector>
 
 #include "../../include/cotix_amd.h"
 #include "cotix_device.h"
@@ -47,19 +46,7 @@ struct cotix_scene {
   // the largest tiling whose LDS fits, lds_default_ew)
   int envs_per_wave = 4;
   int specialize = 1;
-  // one-step launches' key-window caches (cxk::kc_produce), one per key array
-  // (the world's), made on first use: a few worlds per scene at most, the
-  // oldest freed beyond KC_MAX.  key_cache = 0 (cotix_scene_set_key_cache)
-  // runs the prologue's key chain every launch instead
-  struct KCache {
-    const uint32_t* keys;
-    int B;
-    uint32_t* buf;
-  };
-  std::vector<KCache> kc;
-  int key_cache = 1;
 };
-constexpr size_t KC_MAX = 8;
 // a workgroup's LDS at `ew` envs per wave (cxk::lds_bytes: the hot tables +
 // WPB tiles and wave scratches) and the hardware's 160 KiB per CU
 constexpr size_t LDS_CAP = 160 * 1024;
@@ -309,7 +296,6 @@ int cotix_scene_params(const cotix_scene* scene, cotix_params* out) {
 
 int cotix_scene_destroy(cotix_scene* scene) {
   if (!scene) return 0;
-  for (auto& k : scene->kc) (void)hipFree(k.buf);
   if (scene->dev) (void)hipFree(scene->dev);
   delete scene;
   return 0;
@@ -329,12 +315,6 @@ int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specializ
                 std::to_string(LDS_CAP));
   scene->envs_per_wave = envs_per_wave;
   scene->specialize = specialize ? 1 : 0;
-  return 0;
-}
-
-int cotix_scene_set_key_cache(cotix_scene* scene, int on) {
-  if (!scene) return fail("null scene");
-  scene->key_cache = on ? 1 : 0;
   return 0;
 }
 
@@ -382,42 +362,6 @@ static int check_step_args(const cotix_scene* scene, const float* dyn, const uin
   return 0;
 }
 
-// the key-window cache of a one-step launch over `keys` (B envs): found, or
-// made (zeroed on the launch's stream: no window is valid until a launch
-// wrote it); a changed B re-zeroes it, as its words are laid out by B
-static uint32_t* key_cache(cotix_scene* scene, const uint32_t* keys, int B, hipStream_t st) {
-  const size_t words = (size_t)cxk::kc_words(2 + 2 * scene->host.nt + scene->host.nb) * (size_t)B;
-  for (size_t i = 0; i < scene->kc.size(); ++i) {
-    auto& k = scene->kc[i];
-    if (k.keys != keys) continue;
-    if (k.B != B) {
-      if (B > k.B) {
-        (void)hipFree(k.buf);
-        k.buf = nullptr;
-        if (hipMalloc(&k.buf, words * sizeof(uint32_t)) != hipSuccess) {
-          scene->kc.erase(scene->kc.begin() + (long)i);
-          return nullptr;
-        }
-      }
-      k.B = B;
-      if (hipMemsetAsync(k.buf, 0, words * sizeof(uint32_t), st) != hipSuccess) return nullptr;
-    }
-    return k.buf;
-  }
-  if (scene->kc.size() >= KC_MAX) {
-    (void)hipFree(scene->kc.front().buf);
-    scene->kc.erase(scene->kc.begin());
-  }
-  uint32_t* buf = nullptr;
-  if (hipMalloc(&buf, words * sizeof(uint32_t)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(buf, 0, words * sizeof(uint32_t), st) != hipSuccess) {
-    (void)hipFree(buf);
-    return nullptr;
-  }
-  scene->kc.push_back({keys, B, buf});
-  return buf;
-}
-
 // launch the fused step kernel (mode 0 step, 1 rollout forward, 2 backward re-play, 3 eval with a judge/control)
 static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_stream_t stream) {
   if (scene_upload(scene)) return -1;
@@ -436,12 +380,6 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
   ka.dbg_skip = dbg ? atoi(dbg) : 0;
 #endif
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // one-step step / eval launches: the key-window cache (without it -- no
-  // memory, tooling -- the prologue runs the key chain, the same bits)
-  if ((mode == 0 || mode == 3) && scene->key_cache && cxk::k_in_prologue(ka)) {
-    ka.kcache = key_cache(scene, ka.keys, ka.B, st);
-    (void)hipGetLastError();  // (a failed allocation only turns the cache off)
-  }
   const int fs = scene->fnset;
   const int spec = scene_spec(scene);  // scene specialization (compile-time dimensions)
   hipError_t e;

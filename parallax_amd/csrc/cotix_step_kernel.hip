@@ -145,10 +145,10 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
     cxk::run_wave<EW, FNSET, MODE == 1, false,
                   MODE == 0 && (SPEC == cxk::SPEC_ROBOCUP || SPEC == cxk::SPEC_ROBOCUP_PART)>(a, c, t, env0, run, true);
 #ifdef COTIX_PHASE_PROF
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  CXK_STAMP(st3);  // (before the accumulators' atomics: 1024 waves x PH_COUNT adds to the same words)
   if (lane == 0)
     for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  CXK_STAMP(st3);
   const int gw = (int)blockIdx.x * WPB + wave;
   if (lane == 0 && gw < STAMP_WAVES) {
     g_stamps[4 * gw] = st0;

@@ -70,13 +70,6 @@ class Scene:
         _ffi.check(_ffi.lib.cotix_scene_set_variant(self.handle, int(envs_per_wave), 1 if specialize else 0),
                    "cotix_scene_set_variant")
 
-    def set_key_cache(self, on=True):
-        """One-step launches' key-window cache (cotix_scene_set_key_cache; on
-        by default): the next launch's key splits derived at the end of this
-        one, used where the env's key is still the one they came from.  The
-        same bits either way."""
-        _ffi.check(_ffi.lib.cotix_scene_set_key_cache(self.handle, 1 if on else 0), "cotix_scene_set_key_cache")
-
     def variant(self):
         """What a step launch uses: {"envs_per_wave": EW, "specialization":
         one of SPECIALIZATIONS} -- the reference scenes under the default

@@ -121,24 +121,11 @@ int emu_scene_destroy(void* s) {
   return 0;
 }
 
-// the key-window cache the next emu_step launches use (null: off; the
-// library's per-key-array buffer, cotix_step.hip key_cache)
-static uint32_t* g_kcache = nullptr;
-int emu_set_key_cache(uint32_t* kcache) {
-  g_kcache = kcache;
-  return 0;
-}
-int emu_kc_words(void* scene) {
-  const EmuScene* s = static_cast<EmuScene*>(scene);
-  return cxk::kc_words(2 + 2 * s->s.nt + s->s.nb);
-}
-
 int emu_step(void* scene, float* dyn, uint32_t* keys, uint32_t* err, const float* geom, int gstride, int B,
              int n_steps, float dt, int stages, const float* action, int action_body, const float* dyn_reset,
              uint32_t* resets, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
   cxk::KArgs a{};
-  a.kcache = g_kcache;
   a.sc = &s->s;
   a.dyn = dyn;
   a.keys = keys;

@@ -34,8 +34,6 @@ def load(asan=False):
     lib.emu_rollout_backward.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                          ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.c_int]
     lib.emu_rollout_tape_words.argtypes = [P_]
-    lib.emu_set_key_cache.argtypes = [P_]
-    lib.emu_kc_words.argtypes = [P_]
     lib.emu_eval.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_float, ctypes.c_int, P_, P_, P_, ctypes.c_int, P_, P_, ctypes.c_int, P_, P_, P_,
                              ctypes.c_int]

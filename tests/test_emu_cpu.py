@@ -152,78 +152,6 @@ def test_emu_fused_equals_single_steps(emu_lib, EW, scenario):
     assert np.array_equal(fused[1], single[1]) and np.array_equal(fused[2], single[2])
 
 
-@pytest.mark.parametrize("EW", [1, 4])
-@pytest.mark.parametrize("scenario", ["robocup", "lunar"])
-def test_emu_key_cache(emu_lib, EW, scenario):
-    """The one-step launches' key-window cache (KArgs::kcache, kc_produce):
-    22 one-step launches through the cache == one 22-step launch, bit for
-    bit, including the launches that must miss -- the first (zeroed cache),
-    after the caller rewrites some envs' keys, after a launch without the
-    collider stage (its windows lack the choice uniforms) -- and the words
-    it holds after a launch equal the chain of the final keys."""
-    emu, lib = emu_lib
-    from cotix_oracle import physics as P
-    name = "robocup_trace.npz" if scenario == "robocup" else "lunar_trace.npz"
-    tr = np.load(os.path.join(GOLD, name))
-    if scenario == "robocup":
-        h, geom = emu.oracle_scene(lib, P.robocup_bodies())
-        gstride, stages = 0, 1 | 4 | 16
-    else:
-        rows = [emu.oracle_scene(lib, P.lunar_lander_bodies(k))[1] for k in tr["terrain_keys"]]
-        h, _ = emu.oracle_scene(lib, P.lunar_lander_bodies(tr["terrain_keys"][0]))
-        geom = np.ascontiguousarray(np.stack(rows).astype(np.float32))
-        gstride, stages = geom.shape[1], 1 | 2 | 4 | 8 | 16 | 32
-    dyn0 = np.ascontiguousarray(tr["dyn"][0].transpose(1, 2, 0))
-    keys0 = np.ascontiguousarray(tr["keys"][0]).astype(np.uint32)
-    reset = dyn0.copy() if scenario == "robocup" else None
-    B, T = dyn0.shape[2], 22
-    rng = np.random.default_rng(5)
-    newkeys = rng.integers(0, 2 ** 32, size=(B, 2), dtype=np.uint64).astype(np.uint32)
-    flip = np.arange(B) % 3 == 0
-
-    def run(cache):
-        kc = np.zeros((lib.emu_kc_words(h), B), np.uint32) if cache else None
-        lib.emu_set_key_cache(kc.ctypes.data if cache else None)
-        try:
-            st = [dyn0.copy(), keys0.copy(), np.zeros(B, np.uint32)]
-            for t in range(T):
-                if t == 7:  # the caller rewrites a third of the keys
-                    st[1][flip] = newkeys[flip]
-                sg = stages & ~4 if t == 12 else stages  # one launch without the collider
-                emu.step(lib, h, *st, geom, gstride, 1, sg, E=EW, dyn_reset=reset)
-            return st, kc
-        finally:
-            lib.emu_set_key_cache(None)
-
-    plain, _ = run(False)
-    cached, kc = run(True)
-    assert same_f32(plain[0], cached[0])
-    assert np.array_equal(plain[1], cached[1]) and np.array_equal(plain[2], cached[2])
-    # the cache after the last launch: every env's window is its final key's
-    assert np.array_equal(kc[0], cached[1][:, 0]) and np.array_equal(kc[1], cached[1][:, 1])
-    assert np.all(kc[2] == 3)  # written, with the collider's uniforms
-    # (the words themselves: the next launch from the cache == from the chain)
-    nxt = [cached[0].copy(), cached[1].copy(), cached[2].copy()]
-    kc_bad = kc.copy()
-    lib.emu_set_key_cache(kc.ctypes.data)
-    try:
-        emu.step(lib, h, *nxt, geom, gstride, 1, stages, E=EW, dyn_reset=reset)
-    finally:
-        lib.emu_set_key_cache(None)
-    ref = [cached[0].copy(), cached[1].copy(), cached[2].copy()]
-    emu.step(lib, h, *ref, geom, gstride, 1, stages, E=EW, dyn_reset=reset)
-    assert same_f32(nxt[0], ref[0]) and np.array_equal(nxt[1], ref[1])
-    # (and the prologue does take them: a corrupted window word of a hit changes the launch)
-    kc_bad[3] ^= 1
-    bad = [cached[0].copy(), cached[1].copy(), cached[2].copy()]
-    lib.emu_set_key_cache(kc_bad.ctypes.data)
-    try:
-        emu.step(lib, h, *bad, geom, gstride, 1, stages, E=EW, dyn_reset=reset)
-    finally:
-        lib.emu_set_key_cache(None)
-    assert not np.array_equal(bad[1], ref[1])
-
-
 def test_emu_robocup_autoreset_vs_cport(emu_lib):
     """Episode restarts (the bench workload) on CPU: the kernel logic vs the
     C port of the oracle, 64 perturbed envs x 2 launches of 20 fused steps."""

@@ -209,45 +209,3 @@ def test_step_launch_follows_env_attributes(torch_cuda):
         torch.cuda.synchronize()
         assert torch.equal(o.view(torch.int32), ob.view(torch.int32)), (dt, ar, st)
     a.scenario.stages = stages0
-
-
-def test_k1_key_cache_bit_exact(torch_cuda):
-    """The one-step launches' key-window cache (cotix_scene_set_key_cache) on
-    the device: 24 RoboCup env.step(1) calls at 4096 envs with the cache on
-    == the same calls with it off, bit for bit every step (observation, state,
-    keys, error bits, restart counts) -- with the caller rewriting a third of
-    the keys at step 7 and one launch without the collider stage at step 13
-    (both must miss the cache) and an 8-step launch at step 18 (no cache)."""
-    torch = torch_cuda
-    import parallax_amd as pa
-    from parallax_amd import _ffi
-    dev = torch.device("cuda")
-    runs = []
-    for cache in (True, False):
-        scen = pa.RoboCupEnv(batch=4096, perturb=True, device=dev)
-        env = pa.BatchedEnv(scen, autoreset=True)
-        env.reset()
-        w = scen.world
-        w.scene.set_key_cache(cache)
-        g = torch.Generator(device="cpu").manual_seed(11)
-        newkeys = torch.randint(-2 ** 31, 2 ** 31 - 1, (4096, 2), generator=g, dtype=torch.int64).to(torch.int32)
-        flip = (torch.arange(4096) % 3 == 0).to(dev)
-        trail = []
-        for t in range(24):
-            if t == 7:
-                w.keys[flip] = newkeys.to(dev)[flip]
-            if t == 13:
-                w.step(1, env.dt, scen.stages & ~_ffi.STAGE_COLLIDER, dyn_reset=scen.dyn_reset, resets=env.resets)
-                obs = env.observation()
-            elif t == 18:
-                obs = env.step(8)
-            else:
-                obs = env.step(1)
-            trail.append([x.cpu().numpy().copy() for x in (obs, w.dyn, w.keys, w.err, env.resets)])
-        runs.append(trail)
-    torch.cuda.synchronize()
-    for t, (a, b) in enumerate(zip(*runs)):
-        assert same(a[0], b[0]) and same(a[1], b[1]), t
-        for x, y in zip(a[2:], b[2:]):
-            assert np.array_equal(x, y), t
-    assert runs[0][-1][4].sum() > 0  # restarts happened

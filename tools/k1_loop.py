@@ -32,17 +32,6 @@ def main():
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         out[name] = {"env_steps_per_s": 4096 * n / wall, "us_per_call": wall / n * 1e6}
-    # the same loop with the key-window cache off (the prologue's key chain every launch)
-    scen.world.scene.set_key_cache(False)
-    n = 2000
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(n):
-        env.step(1)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    out["step_no_key_cache"] = {"env_steps_per_s": 4096 * n / wall, "us_per_call": wall / n * 1e6}
-    scen.world.scene.set_key_cache(True)
     # the kernel alone: HIP events around each launch (a separate pass)
     n = 500
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]

@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--dump-gather", default=None, help="save the last all-gathered and local observation (.npz)")
     ap.add_argument("--envs-per-wave", type=int, default=0, choices=[0, 1, 2, 4, 8],
                     help="kernel tiling (0: the library default, 4); recorded in config")
+    ap.add_argument("--bwd-envs-per-wave", type=int, default=0, choices=[0, 1, 2, 4, 8],
+                    help="--mode grad: the backward launch's tiling (0: the forward's)")
     ap.add_argument("--specialize", type=int, default=1, choices=[0, 1],
                     help="0: the generic kernel instead of the reference scenes' specializations")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -616,7 +618,7 @@ def main():
 # ---------------------------------------------------------------------------
 # config 5 as its own line
 # ---------------------------------------------------------------------------
-def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario="robocup"):
+def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario="robocup", tiling=(0, 1, 0)):
     """Config 5: forward (cotix_rollout) + backward (cotix_rollout_backward)
     of a T-step rollout, d(sum_t x of the action body)/d(per-step dv of it).
     scenario "box": the same on the box world (finite dynamics), whose
@@ -637,6 +639,8 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario
     world = scen.world
     nb = len(world.bodies)
     ab = nb - 1 if ab is None else ab
+    ew, spec, bwd_ew = tiling  # (--envs-per-wave, --specialize, --bwd-envs-per-wave)
+    world.set_variant(ew, bool(spec))
     variant = world.scene.variant()
     dyn0, keys0 = world.dyn.clone(), world.keys.clone()
     gen = torch.Generator(device="cpu").manual_seed(1234 + rank)
@@ -656,7 +660,11 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario
         if i is not None:
             evf[i][1].record()
             evb[i][0].record()
+        if bwd_ew:
+            world.set_variant(bwd_ew, bool(spec))
         ga, _ = pa.rollout_backward(world, saved)
+        if bwd_ew:
+            world.set_variant(ew, bool(spec))
         if i is not None:
             evb[i][1].record()
         state["ret"], state["ga"] = ret, ga
@@ -717,13 +725,16 @@ def main_grad(a):
     B, T = a.envs, a.substeps
     box, lunar = a.scenario == "box", a.scenario == "lunar"
     r = run_grad(pa, dev, B, T, a.steps, a.warmup, rank, world_size, dist,
-                 "box" if box else ("lunar" if lunar else "robocup"))
+                 "box" if box else ("lunar" if lunar else "robocup"),
+                 (a.envs_per_wave, a.specialize, a.bwd_envs_per_wave))
     nb = 7 if box else (4 if lunar else 5)
     key = "grad_box" if box else ("grad_lunar" if lunar else "grad")
     # algorithmic HBM bytes of the backward launch per env-step: saved state
     # (nb x 6 f32) + key (2 u32) + action (2 f32) + the tape's resolution words
-    # (5 per body) read, grad_action (2 f32) written
-    bwd_bytes = (nb * 6 * 4 + 8 + 8 + nb * 5 * 4 + 8) * B * T
+    # (5 per body; analytic scenes + the 7-word resolution record) read,
+    # grad_action (2 f32) written
+    tape_w = 5 if lunar else 12
+    bwd_bytes = (nb * 6 * 4 + 8 + 8 + nb * tape_w * 4 + 8) * B * T
     achieved = bwd_bytes / (r["bwd_ms"] * 1e-3) / 1e9
     out = {
         "metric": "differentiable %d-step %s rollout, %d envs/GPU: env-steps/s with d(return)/d(action)"

@@ -341,7 +341,9 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
  *        per step and body the resolution RandomizedCollider.resolve applied
  *        (cotix/_colliders.py:274-336: the chosen partner j*, the contact of
  *        cell (i, j*)) and, in polygon scenes, the final EPA edge of every
- *        contact EPA ran for (cotix/_collisions.py:115-273)
+ *        contact EPA ran for (cotix/_collisions.py:115-273); in analytic
+ *        scenes each resolution's record (impulse applied or not, the
+ *        pre-resolution velocities of its two bodies)
  * and cotix_rollout_backward_ex, given that tape (nullable: the re-play of
  * cotix_rollout_backward), restores those decisions instead of re-running the
  * key splits, the narrowphase, the RNG scan and the choice, and starts the

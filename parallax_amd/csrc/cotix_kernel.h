@@ -259,16 +259,25 @@ struct KArgs {
 //              resolution
 //   5 nb + 4 c (polygon scenes) EPA's final edge (e0, e1) of distinct contact
 //              c, written by phase B when EPA ran for it
+//   5 nb + 7 i (analytic scenes) the resolution's record: whether its
+//              impulse was applied, then the pre-resolution v / w of bodies
+//              i and j (REC_W words, the sequential pass of phase E1) --
+//              written only for a resolution
 // Every value is the forward's own; the backward (MODE 4) restores them
 // instead of re-running the key splits, the narrowphase, the RNG scan and the
-// choice, and the VJP of a GJK/EPA contact starts from the recorded edge.
-CX_HD int tape_words(int nb, int nc, int poly) { return 5 * nb + (poly ? 4 * nc : 0); }
+// choice (and, analytic scenes, the sequential resolution pass), and the VJP
+// of a GJK/EPA contact starts from the recorded edge.
+constexpr int REC_W = 7;  // per resolution: applied flag, v/w of body i, v/w of body j (pre-resolution)
+CX_HD int tape_words(int nb, int nc, int poly) { return 5 * nb + (poly ? 4 * nc : REC_W * nb); }
+// the tape carries the resolutions' records (analytic scenes): the forward's
+// phase E1 records them (ph_E TREC), the backward skips its phase E
+CX_HD bool tape_rec(const SceneHdr& sh) { return sh.poly == 0; }
 // the backward's tape words in registers (tape_fetch): per (body, env) item
 // its resolution word + contact, and the recorded EPA edge
 constexpr int TQ = (MAXB * 8 + WAVE - 1) / WAVE;  // items per lane: nb * EW over 64 lanes (EW <= 8)
 struct TapeRegs {
   uint32_t d[TQ][5];
-  float ed[TQ][4];
+  uint32_t x[TQ][REC_W];  // polygon scenes: the EPA edge (4 float words); analytic: the resolution's record
 };
 
 // per-wave tile layout (words, each x EW envs)
@@ -280,7 +289,6 @@ struct Lay {
 // together (phase K) -- the collider keys depend on the key chain only, never
 // on the physics.  Slot s (KW words): sk0[2], skt[2*nt], then choice uniform[nb].
 constexpr int KWIN = 16;
-constexpr int REC_W = 7;  // per resolution: applied flag, v/w of body i, v/w of body j (pre-resolution)
 // per resolution (phase E0 -> E1): partner body (or RP_NONE), cx::ResPre, partner mass/inertia
 enum : int { RP_J, RP_NX, RP_NY, RP_R1X, RP_R1Y, RP_R2X, RP_R2Y, RP_PX, RP_PY, RP_DEN, RP_PT, RP_NE, RP_MU, RP_MJ, RP_IJ,
              RP_QMJ, RP_QIJ, RP_W };
@@ -2480,6 +2488,12 @@ CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
     const bool res = dec != RP_NONE;
     const int j = res ? (int)(dec & 255u) : i, cid = res ? (int)((dec >> 8) & 511u) : -1;
     t.w(L.ch + i, e) = (uint32_t)j;
+    if (tape_rec(c.sh)) {  // the forward's record of the resolution (phase E does not run)
+      t.w(L.rec + REC_W * i, e) = res ? r.x[q][0] : 0u;
+      if (res)
+#pragma unroll
+        for (int k = 1; k < REC_W; ++k) t.w(L.rec + REC_W * i + k, e) = r.x[q][k];
+    }
     if (res) {
       t.w(L.m + i * nb + j, e) = (uint32_t)cid << 18;
       const int co = L.con + 4 * cid;
@@ -2488,9 +2502,10 @@ CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
       if (edges) {
         const int eo = ge_edge_word(c, i);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) t.f(eo + k, e) = r.ed[q][k];
+        for (int k = 0; k < 4; ++k) t.w(eo + k, e) = r.x[q][k];
       }
     }
+    if (tape_rec(c.sh)) continue;  // (the resolution operands are phase E's)
     if (c.sh.rcp_all)
       e0_item<EW, true>(c, t, e, i, j, cid);
     else
@@ -2701,11 +2716,19 @@ CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
     o[0] = j | (cid << 8);
 #pragma unroll
     for (int q = 0; q < 4; ++q) o[(size_t)(q + 1) * a.B] = t.w(co + q, e);
+    if (tape_rec(c.sh)) {  // phase E1's record of the resolution (ph_E TREC)
+      uint32_t* orc = a.tape + ((size_t)step * a.tw + 5 * nb + REC_W * i) * a.B + g;
+#pragma unroll
+      for (int q = 0; q < REC_W; ++q) orc[(size_t)q * a.B] = t.w(L.rec + REC_W * i + q, e);
+    }
   }
 }
 
-template <int EW, bool REC = false, bool RET = false>
+// TREC: the rollout forward with a tape records the resolutions (as REC) for
+// tape_save, and is otherwise the forward's phase E
+template <int EW, bool REC = false, bool RET = false, bool TREC = false>
 CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso, const RetRegs* rr = nullptr) {
+  constexpr bool RC = REC || TREC;
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int nb = c.nb;
@@ -2736,15 +2759,15 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     if (a.stages & COTIX_STAGE_COLLIDER) {
       if (sc.rcp_all) {
         switch (nb) {
-          case 4: e1_regs<EW, REC, 4, true>(c, t, e); break;
-          case 5: e1_regs<EW, REC, 5, true>(c, t, e); break;
-          default: e1_tile<EW, REC, true>(c, t, e); break;
+          case 4: e1_regs<EW, RC, 4, true>(c, t, e); break;
+          case 5: e1_regs<EW, RC, 5, true>(c, t, e); break;
+          default: e1_tile<EW, RC, true>(c, t, e); break;
         }
       } else {
         switch (nb) {
-          case 4: e1_regs<EW, REC, 4, false>(c, t, e); break;
-          case 5: e1_regs<EW, REC, 5, false>(c, t, e); break;
-          default: e1_tile<EW, REC, false>(c, t, e); break;
+          case 4: e1_regs<EW, RC, 4, false>(c, t, e); break;
+          case 5: e1_regs<EW, RC, 5, false>(c, t, e); break;
+          default: e1_tile<EW, RC, false>(c, t, e); break;
         }
       }
     }
@@ -3106,6 +3129,11 @@ CX_DEV void tape_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int ste
     const uint32_t* p = a.tape + ((size_t)step * a.tw + 5 * (ok ? i : 0)) * a.B + (ok ? g : 0);
 #pragma unroll
     for (int k = 0; k < 5; ++k) r.d[q][k] = ok ? p[(size_t)k * a.B] : RP_NONE;
+    if (tape_rec(c.sh)) {  // the resolution's record (read whether or not it resolved: no dependent round trip)
+      const uint32_t* pr = a.tape + ((size_t)step * a.tw + 5 * c.nb + REC_W * (ok ? i : 0)) * a.B + (ok ? g : 0);
+#pragma unroll
+      for (int k = 0; k < REC_W; ++k) r.x[q][k] = ok ? pr[(size_t)k * a.B] : 0u;
+    }
   }
 }
 template <int EW>
@@ -3119,7 +3147,7 @@ CX_DEV void tape_edge_fetch(const KArgs& a, const Ctx& c, int env0, int lane, in
     const int cid = ok ? (int)((r.d[q][0] >> 8) & 511u) : 0;
     const uint32_t* p = a.tape + ((size_t)step * a.tw + 5 * c.nb + 4 * cid) * a.B + (ok ? g : 0);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r.ed[q][k] = ok ? __uint_as_float(p[(size_t)k * a.B]) : 0.0f;
+    for (int k = 0; k < 4; ++k) r.x[q][k] = ok ? p[(size_t)k * a.B] : 0u;
   }
 }
 
@@ -3639,7 +3667,10 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {
-      run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
+      if (ROLL && a.tape != nullptr && tape_rec(c.sh) && (a.stages & COTIX_STAGE_COLLIDER))
+        run(PH_E1, [&](int l) { ph_E<EW, false, ROLL, true>(a, c, t, env0, l, kso, &rr); });
+      else
+        run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
       if (a.dyn_reset != nullptr && a.reset_mode == 1 && !defer && !(rstore && step == a.n_steps - 1))
         run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });
     } else if (ROLL) {
@@ -3713,7 +3744,8 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
       transform_phases<EW, FNSET>(a, c, t, env0, run);
       run(PH_D, [&](int l) { ph_D_tape<EW>(a, c, t, env0, l, tr); });
     }
-    run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
+    // phase E re-runs the sequential pass for its records -- unless the tape has them
+    if (!(col && tape_rec(c.sh))) run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
     if (FNSET != FNS_ANALYTIC && col && ge_fits(c)) {
       if (edges)
         run(PH_GE, [&](int l) { ph_GE<EW, true>(a, c, t, env0, l); });

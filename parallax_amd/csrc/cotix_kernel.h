@@ -2474,7 +2474,7 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
 // one field they read)
 CX_HD bool ge_edges_fit(const Ctx& c) { return 28 * c.nb <= KWIN * c.L.kww; }
 CX_DEV int ge_edge_word(const Ctx& c, int i) { return c.L.kw + 24 * c.nb + 4 * i; }
-template <int EW>
+template <int EW, bool TR>
 CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, const TapeRegs& r) {
   const Lay& L = c.L;
   const int nb = c.nb, ni = nb * EW;
@@ -2488,7 +2488,7 @@ CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
     const bool res = dec != RP_NONE;
     const int j = res ? (int)(dec & 255u) : i, cid = res ? (int)((dec >> 8) & 511u) : -1;
     t.w(L.ch + i, e) = (uint32_t)j;
-    if (tape_rec(c.sh)) {  // the forward's record of the resolution (phase E does not run)
+    if (TR && tape_rec(c.sh)) {  // the forward's record of the resolution (phase E does not run)
       t.w(L.rec + REC_W * i, e) = res ? r.x[q][0] : 0u;
       if (res)
 #pragma unroll
@@ -2505,7 +2505,7 @@ CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
         for (int k = 0; k < 4; ++k) t.w(eo + k, e) = r.x[q][k];
       }
     }
-    if (tape_rec(c.sh)) continue;  // (the resolution operands are phase E's)
+    if (TR && tape_rec(c.sh)) continue;  // (the resolution operands are phase E's)
     if (c.sh.rcp_all)
       e0_item<EW, true>(c, t, e, i, j, cid);
     else
@@ -2698,7 +2698,7 @@ CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const Ret
 // env) item, from the tile's phase-D words of that step -- they live until
 // the next step's phase A resets the collider scratch, so the save runs in
 // the next step's save phase (ph_save) or, for the last step, after the loop
-template <int EW>
+template <int EW, bool TR>
 CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   const Lay& L = c.L;
   const int nb = c.nb;
@@ -2716,7 +2716,7 @@ CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
     o[0] = j | (cid << 8);
 #pragma unroll
     for (int q = 0; q < 4; ++q) o[(size_t)(q + 1) * a.B] = t.w(co + q, e);
-    if (tape_rec(c.sh)) {  // phase E1's record of the resolution (ph_E TREC)
+    if (TR && tape_rec(c.sh)) {  // phase E1's record of the resolution (ph_E TREC)
       uint32_t* orc = a.tape + ((size_t)step * a.tw + 5 * nb + REC_W * i) * a.B + g;
 #pragma unroll
       for (int q = 0; q < REC_W; ++q) orc[(size_t)q * a.B] = t.w(L.rec + REC_W * i + q, e);
@@ -3025,9 +3025,9 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
 // ---------------------------------------------------------------------------
 // state before step `step` -> save_dyn[step], save_keys[step]
 // (+ the tape words of the step before it, tape_save)
-template <int EW>
+template <int EW, bool TR>
 CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
-  if (a.tape != nullptr && step > 0 && (a.stages & COTIX_STAGE_COLLIDER)) tape_save<EW>(a, c, t, env0, lane, step - 1);
+  if (a.tape != nullptr && step > 0 && (a.stages & COTIX_STAGE_COLLIDER)) tape_save<EW, TR>(a, c, t, env0, lane, step - 1);
   const size_t base = (size_t)step * c.nb * 6 * a.B;
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;
@@ -3118,7 +3118,9 @@ CX_DEV void restore_apply(const Ctx& c, Tile<EW> t, int lane, const RestoreRegs&
 // phase D), the resolution word and its contact; the recorded EPA edge of the
 // resolution's contact (polygon scenes) is read once the step's resolution
 // words are current (tape_edge_fetch)
-template <int EW>
+// (TR: the program can meet an analytic scene -- FNSET analytic; the polygon
+// programs' scenes are never analytic, launch_fnset)
+template <int EW, bool TR>
 CX_DEV void tape_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step, TapeRegs& r) {
   const int ni = c.nb * EW;
 #pragma unroll
@@ -3129,7 +3131,7 @@ CX_DEV void tape_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int ste
     const uint32_t* p = a.tape + ((size_t)step * a.tw + 5 * (ok ? i : 0)) * a.B + (ok ? g : 0);
 #pragma unroll
     for (int k = 0; k < 5; ++k) r.d[q][k] = ok ? p[(size_t)k * a.B] : RP_NONE;
-    if (tape_rec(c.sh)) {  // the resolution's record (read whether or not it resolved: no dependent round trip)
+    if (TR && tape_rec(c.sh)) {  // the resolution's record (read whether or not it resolved: no dependent round trip)
       const uint32_t* pr = a.tape + ((size_t)step * a.tw + 5 * c.nb + REC_W * (ok ? i : 0)) * a.B + (ok ? g : 0);
 #pragma unroll
       for (int k = 0; k < REC_W; ++k) r.x[q][k] = ok ? pr[(size_t)k * a.B] : 0u;
@@ -3357,6 +3359,120 @@ CX_DEV void ph_GE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
   }
 }
 
+// phase G of an analytic scene with NB bodies on the env's lane: the same
+// reverse chain as ph_G's tile form, with the adjoints, positions and each
+// resolution's flag and partner in registers (bodies picked by unrolled
+// selects, no scratch) -- the resolutions' LDS reads are then independent of
+// the previous resolution's writes, and the Euler / return terms run on
+// registers.  Every operation and its order are ph_G's: the same bits.
+template <int EW, int NB>
+CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step) {
+  using namespace cx;
+  const SceneHdr& sc = c.sh;
+  const Lay& L = c.L;
+  float g[NB][6], px[NB], py[NB], an[NB];
+  uint32_t fl[NB], jj[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) g[b][k] = t.f(L.adj + 6 * b + k, e);
+    px[b] = t.f(L.dyn + 6 * b, e);
+    py[b] = t.f(L.dyn + 6 * b + 1, e);
+    an[b] = t.f(L.dyn + 6 * b + 4, e);
+    fl[b] = t.w(L.rec + REC_W * b, e);
+    jj[b] = t.w(L.ch + b, e);
+  }
+  if (a.stages & COTIX_STAGE_COLLIDER) {
+#pragma unroll
+    for (int i = NB - 1; i >= 0; --i) {  // resolutions in reverse order
+      if (fl[i] == 0u) continue;
+      const int j = (int)jj[i];
+      const int ro = L.rec + REC_W * i;
+      const int cid = (int)((t.w(L.m + i * NB + j, e) >> 18) & 511u);
+      const int co = L.con + 4 * cid;
+      float pxj = 0.0f, pyj = 0.0f, anj = 0.0f;
+      Dyn gj = Dyn{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (b == j) {
+          pxj = px[b];
+          pyj = py[b];
+          anj = an[b];
+          gj = Dyn{g[b][0], g[b][1], g[b][2], g[b][3], g[b][4], g[b][5]};
+        }
+      const Dyn bi = Dyn{px[i], py[i], t.f(ro + 1, e), t.f(ro + 2, e), an[i], t.f(ro + 3, e)};
+      const Dyn bj = Dyn{pxj, pyj, t.f(ro + 4, e), t.f(ro + 5, e), anj, t.f(ro + 6, e)};
+      Dyn gi = Dyn{g[i][0], g[i][1], g[i][2], g[i][3], g[i][4], g[i][5]};
+      v2 gpen = v2{0.0f, 0.0f}, gcp = v2{0.0f, 0.0f};
+      resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
+                  v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp, baum_of(sc));
+      const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
+      const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
+      const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
+      Shape SA, SB;
+      SA.kind = ka;
+      SB.kind = kb;
+      SA.n = SB.n = 0;
+      for (int k = 0; k < 2 * MAXV; ++k) SA.w[k] = SB.w[k] = 0.0f;
+      for (int k = 0; k < 4; ++k) {
+        SA.w[k] = t.f(wa + k, e);
+        SB.w[k] = t.f(wb + k, e);
+      }
+      float ga[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      contact_vjp(fn, SA, SB, gpen, gcp, ga, gb);
+      const float gw[6] = {gi.px, gi.py, gi.vx, gi.vy, gi.a, gi.w}, hw[6] = {gj.px, gj.py, gj.vx, gj.vy, gj.a, gj.w};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g[i][k] = gw[k];
+      const int qa = t.ti(sc.o_pbody + pa), qb = t.ti(sc.o_pbody + pb);
+      const float ax = ka == KIND_CIRCLE ? ga[1] : ga[0] + ga[2], ay = ka == KIND_CIRCLE ? ga[2] : ga[1] + ga[3];
+      const float bx = kb == KIND_CIRCLE ? gb[1] : gb[0] + gb[2], by = kb == KIND_CIRCLE ? gb[2] : gb[1] + gb[3];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        if (b == j)
+#pragma unroll
+          for (int k = 0; k < 6; ++k) g[b][k] = hw[k];
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (b == qa) {
+          g[b][0] = g[b][0] + ax;
+          g[b][1] = g[b][1] + ay;
+        }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (b == qb) {
+          g[b][0] = g[b][0] + bx;
+          g[b][1] = g[b][1] + by;
+        }
+    }
+  }
+  const int g_env = env0 + e;
+  if (a.action != nullptr && a.grad_action != nullptr) {  // v[action_body] += action[step]
+    float gx = 0.0f, gy = 0.0f;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (b == a.action_body) {
+        gx = g[b][2];
+        gy = g[b][3];
+      }
+    a.grad_action[2 * ((size_t)step * a.B + g_env)] = gx;
+    a.grad_action[2 * ((size_t)step * a.B + g_env) + 1] = gy;
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (a.stages & COTIX_STAGE_EULER) {  // p += v dt, angle += w dt
+      g[b][2] = g[b][2] + g[b][0] * a.dt;
+      g[b][3] = g[b][3] + g[b][1] * a.dt;
+      g[b][5] = g[b][5] + g[b][4] * a.dt;
+    }
+    if (step > 0)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g[b][k] = g[b][k] + t.f(L.rst + 6 * b + k, e);  // ret_w (staged)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) t.f(L.adj + 6 * b + k, e) = g[b][k];
+  }
+}
+
 template <int EW, int FNSET = FNS_ANALYTIC>
 CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   using namespace cx;
@@ -3366,6 +3482,16 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   for (int e = lane; e < EW; e += WAVE) {
     const int g = env0 + e;
     if (g >= a.B) continue;
+#ifndef COTIX_NO_GREGS  // (tooling: the tile form for every scene, tests/test_grad_cpu.py checks the two agree)
+    if (FNSET == FNS_ANALYTIC && nb == 5) {  // RoboCup
+      g_regs<EW, 5>(a, c, t, env0, e, step);
+      continue;
+    }
+    if (FNSET == FNS_ANALYTIC && nb == 7) {  // the box world
+      g_regs<EW, 7>(a, c, t, env0, e, step);
+      continue;
+    }
+#endif
     if (FNSET != FNS_ANALYTIC && (a.stages & COTIX_STAGE_LUNAR) && nb >= 3) joints_vjp<EW>(c, t, e);
     if (a.stages & COTIX_STAGE_COLLIDER) {
       for (int i = nb - 1; i >= 0; --i) {  // resolutions in reverse order
@@ -3626,7 +3752,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   // the state after the last phase E but the judge)
   const bool rstore = a.dyn_reset != nullptr && a.reset_mode == 1 && !(EVAL && a.judge.on);
   for (int step = 0; step < a.n_steps; ++step) {
-    if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW>(a, c, t, env0, l, step); });
+    if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW, FNSET == FNS_ANALYTIC>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
     if (keys && slot == 0 && !(step == 0 && k_in_prologue(a))) {
       const int n = a.n_steps - step < KWIN ? a.n_steps - step : KWIN;
@@ -3667,7 +3793,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     if (a.trace_chosen != nullptr || a.trace_cells != nullptr)
       run(PH_TRACE, [&](int l) { ph_trace<EW>(a, c, t, env0, l, step); });
     if (!CXK_SKIP(a, 32)) {
-      if (ROLL && a.tape != nullptr && tape_rec(c.sh) && (a.stages & COTIX_STAGE_COLLIDER))
+      if (ROLL && FNSET == FNS_ANALYTIC && a.tape != nullptr && tape_rec(c.sh) && (a.stages & COTIX_STAGE_COLLIDER))
         run(PH_E1, [&](int l) { ph_E<EW, false, ROLL, true>(a, c, t, env0, l, kso, &rr); });
       else
         run(PH_E1, [&](int l) { ph_E<EW, false, ROLL>(a, c, t, env0, l, kso, &rr); });
@@ -3692,7 +3818,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     }
   }
   if (ROLL && a.tape != nullptr && (a.stages & COTIX_STAGE_COLLIDER) && a.n_steps > 0)
-    run(PH_SAVE, [&](int l) { tape_save<EW>(a, c, t, env0, l, a.n_steps - 1); });  // the last step's
+    run(PH_SAVE, [&](int l) { tape_save<EW, FNSET == FNS_ANALYTIC>(a, c, t, env0, l, a.n_steps - 1); });  // the last step's
   if (defer && a.n_steps > 0 && !rstore) run(PH_R, [&](int l) { ph_R<EW>(c, t, l); });  // the last step's
   run(PH_STORE, [&](int l) { ph_store<EW, ROLL, EVAL>(a, c, t, env0, l, rstore); });
 }
@@ -3714,12 +3840,13 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
   });
   const bool col = (a.stages & COTIX_STAGE_COLLIDER) != 0;
   const bool edges = FNSET != FNS_ANALYTIC && c.sh.poly && ge_fits(c) && ge_edges_fit(c);
+  constexpr bool TR = FNSET == FNS_ANALYTIC;  // the tape's resolution records (tape_rec)
   RestoreRegs rr;
   TapeRegs tn, tr;  // the next (earlier) step's tape words, the current step's
   if (a.n_steps > 0)
     run(PH_RESTORE, [&](int l) {
       restore_fetch<EW>(a, c, env0, l, a.n_steps - 1, rr);
-      if (col) tape_fetch<EW>(a, c, env0, l, a.n_steps - 1, tn);
+      if (col) tape_fetch<EW, TR>(a, c, env0, l, a.n_steps - 1, tn);
     });
   for (int step = a.n_steps - 1; step >= 0; --step) {
     run(PH_RESTORE, [&](int l) {
@@ -3730,7 +3857,7 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
       }
       if (step > 0) {  // the next (earlier) step, in flight
         restore_fetch<EW>(a, c, env0, l, step - 1, rr);
-        if (col) tape_fetch<EW>(a, c, env0, l, step - 1, tn);
+        if (col) tape_fetch<EW, TR>(a, c, env0, l, step - 1, tn);
       }
     });
     run(PH_A, [&](int l) {  // Euler (+ gravity, + action); no key split, no collider scratch
@@ -3742,10 +3869,10 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
     });
     if (col) {
       transform_phases<EW, FNSET>(a, c, t, env0, run);
-      run(PH_D, [&](int l) { ph_D_tape<EW>(a, c, t, env0, l, tr); });
+      run(PH_D, [&](int l) { ph_D_tape<EW, TR>(a, c, t, env0, l, tr); });
     }
     // phase E re-runs the sequential pass for its records -- unless the tape has them
-    if (!(col && tape_rec(c.sh))) run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
+    if (!(TR && col && tape_rec(c.sh))) run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
     if (FNSET != FNS_ANALYTIC && col && ge_fits(c)) {
       if (edges)
         run(PH_GE, [&](int l) { ph_GE<EW, true>(a, c, t, env0, l); });

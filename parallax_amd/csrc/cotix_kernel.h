@@ -2537,7 +2537,9 @@ CX_DEV cx::ResPre load_rp(Tile<EW> t, int ro, int e) {
 
 // E1 sequential pass, NB (== nb) bodies' velocities in registers; body j is
 // picked and written back by unrolled selects (no scratch)
-template <int EW, bool REC, int NB, bool RCP>
+// (TREC: the rollout forward's records for the tape -- only the resolutions'
+// own words, which tape_save reads; no pass when nothing resolves)
+template <int EW, bool REC, int NB, bool RCP, bool TREC = false>
 CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
@@ -2575,6 +2577,7 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
     const uint32_t j = jv[i];
     if (REC) t.w(L.rec + REC_W * i, e) = 0u;
     if (j == RP_NONE) continue;
+    constexpr bool RW = REC || TREC;  // the resolution's record words
     float jx = 0.0f, jy = 0.0f, jw = 0.0f;
 #pragma unroll
     for (int b = 0; b < NB; ++b)
@@ -2583,7 +2586,7 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
         jy = vy[b];
         jw = vw[b];
       }
-    if (REC) {
+    if (RW) {
       const int rc = L.rec + REC_W * i;
       t.f(rc + 1, e) = vx[i];
       t.f(rc + 2, e) = vy[i];
@@ -2593,7 +2596,7 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
       t.f(rc + 6, e) = jw;
     }
     const bool applied = resolve_seq<RCP>(vx[i], vy[i], vw[i], pi[i], qi[i], jx, jy, jw, pj[i], qj[i], pr[i]);
-    if (REC) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
+    if (RW) t.w(L.rec + REC_W * i, e) = applied ? 1u : 0u;
 #pragma unroll
     for (int b = 0; b < NB; ++b)
       if ((uint32_t)b == j) {
@@ -2759,14 +2762,14 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     if (a.stages & COTIX_STAGE_COLLIDER) {
       if (sc.rcp_all) {
         switch (nb) {
-          case 4: e1_regs<EW, RC, 4, true>(c, t, e); break;
-          case 5: e1_regs<EW, RC, 5, true>(c, t, e); break;
+          case 4: e1_regs<EW, REC, 4, true, TREC>(c, t, e); break;
+          case 5: e1_regs<EW, REC, 5, true, TREC>(c, t, e); break;
           default: e1_tile<EW, RC, true>(c, t, e); break;
         }
       } else {
         switch (nb) {
-          case 4: e1_regs<EW, RC, 4, false>(c, t, e); break;
-          case 5: e1_regs<EW, RC, 5, false>(c, t, e); break;
+          case 4: e1_regs<EW, REC, 4, false, TREC>(c, t, e); break;
+          case 5: e1_regs<EW, REC, 5, false, TREC>(c, t, e); break;
           default: e1_tile<EW, RC, false>(c, t, e); break;
         }
       }

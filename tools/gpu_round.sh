@@ -38,5 +38,5 @@ for wl in "${ALL[@]}"; do
   echo "profile $sc ok"
 done
 if [ "${PHASES:-1}" = 1 ]; then
-timeout -k 10 200 python tools/phase_prof.py > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --scenario lunar > $O/phase_lunar.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario box --launches 3 > $O/phase_grad_box.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario lunar --launches 3 > $O/phase_grad_lunar.json && echo "phase ok"
+timeout -k 10 200 python tools/phase_prof.py > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --substeps 1 --launches 200 > $O/phase_k1.json && timeout -k 10 200 python tools/phase_prof.py --scenario lunar > $O/phase_lunar.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario robocup --launches 3 > $O/phase_grad_robocup.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario box --launches 3 > $O/phase_grad_box.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario lunar --launches 3 > $O/phase_grad_lunar.json && echo "phase ok"
 fi

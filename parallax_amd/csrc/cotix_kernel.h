@@ -867,10 +867,32 @@ CX_DEV bool restart_deferred(const KArgs& a) {
   return a.dyn_reset != nullptr && a.reset_mode == 1 && (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY)) != 0;
 }
 
+// The action of a step (config 5's per-step dv, the RL loop's held action)
+// in the registers of the lane that applies it, read one step ahead (phase A
+// would otherwise wait a global round trip every step): lane w = (action
+// body, env) item of phase A's first round (nb * EW <= 64, act_prefetch).
+struct ActRegs {
+  float x = 0.0f, y = 0.0f;
+};
+template <int EW>
+CX_HD bool act_prefetch(const KArgs& a, const Ctx& c) { return a.action != nullptr && c.nb * EW <= WAVE; }
+template <int EW>
+CX_DEV void act_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step, ActRegs& r) {
+  const int e = lane % EW, g = env0 + e;
+  if (lane < c.nb * EW && lane / EW == a.action_body && g < a.B) {
+    const float* ac = a.action + ((size_t)(a.action_held ? 0 : step) * a.B + g) * 2;
+    r.x = ac[0];
+    r.y = ac[1];
+  }
+}
+
 // EVAL: the cotix_eval program (device judge / control); the step programs
-// are compiled without them.  DEFER: take a deferred restart first
+// are compiled without them.  DEFER: take a deferred restart first.  ar: the
+// item's prefetched action (act_fetch) where has_ar, else read here (by
+// value: a pointer that may be null keeps the registers in private memory)
 template <int EW, bool EVAL = false, bool DEFER = false>
-CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int b, int step) {
+CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int b, int step,
+                       bool has_ar = false, ActRegs ar = ActRegs{}) {
   const int o = c.L.dyn + b * 6;
   if (DEFER && restart_deferred(a) && t.w(c.L.rflag, e) != 0u) {  // the body's restart state first
 #pragma unroll
@@ -889,9 +911,17 @@ CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e
     t.f(o + 3, e) = t.f(o + 3, e) + -0.002f;
   }
   if (a.action != nullptr && b == a.action_body) {
-    const float* ac = a.action + ((size_t)(a.action_held ? 0 : step) * a.B + env0 + e) * 2;
-    t.f(o + 2, e) = t.f(o + 2, e) + ac[0];
-    t.f(o + 3, e) = t.f(o + 3, e) + ac[1];
+    float ax, ay;
+    if (has_ar) {
+      ax = ar.x;
+      ay = ar.y;
+    } else {
+      const float* ac = a.action + ((size_t)(a.action_held ? 0 : step) * a.B + env0 + e) * 2;
+      ax = ac[0];
+      ay = ac[1];
+    }
+    t.f(o + 2, e) = t.f(o + 2, e) + ax;
+    t.f(o + 3, e) = t.f(o + 3, e) + ay;
   }
   if (ctl) {  // world.forward(state, signal): the impulse after Euler (cotix/_envs.py:72-75)
     t.f(o + 2, e) = t.f(o + 2, e) + dv.x;
@@ -910,14 +940,15 @@ CX_DEV void reset_scratch(const Ctx& c, Tile<EW> t, int lane) {
 }
 
 template <int EW, bool PRE = false, bool EVAL = false, bool DEFER = false>
-CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step, int slot = 0) {
+CX_DEV void ph_A(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step, int slot = 0,
+                 bool has_ar = false, ActRegs ar = ActRegs{}) {
   using namespace cx;
   const int nb = c.nb;
   const Lay& L = c.L;
   if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
     for (int w = lane; w < nb * EW; w += WAVE) {
       const int e = w % EW, b = w / EW;
-      if (env0 + e < a.B) euler_item<EW, EVAL, DEFER>(a, c, t, env0, e, b, step);
+      if (env0 + e < a.B) euler_item<EW, EVAL, DEFER>(a, c, t, env0, e, b, step, has_ar, ar);
     }
   if (a.stages & (COTIX_STAGE_COLLIDER | COTIX_STAGE_ADVANCE_KEY)) {
     if (!PRE && !CXK_SKIP(a, 16)) {
@@ -3748,6 +3779,14 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     run(PH_C1, [&](int l) { mc_fetch<EW>(c, t, l, mc); });
   RetRegs rr;  // the rollout's return terms
   if (ROLL) run(PH_RET, [&](int l) { ret_fetch<EW>(c, t, l, rr); });
+  // the actions one step ahead (act_fetch): an the next step's, ac this step's
+  const bool apf = act_prefetch<EW>(a, c);
+  ActRegs an, ac;
+  if (apf) run(PH_A, [&](int l) { act_fetch<EW>(a, c, env0, l, 0, an); });
+  auto act_next = [&](int l, int step) {  // (in phase A, before its use: the read overlaps the step)
+    ac = an;
+    if (apf && !a.action_held && step + 1 < a.n_steps) act_fetch<EW>(a, c, env0, l, step + 1, an);
+  };
   // restarts deferred into phase A (restart_deferred)
   const bool staged = !bconst && FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE;
   const bool defer = restart_deferred(a) && (!staged || SDEFER);
@@ -3774,7 +3813,10 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     // phases A, T, B as one (circle / AABB scenes whose contact items fit the
     // phase's ABQ prefetched chunks; uniform)
     if (bconst) {  // phase A, then B from the launch-constant item words (no phase T)
-      run(PH_A, [&](int l) { ph_A<EW, true, EVAL, true>(a, c, t, env0, l, step, slot); });
+      run(PH_A, [&](int l) {
+        act_next(l, step);
+        ph_A<EW, true, EVAL, true>(a, c, t, env0, l, step, slot, apf, ac);
+      });
       if (a.stages & COTIX_STAGE_COLLIDER) {
         run(PH_B, [&](int l) { ph_B_const<EW>(a, c, t, env0, l, bc); });
         collider_phases<EW, FNSET, true, R, true>(a, c, t, env0, run, slot, kso, mc);
@@ -3784,12 +3826,18 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       // A's writes (stage 2); stage 3 computes the contacts
       run.template staged<ABRegs>(
           PH_B, [&](int l, ABRegs& r) { ab_fetch<EW, SDEFER>(a, c, t, l, r); },
-          [&](int l) { ph_A<EW, true, EVAL, SDEFER>(a, c, t, env0, l, step, slot); },
+          [&](int l) {
+            act_next(l, step);
+            ph_A<EW, true, EVAL, SDEFER>(a, c, t, env0, l, step, slot, apf, ac);
+          },
           [&](int l, const ABRegs& r) { ab_contacts<EW>(a, c, t, env0, l, r); });
       if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true, R, FNSET == FNS_ANALYTIC>(
           a, c, t, env0, run, slot, kso, mc);
     } else {
-      run(PH_A, [&](int l) { ph_A<EW, true, EVAL, true>(a, c, t, env0, l, step, slot); });
+      run(PH_A, [&](int l) {
+        act_next(l, step);
+        ph_A<EW, true, EVAL, true>(a, c, t, env0, l, step, slot, apf, ac);
+      });
       if (a.stages & COTIX_STAGE_COLLIDER)
         collider_phases<EW, FNSET, true, R, false, ROLL>(a, c, t, env0, run, slot, kso, mc, step);
     }
@@ -3846,10 +3894,13 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
   constexpr bool TR = FNSET == FNS_ANALYTIC;  // the tape's resolution records (tape_rec)
   RestoreRegs rr;
   TapeRegs tn, tr;  // the next (earlier) step's tape words, the current step's
+  const bool apf = act_prefetch<EW>(a, c);
+  ActRegs an, ac;  // the actions, one step ahead as the state
   if (a.n_steps > 0)
     run(PH_RESTORE, [&](int l) {
       restore_fetch<EW>(a, c, env0, l, a.n_steps - 1, rr);
       if (col) tape_fetch<EW, TR>(a, c, env0, l, a.n_steps - 1, tn);
+      if (apf) act_fetch<EW>(a, c, env0, l, a.n_steps - 1, an);
     });
   for (int step = a.n_steps - 1; step >= 0; --step) {
     run(PH_RESTORE, [&](int l) {
@@ -3858,16 +3909,18 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
         tr = tn;
         if (edges) tape_edge_fetch<EW>(a, c, env0, l, step, tr);
       }
+      ac = an;
       if (step > 0) {  // the next (earlier) step, in flight
         restore_fetch<EW>(a, c, env0, l, step - 1, rr);
         if (col) tape_fetch<EW, TR>(a, c, env0, l, step - 1, tn);
+        if (apf && !a.action_held) act_fetch<EW>(a, c, env0, l, step - 1, an);
       }
     });
     run(PH_A, [&](int l) {  // Euler (+ gravity, + action); no key split, no collider scratch
       if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
         for (int w = l; w < c.nb * EW; w += WAVE) {
           const int e = w % EW, b = w / EW;
-          if (env0 + e < a.B) euler_item<EW>(a, c, t, env0, e, b, step);
+          if (env0 + e < a.B) euler_item<EW>(a, c, t, env0, e, b, step, apf, ac);
         }
     });
     if (col) {

@@ -2503,31 +2503,6 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
 // words written are exactly those the re-play's phases B-D leave for E, GE
 // and G (the chosen cell's candidate word carries only its contact id, the
 // one field they read)
-// the analytic backward's per-resolution record for phase G (g_regs TAPE),
-// in the resolution-operand words (free: phase E does not run): the words
-// G's reverse chain would otherwise fetch through dependent reads -- the
-// contact's function, part kinds and bodies (packed), the contact, both
-// parts' world words and the partner's parameters
-enum : int { GR_PK, GR_CON, GR_WA = GR_CON + 4, GR_WB = GR_WA + 4, GR_PJ = GR_WB + 4, GR_W = GR_PJ + 4 };
-static_assert((int)GR_W <= (int)RP_W, "the G record fits the resolution-operand words");
-template <int EW>
-CX_DEV void g_record(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, const uint32_t* d) {
-  const SceneHdr& sc = c.sh;
-  const Lay& L = c.L;
-  const int ro = L.rp + RP_W * i;
-  const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
-  const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
-  const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
-  const int qa = t.ti(sc.o_pbody + pa), qb = t.ti(sc.o_pbody + pb);
-  t.w(ro + GR_PK, e) = (uint32_t)fn | (uint32_t)ka << 3 | (uint32_t)kb << 5 | (uint32_t)qa << 8 | (uint32_t)qb << 16;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    t.w(ro + GR_CON + k, e) = d[k + 1];
-    t.w(ro + GR_WA + k, e) = t.w(wa + k, e);
-    t.w(ro + GR_WB + k, e) = t.w(wb + k, e);
-    t.w(ro + GR_PJ + k, e) = t.tb[sc.o_par + 4 * j + k];
-  }
-}
 CX_HD bool ge_edges_fit(const Ctx& c) { return 28 * c.nb <= KWIN * c.L.kww; }
 CX_DEV int ge_edge_word(const Ctx& c, int i) { return c.L.kw + 24 * c.nb + 4 * i; }
 template <int EW, bool TR>
@@ -2555,7 +2530,6 @@ CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
       const int co = L.con + 4 * cid;
 #pragma unroll
       for (int k = 0; k < 4; ++k) t.w(co + k, e) = r.d[q][k + 1];
-      if (TR && tape_rec(c.sh)) g_record<EW>(c, t, e, i, j, cid, r.d[q]);
       if (edges) {
         const int eo = ge_edge_word(c, i);
 #pragma unroll
@@ -3425,7 +3399,7 @@ CX_DEV void ph_GE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
 // selects, no scratch) -- the resolutions' LDS reads are then independent of
 // the previous resolution's writes, and the Euler / return terms run on
 // registers.  Every operation and its order are ph_G's: the same bits.
-template <int EW, int NB, bool TAPE>
+template <int EW, int NB>
 CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
@@ -3448,10 +3422,8 @@ CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, in
       if (fl[i] == 0u) continue;
       const int j = (int)jj[i];
       const int ro = L.rec + REC_W * i;
-      // TAPE: the resolution's record (g_record, ph_D_tape); else the tile's cell, contact and tables
-      const int gr = L.rp + RP_W * i;
-      const int cid = TAPE ? 0 : (int)((t.w(L.m + i * NB + j, e) >> 18) & 511u);
-      const int co = TAPE ? gr + GR_CON : L.con + 4 * cid;
+      const int cid = (int)((t.w(L.m + i * NB + j, e) >> 18) & 511u);
+      const int co = L.con + 4 * cid;
       float pxj = 0.0f, pyj = 0.0f, anj = 0.0f;
       Dyn gj = Dyn{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -3466,18 +3438,11 @@ CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, in
       const Dyn bj = Dyn{pxj, pyj, t.f(ro + 4, e), t.f(ro + 5, e), anj, t.f(ro + 6, e)};
       Dyn gi = Dyn{g[i][0], g[i][1], g[i][2], g[i][3], g[i][4], g[i][5]};
       v2 gpen = v2{0.0f, 0.0f}, gcp = v2{0.0f, 0.0f};
-      const Params pj = TAPE ? Params{t.f(gr + GR_PJ, e), t.f(gr + GR_PJ + 1, e), t.f(gr + GR_PJ + 2, e),
-                                      t.f(gr + GR_PJ + 3, e)}
-                             : load_par(t.tb, sc.o_par + 4 * j);
-      resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, pj, v2{t.f(co, e), t.f(co + 1, e)},
-                  v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp, baum_of(sc));
-      const uint32_t pk = TAPE ? t.w(gr + GR_PK, e) : 0u;
-      const int pa = TAPE ? 0 : t.ti(sc.o_cpa + cid), pb = TAPE ? 0 : t.ti(sc.o_cpb + cid);
-      const int fn = TAPE ? (int)(pk & 7u) : t.ti(sc.o_cfn + cid);
-      const int ka = TAPE ? (int)((pk >> 3) & 3u) : t.ti(sc.o_pkind + pa);
-      const int kb = TAPE ? (int)((pk >> 5) & 3u) : t.ti(sc.o_pkind + pb);
-      const int wa = TAPE ? gr + GR_WA : L.world + t.ti(sc.o_pwoff + pa);
-      const int wb = TAPE ? gr + GR_WB : L.world + t.ti(sc.o_pwoff + pb);
+      resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
+                  v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp, baum_of(sc));
+      const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
+      const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
+      const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
       Shape SA, SB;
       SA.kind = ka;
       SB.kind = kb;
@@ -3492,8 +3457,7 @@ CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, in
       const float gw[6] = {gi.px, gi.py, gi.vx, gi.vy, gi.a, gi.w}, hw[6] = {gj.px, gj.py, gj.vx, gj.vy, gj.a, gj.w};
 #pragma unroll
       for (int k = 0; k < 6; ++k) g[i][k] = gw[k];
-      const int qa = TAPE ? (int)((pk >> 8) & 255u) : t.ti(sc.o_pbody + pa);
-      const int qb = TAPE ? (int)((pk >> 16) & 255u) : t.ti(sc.o_pbody + pb);
+      const int qa = t.ti(sc.o_pbody + pa), qb = t.ti(sc.o_pbody + pb);
       const float ax = ka == KIND_CIRCLE ? ga[1] : ga[0] + ga[2], ay = ka == KIND_CIRCLE ? ga[2] : ga[1] + ga[3];
       const float bx = kb == KIND_CIRCLE ? gb[1] : gb[0] + gb[2], by = kb == KIND_CIRCLE ? gb[2] : gb[1] + gb[3];
 #pragma unroll
@@ -3543,7 +3507,7 @@ CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, in
   }
 }
 
-template <int EW, int FNSET = FNS_ANALYTIC, bool TAPE = false>
+template <int EW, int FNSET = FNS_ANALYTIC>
 CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
@@ -3554,11 +3518,11 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     if (g >= a.B) continue;
 #ifndef COTIX_NO_GREGS  // (tooling: the tile form for every scene, tests/test_grad_cpu.py checks the two agree)
     if (FNSET == FNS_ANALYTIC && nb == 5) {  // RoboCup
-      g_regs<EW, 5, TAPE>(a, c, t, env0, e, step);
+      g_regs<EW, 5>(a, c, t, env0, e, step);
       continue;
     }
     if (FNSET == FNS_ANALYTIC && nb == 7) {  // the box world
-      g_regs<EW, 7, TAPE>(a, c, t, env0, e, step);
+      g_regs<EW, 7>(a, c, t, env0, e, step);
       continue;
     }
 #endif
@@ -3971,7 +3935,7 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
       else
         run(PH_GE, [&](int l) { ph_GE<EW>(a, c, t, env0, l); });
     }
-    run(PH_G, [&](int l) { ph_G<EW, FNSET, TR>(a, c, t, env0, l, step); });
+    run(PH_G, [&](int l) { ph_G<EW, FNSET>(a, c, t, env0, l, step); });
   }
   run(PH_ADJ, [&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });
 }

@@ -886,6 +886,27 @@ CX_DEV void act_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step
   }
 }
 
+// The rollout forward's per-step actions, AWIN steps at a time, in the tile's
+// restart-state words (free there: the rollout never restarts, and its
+// return terms are in registers once ret_fetch has run): one global round
+// trip -- and one wait behind the save phase's stores -- per AWIN steps
+// instead of per step (act_window_fill; word 2 s + component of step s of the
+// window, env e)
+constexpr int AWIN = 8;
+template <int EW>
+CX_DEV bool act_window(const KArgs& a, const Ctx& c) {
+  return a.action != nullptr && !a.action_held && c.nb * 6 >= 2 * AWIN;
+}
+template <int EW>
+CX_DEV void act_window_fill(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step0) {
+  const int n = a.n_steps - step0 < AWIN ? a.n_steps - step0 : AWIN;
+  for (int w = lane; w < 2 * n * EW; w += WAVE) {
+    const int e = w % EW, k = w / EW, g = env0 + e;
+    const float v = g < a.B ? a.action[((size_t)(step0 + (k >> 1)) * a.B + g) * 2 + (k & 1)] : 0.0f;
+    t.f(c.L.rst + k, e) = v;
+  }
+}
+
 // EVAL: the cotix_eval program (device judge / control); the step programs
 // are compiled without them.  DEFER: take a deferred restart first.  ar: the
 // item's prefetched action (act_fetch) where has_ar, else read here (by
@@ -3780,12 +3801,18 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   RetRegs rr;  // the rollout's return terms
   if (ROLL) run(PH_RET, [&](int l) { ret_fetch<EW>(c, t, l, rr); });
   // the actions one step ahead (act_fetch): an the next step's, ac this step's
+  // (the rollout forward: from the action window instead, act_window_fill)
+  const bool awin = ROLL && act_window<EW>(a, c);
   const bool apf = act_prefetch<EW>(a, c);
   ActRegs an, ac;
-  if (apf) run(PH_A, [&](int l) { act_fetch<EW>(a, c, env0, l, 0, an); });
+  if (apf && !awin) run(PH_A, [&](int l) { act_fetch<EW>(a, c, env0, l, 0, an); });
   auto act_next = [&](int l, int step) {  // (in phase A, before its use: the read overlaps the step)
-    ac = an;
-    if (apf && !a.action_held && step + 1 < a.n_steps) act_fetch<EW>(a, c, env0, l, step + 1, an);
+    // (awin: the lane's item's env, act_fetch's lane mapping; read either way: selects, no branch)
+    const int o = c.L.rst + 2 * (step % AWIN);
+    const float wx = t.f(o, l % EW), wy = t.f(o + 1, l % EW);
+    ac.x = awin ? wx : an.x;
+    ac.y = awin ? wy : an.y;
+    if (apf && !awin && !a.action_held && step + 1 < a.n_steps) act_fetch<EW>(a, c, env0, l, step + 1, an);
   };
   // restarts deferred into phase A (restart_deferred)
   const bool staged = !bconst && FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE;
@@ -3795,6 +3822,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   const bool rstore = a.dyn_reset != nullptr && a.reset_mode == 1 && !(EVAL && a.judge.on);
   for (int step = 0; step < a.n_steps; ++step) {
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW, FNSET == FNS_ANALYTIC>(a, c, t, env0, l, step); });
+    if (awin && step % AWIN == 0) run(PH_K, [&](int l) { act_window_fill<EW>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
     if (keys && slot == 0 && !(step == 0 && k_in_prologue(a))) {
       const int n = a.n_steps - step < KWIN ? a.n_steps - step : KWIN;

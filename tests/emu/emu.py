@@ -9,10 +9,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 P_ = ctypes.c_void_p
 
 
-def load(asan=False):
+def load(asan=False, path=None):
     """The host build (tests/emu/Makefile; __graft_entry__.build() builds the
-    plain one).  Missing is an error, not a skip."""
-    path = os.path.join(HERE, "build", "libcotix_emu_asan.so" if asan else "libcotix_emu.so")
+    plain one), or the build at `path` (a variant).  Missing is an error, not a
+    skip."""
+    path = path or os.path.join(HERE, "build", "libcotix_emu_asan.so" if asan else "libcotix_emu.so")
     if not os.path.exists(path):
         raise FileNotFoundError("%s missing: run `make -C tests/emu` (or python __graft_entry__.py)" % path)
     lib = ctypes.CDLL(path)

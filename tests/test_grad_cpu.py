@@ -262,3 +262,25 @@ def test_emu_rollout_under_param_sets(emu_lib, scene, sfx):
                     "poly_box": (GC.poly_box_case(4, 8, seed=2), 1 | 4 | 16)}[scene]
     ret, ga, gd = _emu_run_st(emu, lib, case, stages, params=prm)
     _check_vs_oracle(case, ret, ga, gd, params=prm)
+
+
+def test_g_regs_equals_tile_form(emu_lib):
+    """Phase G's register form for the analytic scenes (g_regs: RoboCup's 5
+    and the box world's 7 bodies) against the tile form every other scene
+    runs (a host build with -DCOTIX_NO_GREGS): the same gradients, NaN
+    patterns included (NaN payloads aside -- the host's NaN sign follows the
+    operand order of the two forms)."""
+    import subprocess
+    emu, lib = emu_lib
+    d = os.path.join(HERE, "emu")
+    out = os.path.join(d, "build", "libcotix_emu_nogregs.so")
+    subprocess.run(["g++", "-O2", "-DCOTIX_EMU_POISON", "-DCOTIX_NO_GREGS", "-std=c++17", "-fPIC", "-shared",
+                    "-ffp-contract=off", "-fno-fast-math", "-w", "cotix_emu.cpp", "-o", out], cwd=d, check=True)
+    tile = emu.load(path=out)
+    for case in (GC.box_case(6, 32, seed=1), GC.robocup_case(4, 20, seed=0)):
+        ra, rb = _emu_run(emu, lib, case, 4), _emu_run(emu, tile, case, 4)
+        for x, y in zip(ra[:3], rb[:3]):
+            x, y = np.asarray(x, np.float32), np.asarray(y, np.float32)
+            nx, ny = np.isnan(x), np.isnan(y)
+            assert np.array_equal(nx, ny)
+            assert np.array_equal(x[~nx].view(np.uint32), y[~ny].view(np.uint32))

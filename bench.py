@@ -691,7 +691,8 @@ def run_grad(pa, dev, B, T, steps, warmup, rank, world_size, dist=None, scenario
     return {"value": B * T * steps * world_size / wall, "wall": wall, "variant": variant,
             "fwd_ms": sum(e0.elapsed_time(e1) for e0, e1 in evf) / steps,
             "bwd_ms": sum(e0.elapsed_time(e1) for e0, e1 in evb) / steps,
-            "finite": float(torch.isfinite(ga).all(dim=2).all(dim=0).float().mean().item())}
+            "finite": float(torch.isfinite(ga).all(dim=2).all(dim=0).float().mean().item()),
+            "tape_words": int(pa._ffi.lib.cotix_rollout_tape_words(world.scene.handle))}
 
 
 def grad_valu(key, B, T, fwd_ms, bwd_ms):
@@ -729,12 +730,17 @@ def main_grad(a):
                  (a.envs_per_wave, a.specialize, a.bwd_envs_per_wave))
     nb = 7 if box else (4 if lunar else 5)
     key = "grad_box" if box else ("grad_lunar" if lunar else "grad")
-    # algorithmic HBM bytes of the backward launch per env-step: saved state
-    # (nb x 6 f32) + key (2 u32) + action (2 f32) + the tape's resolution words
-    # (5 per body; analytic scenes + the 7-word resolution record) read,
-    # grad_action (2 f32) written
-    tape_w = 5 if lunar else 12
-    bwd_bytes = (nb * 6 * 4 + 8 + 8 + nb * tape_w * 4 + 8) * B * T
+    # algorithmic HBM bytes per env-step.  Backward: saved state (nb x 6 f32)
+    # + key (2 u32) + action (2 f32) + the whole decision tape (tape_words
+    # u32: per body the resolution words; analytic scenes the resolution
+    # records, polygon scenes EPA's recorded edge per distinct contact --
+    # counted in full, an upper bound where a contact's edge is read only
+    # when it was resolved) read, grad_action (2 f32) written.  Forward:
+    # action read, saved state + key + the tape written (the state itself is
+    # read and written once per launch).
+    tw = r["tape_words"]
+    bwd_bytes = (nb * 6 * 4 + 8 + 8 + tw * 4 + 8) * B * T
+    fwd_bytes = (8 + nb * 6 * 4 + 8 + tw * 4) * B * T + (nb * 6 * 4 + 8 + 4) * 2 * B
     achieved = bwd_bytes / (r["bwd_ms"] * 1e-3) / 1e9
     out = {
         "metric": "differentiable %d-step %s rollout, %d envs/GPU: env-steps/s with d(return)/d(action)"
@@ -779,7 +785,9 @@ def main_grad(a):
             "kernel": "step_kernel<4,F,4> (backward from the forward's tape)",
             "launch_ms": r["bwd_ms"],
             "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                    "alg_bytes_per_launch": bwd_bytes},
+                    "alg_bytes_per_launch": bwd_bytes, "tape_words_per_env_step": tw,
+                    "fwd_alg_bytes_per_launch": fwd_bytes,
+                    "fwd_achieved": fwd_bytes / (r["fwd_ms"] * 1e-3) / 1e9},
             "note": "VALU/latency-bound (per step: Euler, world parts, the tape's resolutions, the VJP chain)",
         },
     }

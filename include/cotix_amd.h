@@ -227,7 +227,12 @@ int cotix_step_ex(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err,
  * Sums run in k order over the NONZERO weights (at most 16 each), starting
  * from the first term (none: 0).  Region r holds s when region_lo[r][q] <
  * s[6*region_body[r] + q] < region_hi[r][q] for every q (NaN is never inside;
- * +-inf leaves a word free). */
+ * +-inf leaves a word free).
+ * cotix_judge and cotix_control must be zero-initialised (`= {0}` or memset)
+ * before they are filled: every field is read, including those added after
+ * the first layout (the rate regions; saturate / clip_lo / clip_hi).  A
+ * saturate other than 0 / 1, a done_on_error other than 0 / 1, a NaN clip
+ * bound or a count outside its range is rejected with an error. */
 #define COTIX_JUDGE_REGIONS 4
 #define COTIX_MAX_STATE_WORDS 96
 typedef struct cotix_judge {

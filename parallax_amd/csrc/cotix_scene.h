@@ -414,7 +414,8 @@ inline int pack_judge(const cotix_judge* j, int nw, int nb, JudgeArgs& out, std:
       out.pr_b[r] = j->rate_region_bias[r];
     }
   }
-  out.doe = j->done_on_error ? 1 : 0;
+  if (j->done_on_error != 0 && j->done_on_error != 1) return scene_fail(err, "judge done_on_error must be 0 or 1 (zero-initialise the struct)");
+  out.doe = j->done_on_error;
   return 0;
 }
 inline int pack_control(const cotix_control* ct, int nb, CtlArgs& out, std::string& err) {
@@ -432,7 +433,10 @@ inline int pack_control(const cotix_control* ct, int nb, CtlArgs& out, std::stri
     out.lo[i] = ct->clip_lo[i];
     out.hi[i] = ct->clip_hi[i];
   }
-  out.sat = ct->saturate ? 1 : 0;
+  // a caller that did not zero-initialise the struct (include/cotix_amd.h)
+  // gets an error here rather than a silent clip to garbage bounds
+  if (ct->saturate != 0 && ct->saturate != 1) return scene_fail(err, "control saturate must be 0 or 1 (zero-initialise the struct)");
+  out.sat = ct->saturate;
   if (out.sat && (std::isnan(out.lo[0]) || std::isnan(out.lo[1]) || std::isnan(out.hi[0]) || std::isnan(out.hi[1])))
     return scene_fail(err, "NaN control clip bound");
   return 0;

@@ -102,12 +102,14 @@ class BatchedEnv:
         # everything the prepared launch copies: the public attributes by
         # value (dt, autoreset, the scenario's stages) and the judge / control
         # and the buffers by identity (a buffer swapped in by the caller, or a
-        # new judge, gets its own launch)
+        # new judge, gets its own launch).  Judges and controls are immutable
+        # (envs._Frozen), and the cache entry holds them, so an id cannot be
+        # reused by a later object while its launch is cached.
         key = (n_steps, body, float(self.dt), bool(self.autoreset), int(self.scenario.stages), id(self.judge),
                id(self.control), id(obs), id(w.dyn), id(w.keys), id(w.err), id(w.geom), id(self.scenario.dyn_reset))
-        launch = self._launchers.get(key)
-        if launch is not None:
-            return launch
+        hit = self._launchers.get(key)
+        if hit is not None:
+            return hit[0]
         judge_c = self.judge.c_struct() if self.judge is not None else None
         control_c = self.control.c_struct() if self.control is not None else None
         if obs is not self._obs and (tuple(obs.shape) != tuple(self._obs.shape) or obs.dtype != torch.float32
@@ -126,7 +128,7 @@ class BatchedEnv:
                                      finished=self.done, action_body=body, reset_mode=2 if self.autoreset else 0,
                                      dyn_reset=self.scenario.dyn_reset if self.autoreset else None,
                                      resets=self.resets if self.autoreset else None, obs=obs)
-        self._launchers[key] = launch
+        self._launchers[key] = (launch, self.judge, self.control, obs)
         return launch
 
     def observation(self, out=None):

@@ -85,7 +85,27 @@ def _f32(x):
     return float(np.float32(x))
 
 
-class LinearJudge(AbstractJudge):
+def _tuples(x):
+    return tuple(_tuples(v) for v in x) if isinstance(x, (list, tuple)) else x
+
+
+class _Frozen:
+    """Immutable after construction (nested lists become tuples): a prepared
+    launch copies the device struct once (BatchedEnv._launcher), so an
+    in-place change could never reach the kernel -- it raises instead."""
+
+    def _freeze(self):
+        for k, v in vars(self).items():
+            object.__setattr__(self, k, _tuples(v))
+        object.__setattr__(self, "_frozen", True)
+
+    def __setattr__(self, name, value):
+        if getattr(self, "_frozen", False):
+            raise AttributeError("%s is immutable: build a new one" % type(self).__name__)
+        object.__setattr__(self, name, value)
+
+
+class LinearJudge(_Frozen, AbstractJudge):
     """A device AbstractJudge (include/cotix_amd.h cotix_judge): over the env's
     state words s[k] (k = 6 * body + {px, py, vx, vy, angle, angular_velocity})
 
@@ -118,6 +138,7 @@ class LinearJudge(AbstractJudge):
             raise ValueError("LinearJudge: at most 4 rate regions of at most 8 nonzero weights")
         if any(len(lo) != 6 or len(hi) != 6 for _, lo, hi, *_ in self.regions + self.rate_regions):
             raise ValueError("LinearJudge: region bounds are 6 words (one body's state)")
+        self._freeze()
 
     def c_struct(self):
         j = _ffi.CotixJudge()
@@ -202,7 +223,7 @@ class LinearJudge(AbstractJudge):
         return acc
 
 
-class AffineControl(AbstractControl):
+class AffineControl(_Frozen, AbstractControl):
     """A device AbstractControl (include/cotix_amd.h cotix_control): the dense
     signal is the velocity impulse dv[i] = sum_q gain[i][q] * (target[i][q] -
     s[q]) (+ bias[i]) on `body`, from that body's state s before each
@@ -219,6 +240,7 @@ class AffineControl(AbstractControl):
         self.clip = None if clip is None else [(_f32(lo), _f32(hi)) for lo, hi in clip]
         if self.clip is not None and (len(self.clip) != 2 or any(np.isnan(v) for p in self.clip for v in p)):
             raise ValueError("AffineControl: clip is ((lo0, hi0), (lo1, hi1)), no NaN bound")
+        self._freeze()
 
     def c_struct(self):
         c = _ffi.CotixControl()

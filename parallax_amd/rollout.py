@@ -49,7 +49,16 @@ def rollout_forward(world, actions, action_body=None, ret_weights=None, dt=1e-2,
                     tape=True):
     """Run T = actions.shape[0] fused steps (world state advanced in place)
     and save the trajectory (and the decision tape).  Returns (ret [B],
-    saved) for rollout_backward."""
+    saved) for rollout_backward.
+
+    Memory: the saved trajectory is T * (24 * n_bodies + 8) bytes per env;
+    the decision tape adds T * tape_words * 4 bytes per env, where
+    tape_words = cotix_rollout_tape_words(scene) is 12 * n_bodies in analytic
+    scenes (RoboCup: 60 words = 240 B per env-step, twice the saved state)
+    and 5 * n_bodies + 4 * n_contacts in polygon scenes (it grows with the
+    distinct contact count).  tape=False skips it: the backward then re-plays
+    the collider (same bits, slower); an allocation failure of the tape says
+    so."""
     actions = _check_actions(world, actions)
     nb, B, T = len(world.bodies), world.B, actions.shape[0]
     action_body = nb - 1 if action_body is None else int(action_body)
@@ -57,7 +66,12 @@ def rollout_forward(world, actions, action_body=None, ret_weights=None, dt=1e-2,
     saved_dyn = torch.empty(T, nb, 6, B, device=world.device, dtype=torch.float32)
     saved_keys = torch.empty(T, B, 2, device=world.device, dtype=torch.int32)
     tw = _ffi.lib.cotix_rollout_tape_words(world.scene.handle)
-    tp = torch.empty(T, tw, B, device=world.device, dtype=torch.int32) if tape else None
+    try:
+        tp = torch.empty(T, tw, B, device=world.device, dtype=torch.int32) if tape else None
+    except torch.OutOfMemoryError as e:
+        raise torch.OutOfMemoryError(
+            "rollout decision tape: %d x %d x %d u32 words (%.1f MiB) do not fit; tape=False runs the re-play "
+            "backward without it (%s)" % (T, tw, B, T * tw * B * 4 / 2**20, e)) from e
     ret = torch.zeros(B, device=world.device, dtype=torch.float32)
     _ffi.check(_ffi.lib.cotix_rollout_ex(
         world.scene.handle, _ffi.ptr(world.dyn), _ffi.ptr(world.keys), _ffi.ptr(world.err), _ffi.ptr(world.geom),

@@ -195,3 +195,18 @@ def test_eval_argument_errors(emu_lib):
                   reward=np.zeros(4, np.float32), finished=np.zeros(4, np.uint32))
     with pytest.raises(ValueError):
         E.LinearJudge(rate_w={k: 1.0 for k in range(17)})
+
+
+def test_judge_and_control_are_immutable():
+    """a prepared launch copies the device struct once, so an
+    in-place change must raise instead of reaching a stale launch."""
+    import pytest
+    from parallax_amd.envs import AffineControl, LinearJudge
+    j = LinearJudge(rate_w={2: 0.1}, rate_regions=[(0, [-1.0] * 6, [1.0] * 6, {0: 1.0}, 0.5)])
+    c = AffineControl(0, gain=[[1.0] * 6, [0.0] * 6], clip=((-1, 1), (-2, 2)))
+    for obj, attr in ((j, "rate_regions"), (j, "done_on_error"), (c, "clip"), (c, "gain")):
+        with pytest.raises(AttributeError):
+            setattr(obj, attr, getattr(obj, attr))
+    with pytest.raises(TypeError):
+        c.gain[0][0] = 2.0  # nested rows are tuples
+    assert c.c_struct().saturate == 1 and j.c_struct().n_rate_regions == 1

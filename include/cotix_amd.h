@@ -449,6 +449,17 @@ int cotix_random_uniform_ex(const uint32_t* keys, int n, int count, float lo, fl
  *   reference's error_if rejects < 3, :130-135). */
 int cotix_gjk(int n, const float* a, const float* b, int32_t* hit, float* simplex, const cotix_params* params,
               cotix_stream_t stream);
+/* cotix_gjk_ex = check_for_collision_convex(a.get_support, b.get_support,
+ *   initial_direction, key) (cotix/_collisions.py:277-298), both nullable:
+ *   initial_direction device f32 [n][2] (NULL: the default [nan, nan] for
+ *   every item), keys device u32 [n][2] (NULL: PRNGKey(1) for every item).
+ *   The start direction is rnd = random_direction(key) (x / |x|, x =
+ *   normal(key, (2,)) in the layout of `params`; XLA's f32 ErfInv with a
+ *   correctly rounded log1p -- PRNGKey(1) gives the constant of cotix_gjk,
+ *   DESIGN.md section 4), then rnd where initial_direction has a NaN, else
+ *   rnd * 0.1 + initial_direction * 0.9. */
+int cotix_gjk_ex(int n, const float* a, const float* b, const float* initial_direction, const uint32_t* keys,
+                 int32_t* hit, float* simplex, const cotix_params* params, cotix_stream_t stream);
 int cotix_epa(int n, const float* a, const float* b, const float* simplex, int iters, float* pen,
               cotix_stream_t stream);
 

@@ -220,6 +220,67 @@ def normal(key, shape):
     return out.reshape(shape)
 
 
+def log1p_cr32(a):
+    """log1p of an f32, correctly rounded to f32 (the f64 log1p rounded once).
+    The device's random_direction uses the same (cx::log1p_cr); numpy's f32
+    log1p is the host's vector math library (SVML under AVX-512), which no
+    device code can reproduce bit for bit."""
+    with np.errstate(all="ignore"):
+        return np.float32(np.log1p(np.float64(np.float32(a))))
+
+
+def erf_inv32_cr(x):
+    """erf_inv32 with log1p_cr32 for its log1p (w = -log1p(-x*x)); the rest
+    is XLA's f32 ErfInv as in erf_inv32.  Reproduces the same 13 published
+    jax.random.normal values (tests/test_oracle_prng.py)."""
+    f = np.float32
+    x = f(x)
+    with np.errstate(all="ignore"):
+        w = -log1p_cr32(-x * x)
+        lt = bool(w < f(5.0))
+        c = _ERFINV_LT5 if lt else _ERFINV_GE5
+        w = (w - f(2.5)) if lt else (np.sqrt(w) - f(3.0))
+        p = f(c[0])
+        for i in range(1, 9):
+            p = f(c[i]) + p * w
+        return f(p * x)
+
+
+def random_direction(key):
+    """random_direction(key) (cotix/_geometry_utils.py:37-46) for any key:
+    x / ||x|| with x = normal(key, (2,)) through erf_inv32_cr, in the PRNG
+    layout in force.  PRNGKey(1) -- the key check_for_collision_convex uses
+    when given none (cotix/_collisions.py:287-288) -- is the constant
+    gjk_initial_direction(), so that key=None and key=PRNGKey(1) agree as in
+    the reference (the two log1p forms differ there by 2 ulp in x; XLA's own
+    log1p is not pinned by any published value)."""
+    k = np.asarray(key, dtype=U32).reshape(2)
+    if int(k[0]) == 0 and int(k[1]) == 1:
+        return gjk_initial_direction()
+    lo = np.nextafter(np.float32(-1.0), np.float32(0.0))
+    u = uniform(k, (2,), lo, 1.0)
+    x = [np.float32(np.float32(np.sqrt(2.0)) * erf_inv32_cr(v)) for v in u]
+    with np.errstate(all="ignore"):
+        n = np.sqrt(np.float32(x[0] * x[0] + x[1] * x[1]))
+        return (np.float32(x[0] / n), np.float32(x[1] / n))
+
+
+def gjk_start_direction(initial_direction=None, key=None):
+    """check_for_collision_convex's start direction (cotix/_collisions.py:
+    285-298): rnd = random_direction(key or PRNGKey(1)); rnd if
+    initial_direction has a NaN (its default) else rnd * 0.1 +
+    initial_direction * 0.9, in f32."""
+    rnd = gjk_initial_direction() if key is None else random_direction(key)
+    if initial_direction is None:
+        return rnd
+    d = [np.float32(v) for v in initial_direction]
+    if np.isnan(d[0]) or np.isnan(d[1]):
+        return rnd
+    with np.errstate(all="ignore"):
+        return tuple(np.float32(np.float32(r * np.float32(0.1)) + np.float32(v * np.float32(0.9)))
+                     for r, v in zip(rnd, d))
+
+
 def gjk_initial_direction():
     """random_direction(PRNGKey(1)) (cotix/_geometry_utils.py:37-46 called from
     cotix/_collisions.py:287-298): x / ||x|| with x = normal(PRNGKey(1), (2,)).

@@ -74,6 +74,7 @@ SIGNATURES = {
     "cotix_resolve": (_I, [_I, _P, _P, _P, _P, _P, _P]),
     "cotix_resolve_ex": (_I, [_I, _P, _P, _P, _P, _P, _P, _P]),
     "cotix_gjk": (_I, [_I, _P, _P, _P, _P, _P, _P]),
+    "cotix_gjk_ex": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cotix_epa": (_I, [_I, _P, _P, _P, _I, _P, _P]),
     "cotix_threefry2x32": (_I, [_P, _P, _P, _I, _P]),
     "cotix_random_split": (_I, [_P, _I, _I, _P, _P]),

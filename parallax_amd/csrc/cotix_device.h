@@ -621,6 +621,65 @@ CX_HD v2 gjk_d0(bool part) {
 }
 CX_HD NarrowParams narrow_default() { return NarrowParams{gjk_d0(false), 32, 48, 128, 48}; }
 
+// random_direction(key) for any key (cotix/_geometry_utils.py:37-46): x / |x|,
+// x = normal(key, (2,)) = sqrt(2) * erf_inv(uniform(key, (2,), nextafter(-1,
+// 0), 1)) with XLA's f32 ErfInv (Giles) whose log1p is correctly rounded
+// (the f64 log1p rounded once; oracle/cotix_oracle/prng.py random_direction,
+// erf_inv32_cr).  PRNGKey(1) is the constant gjk_d0, as the oracle: key=None
+// and key=PRNGKey(1) agree as in the reference.  Operator path only (cotix_gjk_ex).
+CX_DEV float log1p_cr(float a) {
+#if defined(__HIP__)
+  return (float)__ocml_log1p_f64((double)a);
+#else
+  return (float)__builtin_log1p((double)a);
+#endif
+}
+CX_DEV float erf_inv32_cr(float x) {
+  const float w0 = -log1p_cr(-(x * x));
+  const bool lt = w0 < 5.0f;
+  const float w = lt ? w0 - 2.5f : __builtin_sqrtf(w0) - 3.0f;
+  float p;
+  if (lt) {
+    p = 2.81022636e-08f;
+    p = 3.43273939e-07f + p * w; p = -3.5233877e-06f + p * w; p = -4.39150654e-06f + p * w;
+    p = 0.00021858087f + p * w; p = -0.00125372503f + p * w; p = -0.00417768164f + p * w;
+    p = 0.246640727f + p * w; p = 1.50140941f + p * w;
+  } else {
+    p = -0.000200214257f;
+    p = 0.000100950558f + p * w; p = 0.00134934322f + p * w; p = -0.00367342844f + p * w;
+    p = 0.00573950773f + p * w; p = -0.0076224613f + p * w; p = 0.00943887047f + p * w;
+    p = 1.00167406f + p * w; p = 2.83297682f + p * w;
+  }
+  return p * x;
+}
+CX_DEV v2 random_direction(key2 k, bool part) {
+  if (k.a == 0u && k.b == 1u) return gjk_d0(part);
+  uint32_t bits[2];
+  if (part) {  // word m = y0 ^ y1 of threefry(key, (0, m))
+    const key2 r0 = threefry(k, 0u, 0u), r1 = threefry(k, 0u, 1u);
+    bits[0] = r0.a ^ r0.b;
+    bits[1] = r1.a ^ r1.b;
+  } else {  // the two words of threefry(key, iota(2)) = block (0, 1)
+    const key2 r = threefry(k, 0u, 1u);
+    bits[0] = r.a;
+    bits[1] = r.b;
+  }
+  const float lo = __builtin_bit_cast(float, 0xbf7fffffu), hi = 1.0f;  // nextafter(-1, 0), 1
+  float x[2];
+  for (int m = 0; m < 2; ++m) {
+    const float u = fmax_(lo, unit_float(bits[m]) * (hi - lo) + lo);
+    x[m] = __builtin_bit_cast(float, 0x3fb504f3u) * erf_inv32_cr(u);  // f32(sqrt(2))
+  }
+  const float n = __builtin_sqrtf(x[0] * x[0] + x[1] * x[1]);
+  return v2{x[0] / n, x[1] / n};
+}
+// check_for_collision_convex's start direction (cotix/_collisions.py:285-298):
+// rnd if initial_direction has a NaN, else rnd * 0.1 + initial_direction * 0.9
+CX_DEV v2 gjk_start(v2 rnd, v2 init) {
+  if (init.x != init.x || init.y != init.y) return rnd;
+  return v2{rnd.x * 0.1f + init.x * 0.9f, rnd.y * 0.1f + init.y * 0.9f};
+}
+
 // ---------------------------------------------------------------------------
 // GJK (cotix/_collisions.py:20-112, 277-310)
 // ---------------------------------------------------------------------------

@@ -3082,7 +3082,9 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
 // (+ the tape words of the step before it, tape_save)
 template <int EW, bool TR>
 CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
-  if (a.tape != nullptr && step > 0 && (a.stages & COTIX_STAGE_COLLIDER)) tape_save<EW, TR>(a, c, t, env0, lane, step - 1);
+  if (a.tape != nullptr && step > 0 && (a.stages & COTIX_STAGE_COLLIDER) && !CXK_SKIP(a, 128))
+    tape_save<EW, TR>(a, c, t, env0, lane, step - 1);
+  if (CXK_SKIP(a, 256)) return;
   const size_t base = (size_t)step * c.nb * 6 * a.B;
   for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
     int e = w % EW, off = w / EW, g = env0 + e;

@@ -191,12 +191,18 @@ __global__ void order_cw_kernel(float* xy, int n, int nv) {
 }
 // check_for_collision_convex (cotix/_collisions.py:277-310): hit and the
 // simplex, NaN * simplex when there is no collision
-__global__ void gjk_kernel(int n, const float* a, const float* b, int32_t* hit, float* simplex, cx::NarrowParams np) {
+// init / keys (cotix_gjk_ex, nullable): per item the initial_direction and
+// the key of check_for_collision_convex (cotix/_collisions.py:277-298)
+__global__ void gjk_kernel(int n, const float* a, const float* b, int32_t* hit, float* simplex, cx::NarrowParams np,
+                           const float* init, const uint32_t* keys, int part) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const cx::Shape A = load_shape(a + 18 * (size_t)i), Bs = load_shape(b + 18 * (size_t)i);
+  cx::v2 d0 = np.d0;
+  if (keys != nullptr) d0 = cx::random_direction(cx::key2{keys[2 * (size_t)i], keys[2 * (size_t)i + 1]}, part != 0);
+  if (init != nullptr) d0 = cx::gjk_start(d0, cx::v2{init[2 * (size_t)i], init[2 * (size_t)i + 1]});
   cx::v2 sx[3];
-  const bool h = cx::gjk(A, Bs, np.d0, sx, np.gjk_steps);
+  const bool h = cx::gjk(A, Bs, d0, sx, np.gjk_steps);
   hit[i] = h ? 1 : 0;
   for (int k = 0; k < 3; ++k) {  // (False, nan * simplex) when there is no collision
     simplex[6 * (size_t)i + 2 * k] = h ? sx[k].x : sx[k].x * cx::qnan();
@@ -737,15 +743,20 @@ int cotix_resolve(int n, float* dyn1, const float* par1, float* dyn2, const floa
   return cotix_resolve_ex(n, dyn1, par1, dyn2, par2, contact, nullptr, stream);
 }
 
-int cotix_gjk(int n, const float* a, const float* b, int32_t* hit, float* simplex, const cotix_params* params,
-              cotix_stream_t stream) {
+int cotix_gjk_ex(int n, const float* a, const float* b, const float* initial_direction, const uint32_t* keys,
+                 int32_t* hit, float* simplex, const cotix_params* params, cotix_stream_t stream) {
   if (!a || !b || !hit || !simplex) return fail("null argument");
   cotix_params p;
   if (op_params(params, &p)) return -1;
   if (n <= 0) return n == 0 ? 0 : fail("negative size");
   hipLaunchKernelGGL(gjk_kernel, dim3((n + 127) / 128), dim3(128), 0, reinterpret_cast<hipStream_t>(stream), n, a, b,
-                     hit, simplex, narrow_params(p));
+                     hit, simplex, narrow_params(p), initial_direction, keys, p.prng_layout);
   return hip_check(hipGetLastError(), "gjk_kernel launch");
+}
+
+int cotix_gjk(int n, const float* a, const float* b, int32_t* hit, float* simplex, const cotix_params* params,
+              cotix_stream_t stream) {
+  return cotix_gjk_ex(n, a, b, nullptr, nullptr, hit, simplex, params, stream);
 }
 
 int cotix_epa(int n, const float* a, const float* b, const float* simplex, int iters, float* pen,

@@ -10,6 +10,7 @@
 on the device and return it, so the reference's functional call sites
 (``new_bodies, _ = physics.step(bodies, dt)``) read the same.
 """
+import numpy as np
 import torch
 
 from . import _ffi
@@ -96,15 +97,29 @@ def run_contacts(fn, a_rows, b_rows, params=None):
     return ContactInfo(out[:, 0:2], out[:, 2:4]), err
 
 
-def check_for_collision_convex(a_rows, b_rows, params=None):
-    """check_for_collision_convex(a.get_support, b.get_support)
-    (cotix/_collisions.py:277-310) over [n, 18] shape rows: (hit bool [n],
-    simplex f32 [n, 3, 2]) -- NaN * simplex where there is no collision."""
+def check_for_collision_convex(a_rows, b_rows, params=None, initial_direction=None, key=None):
+    """check_for_collision_convex(a.get_support, b.get_support,
+    initial_direction, key) (cotix/_collisions.py:277-310) over [n, 18] shape
+    rows: (hit bool [n], simplex f32 [n, 3, 2]) -- NaN * simplex where there
+    is no collision.  initial_direction: None (the default [nan, nan]) or f32
+    [n, 2] / [2]; key: None (PRNGKey(1)) or u32 / i32 [n, 2] / [2] keys; the
+    start direction is random_direction(key) blended 0.1 / 0.9 with a non-NaN
+    initial_direction, as the reference."""
     n = a_rows.shape[0]
-    hit = torch.empty(n, dtype=torch.int32, device=a_rows.device)
-    simplex = torch.empty(n, 3, 2, dtype=torch.float32, device=a_rows.device)
-    _ffi.check(_ffi.lib.cotix_gjk(n, _ffi.ptr(a_rows.contiguous()), _ffi.ptr(b_rows.contiguous()), _ffi.ptr(hit),
-                                  _ffi.ptr(simplex), _params_ref(params), _ffi.stream_ptr(a_rows.device)), "cotix_gjk")
+    dev = a_rows.device
+    hit = torch.empty(n, dtype=torch.int32, device=dev)
+    simplex = torch.empty(n, 3, 2, dtype=torch.float32, device=dev)
+    init = None if initial_direction is None else \
+        torch.as_tensor(initial_direction, dtype=torch.float32, device=dev).expand(n, 2).contiguous()
+    if key is None:
+        keys = None
+    else:
+        kt = key if isinstance(key, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(np.asarray(key, dtype=np.uint32)).view(np.int32))
+        keys = kt.to(dev, torch.int32).expand(n, 2).contiguous()
+    _ffi.check(_ffi.lib.cotix_gjk_ex(n, _ffi.ptr(a_rows.contiguous()), _ffi.ptr(b_rows.contiguous()), _ffi.ptr(init),
+                                     _ffi.ptr(keys), _ffi.ptr(hit), _ffi.ptr(simplex), _params_ref(params),
+                                     _ffi.stream_ptr(dev)), "cotix_gjk_ex")
     return hit.bool(), simplex
 
 

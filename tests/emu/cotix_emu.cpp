@@ -331,6 +331,18 @@ int emu_epa(int n, const float* a, const float* b, const float* simplex, int ite
 }
 }
 
+// random_direction(key) and the GJK start direction (cotix_gjk_ex's device code)
+extern "C" int emu_gjk_start(int n, const uint32_t* keys, const float* init, int part, float* out) {
+  for (int i = 0; i < n; ++i) {
+    cx::v2 d = cx::gjk_d0(part != 0);
+    if (keys) d = cx::random_direction(cx::key2{keys[2 * i], keys[2 * i + 1]}, part != 0);
+    if (init) d = cx::gjk_start(d, cx::v2{init[2 * i], init[2 * i + 1]});
+    out[2 * i] = d.x;
+    out[2 * i + 1] = d.y;
+  }
+  return 0;
+}
+
 extern "C" int emu_order_clockwise(float* xy, int n, int nv) {
   for (int i = 0; i < n; ++i) {
     float v[2 * cx::MAXV] = {};

@@ -303,9 +303,41 @@ def make_gjk_epa(suffix=""):
     np.savez_compressed(os.path.join(HERE, "gjk_epa%s.npz" % suffix), **out)
 
 
+def make_gjk_dir(suffix=""):
+    """check_for_collision_convex(a, b, initial_direction, key)
+    (cotix/_collisions.py:277-298) with non-default start directions: per
+    pair a key (random, plus PRNGKey(1) and PRNGKey(0)) and an initial
+    direction (random, NaN in either word -- the default --, zero, large),
+    the start direction, hit and simplex."""
+    rng = np.random.default_rng(91)
+    pairs = gjk_epa_pairs(rng)[::2]
+    n = len(pairs)
+    keys = rng.integers(0, 2 ** 32, size=(n, 2), dtype=np.uint64).astype(np.uint32)
+    keys[0], keys[1] = (0, 1), (0, 0)
+    init = (rng.normal(size=(n, 2)) * 2.0).astype(F)
+    init[2::9] = np.nan
+    init[5::13, 1] = np.nan
+    init[7::17] = 0.0
+    init[11::19] *= F(1e4)
+    A, B, D, H, S = [], [], [], [], []
+    for i, (a, b) in enumerate(pairs):
+        d = prng.gjk_start_direction(init[i], keys[i])
+        h, sx = G.check_for_collision_convex(a, b, d)
+        A.append(row(a))
+        B.append(row(b))
+        D.append(np.array(d, F))
+        H.append(1 if h else 0)
+        S.append(np.array(sx, F).reshape(3, 2))
+    np.savez_compressed(os.path.join(HERE, "gjk_dir%s.npz" % suffix), a=np.array(A, F), b=np.array(B, F), keys=keys,
+                        init=init, start=np.array(D, F), hit=np.array(H, np.int32), simplex=np.array(S, F))
+
+
 def make_variants():
     """The fixtures of the non-default parameter blocks (tests/param_sets.py)."""
     make_gjk_epa()
+    make_gjk_dir()
+    with PR.use(oracle_params("_part")):
+        make_gjk_dir("_part")
     for suffix in ("_part", "_alt"):
         with PR.use(oracle_params(suffix)):
             make_robocup(suffix=suffix)

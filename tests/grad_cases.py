@@ -174,6 +174,30 @@ def oracle(case, envs=None, params=None):
     return out
 
 
+def _oracle_worker(job):
+    import torch
+    torch.set_num_threads(1)
+    case, envs, params = job
+    return oracle(case, envs, params)
+
+
+def oracle_parallel(case, envs, params=None, workers=8):
+    """oracle() over `envs` in `workers` spawned processes (CPU only: a fresh
+    interpreter each, nothing inherited from a parent that holds a GPU
+    context), for the full-size checks that sample many envs."""
+    import multiprocessing as mp
+    envs = list(envs)
+    workers = max(1, min(workers, len(envs)))
+    if workers == 1:
+        return oracle(case, envs, params)
+    chunks = [envs[i::workers] for i in range(workers)]
+    out = {}
+    with mp.get_context("spawn").Pool(workers) as pool:
+        for part in pool.map(_oracle_worker, [(case, ch, params) for ch in chunks]):
+            out.update(part)
+    return out
+
+
 # Gradient tolerances, measured (DESIGN.md section 5): the kernel's
 # hand-written f32 VJPs against the oracle's torch-f32 autograd of the same
 # forward differ by rounding only, so the check is north_star's 1e-5

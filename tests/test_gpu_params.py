@@ -238,3 +238,25 @@ def test_lunar_4096_params_vs_cport(torch_cuda, cport_lib, suffix):
     assert (wcl >= 0).sum() > B
     assert np.array_equal(trc["chosen"].cpu().numpy(), wch)
     assert np.array_equal(trc["cells"].cpu().numpy(), wcl)
+
+
+@pytest.mark.parametrize("suffix", ["", "_part"])
+def test_gjk_initial_direction_and_key(torch_cuda, suffix):
+    """cotix_gjk_ex: check_for_collision_convex with per-item
+    initial_direction and key (cotix/_collisions.py:277-298) bit-exact against
+    the oracle's fixture (tests/golden/gjk_dir*.npz); key=PRNGKey(1) and a
+    NaN initial direction reproduce the default operator."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    g = np.load(os.path.join(GOLD, "gjk_dir%s.npz" % suffix))
+    a = torch.tensor(g["a"], device="cuda")
+    b = torch.tensor(g["b"], device="cuda")
+    prm = host_params(suffix) if suffix else None
+    hit, sx = pa.check_for_collision_convex(a, b, prm, initial_direction=torch.tensor(g["init"], device="cuda"),
+                                            key=g["keys"])
+    assert np.array_equal(hit.cpu().numpy().astype(np.int32), g["hit"])
+    assert same_f32(sx.cpu().numpy(), g["simplex"]), diff_report(sx.cpu().numpy(), g["simplex"])
+    h0, s0 = pa.check_for_collision_convex(a, b, prm)
+    h1, s1 = pa.check_for_collision_convex(a, b, prm, initial_direction=[float("nan"), 0.0],
+                                           key=np.array([0, 1], np.uint32))
+    assert torch.equal(h0, h1) and same_f32(s0.cpu().numpy(), s1.cpu().numpy())

@@ -703,28 +703,42 @@ def test_rollout_grad_robocup_vs_oracle(torch_cuda):
 
 def test_rollout_config5_full_size_vs_vjp_oracle(torch_cuda):
     """BASELINE config 5 at full size (4096 envs x 64 steps) checked
-    independently of the kernel's host emulation: 32 envs sampled across the
-    batch (every 128th) against the torch-f32 VJP oracle of the reference
-    step (oracle/cotix_oracle/grad.py, itself checked against finite
-    differences in tests/test_grad_cpu.py): return bit for bit, d(return)/
-    d(action) within 2e-4 (scaled), the same NaN pattern."""
+    independently of the kernel's host emulation, against the torch-f32 VJP
+    oracle of the reference step (oracle/cotix_oracle/grad.py, itself checked
+    against finite differences in tests/test_grad_cpu.py).  On this scene most
+    envs' gradients are NaN (the reference's NaN at step 1 and its error_if
+    trip), so the sample is taken from the GPU run's own split: 32 envs spread
+    over the FINITE-gradient set (every entry compared at GC.ANALYTIC_TOL:
+    rtol 1e-5 elementwise + 1e-7 * max|want|) and 32 over the rest (the NaN
+    pattern compared exactly).  Return bit for bit in all 64.  Prints the floor
+    each sampled block needed."""
     torch = torch_cuda
     import parallax_amd as pa
     import grad_cases as GC
     B, T = 4096, 64
     case = GC.robocup_case(B, T)
     _, ret, ga, _, _ = _gpu_rollout(torch, case, pa.scenarios.robocup_bodies())
-    envs = list(range(0, B, 128))
-    orc = GC.oracle(case, envs)
-    finite = 0
-    for e in envs:
+    fin = np.isfinite(ga).all(axis=(0, 2))  # ga [T, B, 2]
+    fin_envs, nan_envs = np.flatnonzero(fin), np.flatnonzero(~fin)
+    assert len(fin_envs) >= 32 and len(nan_envs) >= 32, (len(fin_envs), len(nan_envs))
+    pick = lambda ids: [int(ids[i]) for i in np.linspace(0, len(ids) - 1, 32).round().astype(int)]  # noqa: E731
+    sf, sn = pick(fin_envs), pick(nan_envs)
+    orc = GC.oracle_parallel(case, sf + sn)
+    need = 0.0
+    for e in sf + sn:
         r, oga, _ = orc[e]
         assert (np.isnan(ret[e]) and np.isnan(r)) or np.float32(ret[e]).view(np.uint32) == np.float32(r).view(
             np.uint32), (e, ret[e], r)
         ok, msg = GC.close(ga[:, e], oga, case["tol"], case["name"])
         assert ok, "env %d %s" % (e, msg)
-        finite += int(np.isfinite(oga).all())
-    assert finite > 0
+        if e in sf:
+            assert np.isfinite(oga).all(), "env %d: finite on the GPU, not in the oracle" % e
+            want = oga.astype(np.float64)
+            m = np.abs(want).max()
+            excess = np.abs(ga[:, e].astype(np.float64) - want) - 1e-5 * np.abs(want)
+            need = max(need, float(excess.max()) / m if m > 0 else 0.0)
+    print("config-5 full size: %d finite / %d NaN-pattern envs compared; floor needed at rtol 1e-5: %.3g"
+          % (len(sf), len(sn), max(need, 0.0)))
 
 
 def test_rollout_config5_full_size_vs_emulation(torch_cuda):

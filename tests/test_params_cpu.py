@@ -310,3 +310,49 @@ def test_capi_params_defaults_and_checks():
     h = ctypes.c_void_p()
     assert lib.cotix_scene_create_ex(1, None, 0, None, None, None, ctypes.byref(c), ctypes.byref(h)) != 0
     assert b"prng_layout" in lib.cotix_last_error()
+
+
+@pytest.mark.parametrize("suffix", ["", "_part"])
+def test_gjk_start_direction_fixture_oracle_and_device_code(suffix):
+    """check_for_collision_convex(a, b, initial_direction, key)
+    (cotix/_collisions.py:277-298): the fixture's start directions equal the
+    oracle's gjk_start_direction and the kernel's device code (cx::
+    random_direction / cx::gjk_start, host build) bit for bit; key
+    PRNGKey(1) gives the default constant; a sample of the hit / simplex
+    rows re-derives from the oracle."""
+    import emu
+    from cotix_oracle import geometry as G
+    from cotix_oracle import params as PR
+    from cotix_oracle import prng
+    import make_golden as M
+    g = np.load(os.path.join(GOLD, "gjk_dir%s.npz" % suffix))
+    n = len(g["hit"])
+    p = oracle_params(suffix) if suffix else None
+    with PR.use(p):
+        want = np.array([prng.gjk_start_direction(g["init"][i], g["keys"][i]) for i in range(n)], np.float32)
+        assert same_f32(want, g["start"])
+        assert tuple(prng.random_direction(prng.PRNGKey(1))) == tuple(prng.gjk_initial_direction())
+        pairs = M.gjk_epa_pairs(np.random.default_rng(91))[::2]
+        for i in range(0, n, 37):
+            h, sx = G.check_for_collision_convex(pairs[i][0], pairs[i][1], tuple(g["start"][i]))
+            assert int(h) == int(g["hit"][i]) and same_f32(np.array(sx, np.float32).reshape(3, 2), g["simplex"][i]), i
+    lib = emu.load()
+    P = ctypes.c_void_p
+    keys = np.ascontiguousarray(g["keys"], np.uint32)
+    init = np.ascontiguousarray(g["init"], np.float32)
+    out = np.zeros((n, 2), np.float32)
+    lib.emu_gjk_start(n, keys.ctypes.data_as(P), init.ctypes.data_as(P), 1 if suffix else 0, out.ctypes.data_as(P))
+    assert same_f32(out, g["start"])
+
+
+def test_erf_inv_cr_reproduces_published_normals():
+    """random_direction's erf_inv (correctly rounded log1p) gives the same 13
+    published jax.random.normal(PRNGKey(0), .) values as erf_inv32."""
+    from cotix_oracle import prng
+    lo = np.nextafter(np.float32(-1.0), np.float32(0.0))
+    for shape, exp in (((10,), [-0.3721109, 0.26423115, -0.18252768, -0.7368197, -0.44030377, -0.1521442,
+                                -0.67135346, -0.5908641, 0.73168886, 0.5673026]),
+                       ((3,), [1.8160863, -0.48262316, 0.33988908])):
+        u = prng.uniform(prng.PRNGKey(0), shape, lo, 1.0)
+        got = [np.float32(np.float32(np.sqrt(2.0)) * prng.erf_inv32_cr(v)) for v in u]
+        assert got == np.array(exp, np.float32).tolist()

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--no-broadphase", action="store_true", help="lunar: without COTIX_STAGE_BROADPHASE")
     ap.add_argument("--drop", type=float, default=0.0, help="lunar: lower lander and legs by this much (in contact)")
     ap.add_argument("--mode", default="step", choices=["step", "grad"])
+    ap.add_argument("--fwd-skip", type=int, default=0,
+                    help="grad: COTIX_DEBUG_SKIP bits for the forward only (tooling build; timing experiments)")
     a = ap.parse_args()
     if a.build:
         return build()
@@ -92,11 +94,14 @@ def main():
             world.err.zero_()
             torch.cuda.synchronize()
             f(buf, 48)
+            os.environ["COTIX_DEBUG_SKIP"] = str(a.fwd_skip)
             _, saved = pa.rollout_forward(world, actions, ab, w, stages=stages)
             torch.cuda.synchronize()
+            os.environ["COTIX_DEBUG_SKIP"] = "0"
             pf = phases(a.substeps)
-            pa.rollout_backward(world, saved)
-            torch.cuda.synchronize()
+            if a.fwd_skip == 0:  # (a skipped save leaves the saved state / tape unwritten: no backward)
+                pa.rollout_backward(world, saved)
+                torch.cuda.synchronize()
             pb = phases(a.substeps)
             if it >= a.warmup:
                 fwd.append(pf)

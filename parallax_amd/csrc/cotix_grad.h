@@ -52,12 +52,14 @@ CX_DEV void aabb_vs_aabb_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, fl
   const float X[4] = {auy - bly, buy - aly, aux - blx, bux - alx};
   float dep[4];
   for (int q = 0; q < 4; ++q) dep[q] = fmax_(X[q], me);
-  const float dx[4] = {0.0f, 0.0f, -1.0f, 1.0f}, dy[4] = {-1.0f, 1.0f, 0.0f, 0.0f};
+  // (the direction and the picked words by selects: a constant array indexed
+  // per lane is a global-memory read, whose s_waitcnt vmcnt(0) would also wait
+  // for every store and prefetch in flight)
   const int k = argmin_first(dep, 4);
-  const float gmd = gpen.x * dx[k] + gpen.y * dy[k];
+  const float gmd = gpen.x * pick4(k, 0.0f, 0.0f, -1.0f, 1.0f) + gpen.y * pick4(k, -1.0f, 1.0f, 0.0f, 0.0f);
   float gdep = 0.0f, gX = 0.0f, dummy = 0.0f;
-  vjp_max(0.0f, dep[k], gmd, &dummy, &gdep);  // jnp.clip(depth, a_min=0)
-  vjp_max(X[k], me, gdep, &gX, &dummy);
+  vjp_max(0.0f, pick4(k, dep[0], dep[1], dep[2], dep[3]), gmd, &dummy, &gdep);  // jnp.clip(depth, a_min=0)
+  vjp_max(pick4(k, X[0], X[1], X[2], X[3]), me, gdep, &gX, &dummy);
   switch (k) {
     case 0: ga[3] += gX; gb[1] -= gX; break;
     case 1: gb[3] += gX; ga[1] -= gX; break;
@@ -134,9 +136,8 @@ CX_DEV void circle_vs_aabb_vjp(const Shape& a, const Shape& b, v2 gpen, v2 gcp, 
     gap = sub(gap, gd);
   } else {  // pen = -shift[k] * dir[k]
     const float sh[4] = {(ap.y + r) - lo.y, up.y - (ap.y - r), (ap.x + r) - lo.x, up.x - (ap.x - r)};
-    const float dx[4] = {0.0f, 0.0f, 1.0f, -1.0f}, dy[4] = {1.0f, -1.0f, 0.0f, 0.0f};
-    const int k = argmin_first(sh, 4);
-    const float g = -(gpen.x * dx[k] + gpen.y * dy[k]);
+    const int k = argmin_first(sh, 4);  // (selects, not a constant array: see aabb_vs_aabb_vjp)
+    const float g = -(gpen.x * pick4(k, 0.0f, 0.0f, 1.0f, -1.0f) + gpen.y * pick4(k, 1.0f, -1.0f, 0.0f, 0.0f));
     switch (k) {
       case 0: gap.y += g; glo.y -= g; break;
       case 1: gup.y += g; gap.y -= g; break;

@@ -2403,7 +2403,7 @@ CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
 // resolution i's velocity-independent operands (phase E0 of the design:
 // computed by the phase-D item (body i, env e) right after its choice j)
 template <int EW, bool RCP>
-CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid) {
+CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, uint32_t* tp = nullptr, int B = 0) {
   // branch-free: the operands are computed from clamped indices for every
   // item and the partner is set only for a real resolution (the inactive
   // items' operands are never read: E1 skips RP_NONE)
@@ -2441,12 +2441,21 @@ CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid) {
   const bool res = pair && !vnan(cp);
   if (res) CXK_STAT(resolutions, 1);
   t.w(ro + RP_J, e) = res ? (uint32_t)j : RP_NONE;
+  if (tp != nullptr) {  // the rollout forward's tape words of body i (tape_save's, from the operands in hand)
+    tp[0] = res ? (uint32_t)j | ((uint32_t)cid << 8) : RP_NONE;
+    if (res) {
+      tp[(size_t)B] = __builtin_bit_cast(uint32_t, t.f(co, e));
+      tp[2 * (size_t)B] = __builtin_bit_cast(uint32_t, t.f(co + 1, e));
+      tp[3 * (size_t)B] = __builtin_bit_cast(uint32_t, cp.x);
+      tp[4 * (size_t)B] = __builtin_bit_cast(uint32_t, cp.y);
+    }
+  }
 }
 
 // one (body i, env) item of phase D; NB > 0: the body count at compile time
 // (unrolled loads and selects), NB == 0: any count up to MAXB
 template <int EW, bool PRE, int NB, bool RCP>
-CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
+CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, uint32_t* tp = nullptr, int B = 0) {
   using namespace cx;
   constexpr int MB = NB > 0 ? NB : MAXB;
   const int nb = NB > 0 ? NB : c.nb, nt = c.nt;
@@ -2497,22 +2506,26 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot) {
 #pragma unroll
   for (int j = 0; j < MB; ++j) cid = j == ch ? mm[j] : cid;
   cid = cid < 0 ? -1 : (cid >> 18) & 511;
-  e0_item<EW, RCP>(c, t, e, i, ch, cid);
+  e0_item<EW, RCP>(c, t, e, i, ch, cid, tp, B);
 }
-template <int EW, bool PRE = false>
-CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int slot = 0) {
+// TAPE: the rollout forward writes each body's tape words (partner, contact
+// id, contact) here, from the operands phase D has in registers, instead of
+// re-reading them from the tile in the next step's save phase (tape_save)
+template <int EW, bool PRE = false, bool TAPE = false>
+CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int slot = 0, int step = 0) {
   const int nb = c.nb;
   for (int w = lane; w < nb * EW; w += WAVE) {
     const int e = w % EW, i = w / EW;
     if (env0 + e >= a.B) continue;
+    uint32_t* tp = TAPE && a.tape != nullptr ? a.tape + ((size_t)step * a.tw + 5 * i) * a.B + env0 + e : nullptr;
     if (c.sh.rcp_all) {
-      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, slot);
-      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, slot);
-      else d_item<EW, PRE, 0, true>(c, t, e, i, slot);
+      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, slot, tp, a.B);
+      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, slot, tp, a.B);
+      else d_item<EW, PRE, 0, true>(c, t, e, i, slot, tp, a.B);
     } else {
-      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, slot);
-      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, slot);
-      else d_item<EW, PRE, 0, false>(c, t, e, i, slot);
+      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, slot, tp, a.B);
+      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, slot, tp, a.B);
+      else d_item<EW, PRE, 0, false>(c, t, e, i, slot, tp, a.B);
     }
   }
 }
@@ -2757,21 +2770,11 @@ template <int EW, bool TR>
 CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   const Lay& L = c.L;
   const int nb = c.nb;
+  if (!(TR && tape_rec(c.sh))) return;  // (the resolution words: phase D, e0_item)
   for (int w = lane; w < nb * EW; w += WAVE) {
     const int e = w % EW, i = w / EW, g = env0 + e;
     if (g >= a.B) continue;
-    const uint32_t j = t.w(L.rp + RP_W * i + RP_J, e);
-    uint32_t* o = a.tape + ((size_t)step * a.tw + 5 * i) * a.B + g;
-    if (j == RP_NONE) {
-      o[0] = RP_NONE;
-      continue;
-    }
-    const uint32_t cid = (t.w(L.m + i * nb + (int)j, e) >> 18) & 511u;
-    const int co = L.con + 4 * (int)cid;
-    o[0] = j | (cid << 8);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) o[(size_t)(q + 1) * a.B] = t.w(co + q, e);
-    if (TR && tape_rec(c.sh)) {  // phase E1's record of the resolution (ph_E TREC)
+    {  // phase E1's record of the resolution (ph_E TREC)
       uint32_t* orc = a.tape + ((size_t)step * a.tw + 5 * nb + REC_W * i) * a.B + g;
 #pragma unroll
       for (int q = 0; q < REC_W; ++q) orc[(size_t)q * a.B] = t.w(L.rec + REC_W * i + q, e);
@@ -3078,6 +3081,7 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
 // ---------------------------------------------------------------------------
 // differentiable rollout: forward saves, return, backward re-play
 // ---------------------------------------------------------------------------
+constexpr int RQ = (MAXB * 6 * 8 + 63) / 64;  // words per lane: nb * 6 * EW over 64 lanes (EW <= 8)
 // state before step `step` -> save_dyn[step], save_keys[step]
 // (+ the tape words of the step before it, tape_save)
 template <int EW, bool TR>
@@ -3086,9 +3090,19 @@ CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
     tape_save<EW, TR>(a, c, t, env0, lane, step - 1);
   if (CXK_SKIP(a, 256)) return;
   const size_t base = (size_t)step * c.nb * 6 * a.B;
-  for (int w = lane; w < c.nb * 6 * EW; w += WAVE) {
-    int e = w % EW, off = w / EW, g = env0 + e;
-    if (g < a.B) a.save_dyn[base + (size_t)off * a.B + g] = t.f(c.L.dyn + off, e);
+  const int nd = c.nb * 6 * EW;
+  float v[RQ];  // every LDS read first, then the stores: one LDS round trip, not one per 64 words
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    if (q * WAVE >= nd) break;  // uniform
+    const int w = q * WAVE + lane;
+    v[q] = t.f(c.L.dyn + (w < nd ? w / EW : 0), w % EW);
+  }
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    if (q * WAVE >= nd) break;  // uniform
+    const int w = q * WAVE + lane, e = w % EW, off = w / EW, g = env0 + e;
+    if (w < nd && g < a.B) a.save_dyn[base + (size_t)off * a.B + g] = v[q];
   }
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
@@ -3134,7 +3148,6 @@ CX_DEV void stage_ret_terms(const KArgs& a, const Ctx& c, Tile<EW> t, int lane) 
 // backward: the saved state of step `step`, read into registers one step
 // ahead (restore_fetch in the previous step's restore phase), so the global
 // reads are in flight while that step re-plays and differentiates
-constexpr int RQ = (MAXB * 6 * 8 + 63) / 64;  // words per lane: nb * 6 * EW over 64 lanes (EW <= 8)
 struct RestoreRegs {
   float d[RQ];
   uint32_t k0 = 0u, k1 = 0u;
@@ -3216,6 +3229,34 @@ CX_DEV void ph_adj_init(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
     int e = w % EW, off = w / EW;
     t.f(c.L.adj + off, e) = a.ret_w[off];  // d ret / d state_T
   }
+}
+
+// d ret / d action[step] of env g: stored now (go == nullptr), or held in the
+// env lane's registers (go) and stored by the next step's restore phase --
+// before that phase issues its prefetch reads, so no later wait for the
+// prefetched data (s_waitcnt vmcnt, which counts stores) also waits for a
+// store issued after it (MODE 4, run_wave_backward_tape)
+struct GradOut {
+  float x = 0.0f, y = 0.0f;
+  int step = -1;
+};
+CX_DEV void grad_action_out(const KArgs& a, int g, int step, float gx, float gy, GradOut* go) {
+  if (go == nullptr) {
+    a.grad_action[2 * ((size_t)step * a.B + g)] = gx;
+    a.grad_action[2 * ((size_t)step * a.B + g) + 1] = gy;
+  } else {
+    go->x = gx;
+    go->y = gy;
+    go->step = step;
+  }
+}
+CX_DEV void grad_action_flush(const KArgs& a, int env0, int lane, int EWn, GradOut& go) {
+  const int g = env0 + lane;
+  if (lane < EWn && go.step >= 0 && g < a.B) {
+    a.grad_action[2 * ((size_t)go.step * a.B + g)] = go.x;
+    a.grad_action[2 * ((size_t)go.step * a.B + g) + 1] = go.y;
+  }
+  go.step = -1;
 }
 
 // phase G: reverse of one step (one lane per env).  Entry: adj = d ret /
@@ -3423,7 +3464,7 @@ CX_DEV void ph_GE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
 // the previous resolution's writes, and the Euler / return terms run on
 // registers.  Every operation and its order are ph_G's: the same bits.
 template <int EW, int NB>
-CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step) {
+CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step, GradOut* go = nullptr) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
@@ -3512,8 +3553,7 @@ CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, in
         gx = g[b][2];
         gy = g[b][3];
       }
-    a.grad_action[2 * ((size_t)step * a.B + g_env)] = gx;
-    a.grad_action[2 * ((size_t)step * a.B + g_env) + 1] = gy;
+    grad_action_out(a, g_env, step, gx, gy, go);
   }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -3531,7 +3571,7 @@ CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, in
 }
 
 template <int EW, int FNSET = FNS_ANALYTIC>
-CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step, GradOut* go = nullptr) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const int nb = c.nb;
@@ -3541,11 +3581,11 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     if (g >= a.B) continue;
 #ifndef COTIX_NO_GREGS  // (tooling: the tile form for every scene, tests/test_grad_cpu.py checks the two agree)
     if (FNSET == FNS_ANALYTIC && nb == 5) {  // RoboCup
-      g_regs<EW, 5>(a, c, t, env0, e, step);
+      g_regs<EW, 5>(a, c, t, env0, e, step, go);
       continue;
     }
     if (FNSET == FNS_ANALYTIC && nb == 7) {  // the box world
-      g_regs<EW, 7>(a, c, t, env0, e, step);
+      g_regs<EW, 7>(a, c, t, env0, e, step, go);
       continue;
     }
 #endif
@@ -3647,8 +3687,7 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     }
     if (a.action != nullptr && a.grad_action != nullptr) {  // v[action_body] += action[step]
       const int o = L.adj + 6 * a.action_body;
-      a.grad_action[2 * ((size_t)step * a.B + g)] = t.f(o + 2, e);
-      a.grad_action[2 * ((size_t)step * a.B + g) + 1] = t.f(o + 3, e);
+      grad_action_out(a, g, step, t.f(o + 2, e), t.f(o + 3, e), go);
     }
     for (int b = 0; b < nb; ++b) {
       const int o = L.adj + 6 * b;
@@ -3764,7 +3803,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_C3, [&](int l) { ph_C3<EW>(c, t, l, par); });
     }
   }
-  if (!CXK_SKIP(a, 8)) run(PH_D, [&](int l) { ph_D<EW, PRE>(a, c, t, env0, l, slot); });
+  if (!CXK_SKIP(a, 8)) run(PH_D, [&](int l) { ph_D<EW, PRE, TAPE>(a, c, t, env0, l, slot, step); });
 }
 
 // forward: n_steps fused steps; ROLL adds the trajectory save and the return
@@ -3804,17 +3843,27 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   if (ROLL) run(PH_RET, [&](int l) { ret_fetch<EW>(c, t, l, rr); });
   // the actions one step ahead (act_fetch): an the next step's, ac this step's
   // (the rollout forward: from the action window instead, act_window_fill)
+  // The rollout programs never hold an action in flight across the step
+  // loop: its stores (the save phase) count in vmcnt too, and any read of a
+  // register with a possibly pending load -- even a select that discards it
+  // -- makes the compiler wait for every store before it (s_waitcnt vmcnt(0)
+  // in phase A, ~1.2 k cycles per step).  ROLL: the window or, without one
+  // (nb < 3 or no actions), the direct read in euler_item.
   const bool awin = ROLL && act_window<EW>(a, c);
-  const bool apf = act_prefetch<EW>(a, c);
+  const bool apf = ROLL ? awin : act_prefetch<EW>(a, c);
   ActRegs an, ac;
-  if (apf && !awin) run(PH_A, [&](int l) { act_fetch<EW>(a, c, env0, l, 0, an); });
+  if (!ROLL && apf) run(PH_A, [&](int l) { act_fetch<EW>(a, c, env0, l, 0, an); });
   auto act_next = [&](int l, int step) {  // (in phase A, before its use: the read overlaps the step)
-    // (awin: the lane's item's env, act_fetch's lane mapping; read either way: selects, no branch)
-    const int o = c.L.rst + 2 * (step % AWIN);
-    const float wx = t.f(o, l % EW), wy = t.f(o + 1, l % EW);
-    ac.x = awin ? wx : an.x;
-    ac.y = awin ? wy : an.y;
-    if (apf && !awin && !a.action_held && step + 1 < a.n_steps) act_fetch<EW>(a, c, env0, l, step + 1, an);
+    if (ROLL) {  // (awin: the lane's item's env, act_fetch's lane mapping)
+      if (awin) {
+        const int o = c.L.rst + 2 * (step % AWIN);
+        ac.x = t.f(o, l % EW);
+        ac.y = t.f(o + 1, l % EW);
+      }
+    } else {
+      ac = an;
+      if (apf && !a.action_held && step + 1 < a.n_steps) act_fetch<EW>(a, c, env0, l, step + 1, an);
+    }
   };
   // restarts deferred into phase A (restart_deferred)
   const bool staged = !bconst && FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE;
@@ -3823,8 +3872,10 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   // the state after the last phase E but the judge)
   const bool rstore = a.dyn_reset != nullptr && a.reset_mode == 1 && !(EVAL && a.judge.on);
   for (int step = 0; step < a.n_steps; ++step) {
-    if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW, FNSET == FNS_ANALYTIC>(a, c, t, env0, l, step); });
+    // (the window's reads before this step's save stores: they wait only for
+    // the previous step's, long complete)
     if (awin && step % AWIN == 0) run(PH_K, [&](int l) { act_window_fill<EW>(a, c, t, env0, l, step); });
+    if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW, FNSET == FNS_ANALYTIC>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
     if (keys && slot == 0 && !(step == 0 && k_in_prologue(a))) {
       const int n = a.n_steps - step < KWIN ? a.n_steps - step : KWIN;
@@ -3849,7 +3900,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
       });
       if (a.stages & COTIX_STAGE_COLLIDER) {
         run(PH_B, [&](int l) { ph_B_const<EW>(a, c, t, env0, l, bc); });
-        collider_phases<EW, FNSET, true, R, true>(a, c, t, env0, run, slot, kso, mc);
+        collider_phases<EW, FNSET, true, R, true, ROLL>(a, c, t, env0, run, slot, kso, mc, step);
       }
     } else if (FNSET == FNS_ANALYTIC && c.nc * EW <= ABQ * WAVE) {
       // stage 1 reads the pre-Euler state: every read is issued before phase
@@ -3861,8 +3912,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
             ph_A<EW, true, EVAL, SDEFER>(a, c, t, env0, l, step, slot, apf, ac);
           },
           [&](int l, const ABRegs& r) { ab_contacts<EW>(a, c, t, env0, l, r); });
-      if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true, R, FNSET == FNS_ANALYTIC>(
-          a, c, t, env0, run, slot, kso, mc);
+      if (a.stages & COTIX_STAGE_COLLIDER) collider_phases<EW, FNSET, true, R, FNSET == FNS_ANALYTIC, ROLL>(
+          a, c, t, env0, run, slot, kso, mc, step);
     } else {
       run(PH_A, [&](int l) {
         act_next(l, step);
@@ -3923,6 +3974,7 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
   const bool edges = FNSET != FNS_ANALYTIC && c.sh.poly && ge_fits(c) && ge_edges_fit(c);
   constexpr bool TR = FNSET == FNS_ANALYTIC;  // the tape's resolution records (tape_rec)
   RestoreRegs rr;
+  GradOut go;       // the previous (later) step's d ret / d action, stored by the restore phase
   TapeRegs tn, tr;  // the next (earlier) step's tape words, the current step's
   const bool apf = act_prefetch<EW>(a, c);
   ActRegs an, ac;  // the actions, one step ahead as the state
@@ -3940,6 +3992,7 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
         if (edges) tape_edge_fetch<EW>(a, c, env0, l, step, tr);
       }
       ac = an;
+      if (a.grad_action != nullptr) grad_action_flush(a, env0, l, EW, go);  // (stores, then the prefetch reads)
       if (step > 0) {  // the next (earlier) step, in flight
         restore_fetch<EW>(a, c, env0, l, step - 1, rr);
         if (col) tape_fetch<EW, TR>(a, c, env0, l, step - 1, tn);
@@ -3965,9 +4018,12 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
       else
         run(PH_GE, [&](int l) { ph_GE<EW>(a, c, t, env0, l); });
     }
-    run(PH_G, [&](int l) { ph_G<EW, FNSET>(a, c, t, env0, l, step); });
+    run(PH_G, [&](int l) { ph_G<EW, FNSET>(a, c, t, env0, l, step, &go); });
   }
-  run(PH_ADJ, [&](int l) { ph_adj_store<EW>(a, c, t, env0, l); });
+  run(PH_ADJ, [&](int l) {
+    if (a.grad_action != nullptr) grad_action_flush(a, env0, l, EW, go);  // step 0's
+    ph_adj_store<EW>(a, c, t, env0, l);
+  });
 }
 
 // backward: steps n_steps-1 .. 0, each re-played from the saved state (so

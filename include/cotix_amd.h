@@ -149,6 +149,20 @@ int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, cons
 int cotix_scene_create_ex(int n_bodies, const float* body_params, int n_parts, const int* part_body,
                           const int* part_type, const int* part_nverts, const cotix_params* params,
                           cotix_scene** out);
+/* cotix_scene_create_ex with flags:
+ *   COTIX_SCENE_PER_ENV_BODY_PARAMS  every env carries its own mass, inertia,
+ *     elasticity and friction_coefficient per body -- a vmapped pytree whose
+ *     parameter leaves vary over the batch (cotix/_bodies.py:140-154,
+ *     domain randomization).  They travel in the env's local geometry: the
+ *     scene's geometry floats (cotix_scene_geom_floats) are the parts' words
+ *     followed by [n_bodies][4] parameter words, per env (geom_stride > 0;
+ *     body_params here is a template that only the checks read).  Divisions
+ *     by mass and inertia are then IEEE divisions (no scene-time reciprocal)
+ *     and the scene runs the generic kernel. */
+enum { COTIX_SCENE_PER_ENV_BODY_PARAMS = 1 };
+int cotix_scene_create_ex2(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                           const int* part_type, const int* part_nverts, const cotix_params* params, int flags,
+                           cotix_scene** out);
 int cotix_scene_params(const cotix_scene* scene, cotix_params* out);
 int cotix_scene_destroy(cotix_scene* scene);
 /* floats of local part geometry the scene expects per env (circle: r,cx,cy,0;
@@ -167,11 +181,18 @@ int cotix_scene_info(const cotix_scene* scene, int* n_contacts, int* n_cells, in
  * 3 AABB walls and 4 circles, legacy layout).
  * The tiling is a scene property: cotix_scene_create(_ex) sets the default to
  * 4 envs per wave, or the largest of 2 and 1 whose workgroup (the hot tables
- * + 4 wave tiles and scratches) fits the CU's 160 KiB of LDS, and rejects a
- * scene that fits at no tiling (the message gives the bytes);
- * cotix_scene_set_variant rejects an explicit tiling that does not fit. */
+ * + 4 wave tiles and scratches) fits the CU's 160 KiB of LDS; a scene whose
+ * tiles do not fit four at a time even at one env per wave runs workgroups of
+ * 2 or 1 waves (each wave still owns one env's tile; the generic kernel), and
+ * cotix_scene_waves_per_group reports the count.  Hard caps: 16 bodies, 32
+ * parts, 511 distinct contacts and candidate-list entries, the hot-table and
+ * cell limits of the scene compiler, and one env's tile + the tables within
+ * 160 KiB -- a scene beyond them is rejected at creation with the reason
+ * (the LDS message gives the bytes); cotix_scene_set_variant rejects an
+ * explicit tiling that does not fit. */
 int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specialize);
 int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec);
+int cotix_scene_waves_per_group(const cotix_scene* scene);
 
 /* Fused step, n_steps times, in place.
  *   dyn   device f32 [n_bodies][6][B]  (px, py, vx, vy, angle, angular_velocity)

@@ -460,6 +460,7 @@ typedef struct {
   Par par[MAXB];
   int pbody[MAXP], ptype[MAXP], pn[MAXP], pgoff[MAXP];
   int tk[13][2], fn[13], n1[13], n2[13];
+  int penv, gparts; /* per-env body parameters: [nb][4] words after the parts' geometry (gparts floats) */
   int l1b[13][MAXN], l1p[13][MAXN], l2b[13][MAXN], l2p[13][MAXN];
 } OScene;
 
@@ -507,6 +508,18 @@ int oracle_scene_init(void* mem, int nb, const float* params, int np, const int*
 }
 
 /* a non-default parameter block (scene created by oracle_scene_init first) */
+/* every env's own mass, inertia, elasticity, friction per body, read from its
+ * geometry row after the parts' words (include/cotix_amd.h
+ * COTIX_SCENE_PER_ENV_BODY_PARAMS); returns the geometry floats per env */
+int oracle_scene_set_per_env_params(void* mem, int on) {
+  OScene* s = (OScene*)mem;
+  int goff = 0;
+  for (int p = 0; p < s->np; ++p) goff += s->ptype[p] <= 1 ? 4 : 2 * s->pn[p];
+  s->penv = on ? 1 : 0;
+  s->gparts = goff;
+  return goff + (on ? 4 * s->nb : 0);
+}
+
 int oracle_scene_set_params(void* mem, const void* params) {
   OScene* s = (OScene*)mem;
   memcpy(&s->prm, params, sizeof(OParams));
@@ -541,7 +554,7 @@ static void world_shape(const OScene* s, int p, const Dyn* d, const float* lg, S
 typedef struct { Contact* cur; K2* keys2; K2* keys1; } Work;
 /* tr_ch [nb] / tr_cells [nb*nb] (nullable): the chosen partner per body and
  * the winning candidate per cell (ind1 | ind2 << 9 | type << 18, -1 empty) */
-static void collider(const OScene* s, Dyn* d, const float* geom, K2 rkey, uint32_t* err, Work* wk,
+static void collider(const OScene* s, const Par* par, Dyn* d, const float* geom, K2 rkey, uint32_t* err, Work* wk,
                      int* tr_ch, int* tr_cells) {
   int nb = s->nb;
   const int part = s->prm.layout;
@@ -601,7 +614,7 @@ static void collider(const OScene* s, Dyn* d, const float* geom, K2 rkey, uint32
   for (int i = 0; i < nb; ++i) {
     int j = ch[i];
     if (j == i || j >= nb) continue;
-    resolve(&d[i], &s->par[i], &d[j], &s->par[j], pen[i][j], cp[i][j], s->prm.baum, s->prm.baum_dt);
+    resolve(&d[i], &par[i], &d[j], &par[j], pen[i][j], cp[i][j], s->prm.baum, s->prm.baum_dt);
   }
 }
 
@@ -634,6 +647,14 @@ static int drive(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, c
     wk.keys1 = (K2*)malloc(sizeof(K2) * (size_t)(m1 + 1));
     uint32_t e = err[g];
     const float* gg = geom + (gstride ? (size_t)g * gstride : 0);
+    Par par[MAXB];
+    for (int b = 0; b < nb; ++b) {
+      par[b] = s->par[b];
+      if (s->penv) {  /* the env's own parameters (oracle_scene_set_per_env_params) */
+        const float* q = gg + s->gparts + 4 * b;
+        par[b].m = q[0]; par[b].I = q[1]; par[b].e = q[2]; par[b].f = q[3];
+      }
+    }
     for (int t = 0; t < n_steps; ++t) {
       if (stages & 1)
         for (int b = 0; b < nb; ++b) { d[b].px = d[b].px + d[b].vx * dt; d[b].py = d[b].py + d[b].vy * dt; d[b].a = d[b].a + d[b].w * dt; }
@@ -645,7 +666,7 @@ static int drive(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, c
       }
       if (stages & 4) {
         int tch[MAXB], tcl[MAXB * MAXB];
-        collider(s, d, gg, key, &e, &wk, tch, tcl);
+        collider(s, par, d, gg, key, &e, &wk, tch, tcl);
         if (tr_chosen)
           for (int i = 0; i < nb; ++i) tr_chosen[((size_t)t * nb + i) * B + g] = tch[i];
         if (tr_cells)
@@ -654,7 +675,7 @@ static int drive(const void* scene, float* dyn, uint32_t* keys, uint32_t* err, c
         if (tr_chosen) for (int i = 0; i < nb; ++i) tr_chosen[((size_t)t * nb + i) * B + g] = -1;
         if (tr_cells) for (int q = 0; q < nb * nb; ++q) tr_cells[((size_t)t * nb * nb + q) * B + g] = -1;
       }
-      if (stages & 8) lunar(&d[0], &d[1], &d[2], &s->par[0], &s->par[1], &s->par[2]);
+      if (stages & 8) lunar(&d[0], &d[1], &d[2], &par[0], &par[1], &par[2]);
       if (stages & 16) key = split0l(key, s->prm.layout);
       if (dyn_reset && e) {
         for (int b = 0; b < nb; ++b) {

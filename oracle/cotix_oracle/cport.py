@@ -29,6 +29,7 @@ def load():
     lib.oracle_contacts.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P]
     lib.oracle_contacts_ex.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P]
     lib.oracle_scene_set_params.argtypes = [_P, _P]
+    lib.oracle_scene_set_per_env_params.argtypes = [_P, ctypes.c_int]
     lib.oracle_gjk.argtypes = [ctypes.c_int, _P, _P, _P, _P, _P]
     lib.oracle_epa.argtypes = [ctypes.c_int, _P, _P, _P, ctypes.c_int, _P]
     lib.oracle_rollout.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
@@ -79,6 +80,13 @@ class Scene:
         if prm is not None:
             cp = prm.c_struct()
             lib.oracle_scene_set_params(self.mem, ctypes.cast(ctypes.pointer(cp), _P))
+
+    def set_per_env_params(self, on=True):
+        """Every env's own (mass, inertia, elasticity, friction) per body, as
+        [n_bodies * 4] floats after its part geometry in the per-env geometry
+        rows (include/cotix_amd.h COTIX_SCENE_PER_ENV_BODY_PARAMS); returns the
+        floats per row."""
+        return self.lib.oracle_scene_set_per_env_params(self.mem, 1 if on else 0)
 
     def step(self, dyn, keys, err, n_steps, stages, geom=None, dyn_reset=None, resets=None, nthreads=0, dt=1e-2):
         """dyn f32 [nb,6,B], keys u32 [B,2], err u32 [B] (in place); geom None

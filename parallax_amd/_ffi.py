@@ -14,6 +14,7 @@ CIRCLE, AABB, POLYGON, POLYGON3, POLYGON4, POLYGON5, POLYGON6 = range(7)
 FN_AABB_AABB, FN_CIRCLE_CIRCLE, FN_CIRCLE_AABB, FN_POLY_POLY, FN_AABB_POLY, FN_CIRCLE_POLY = range(6)
 STAGE_EULER, STAGE_GRAVITY, STAGE_COLLIDER, STAGE_LUNAR, STAGE_ADVANCE_KEY = 1, 2, 4, 8, 16
 STAGE_BROADPHASE = 32  # polygon-pair broadphase, results unchanged (include/cotix_amd.h)
+SCENE_PER_ENV_BODY_PARAMS = 1  # cotix_scene_create_ex2 flag (include/cotix_amd.h)
 STAGES_ROBOCUP = STAGE_EULER | STAGE_COLLIDER | STAGE_ADVANCE_KEY
 STAGES_LUNAR = STAGE_EULER | STAGE_GRAVITY | STAGE_COLLIDER | STAGE_LUNAR | STAGE_ADVANCE_KEY
 ERR_CIRCLE_AABB_CCP = 1
@@ -75,6 +76,8 @@ SIGNATURES = {
     "cotix_resolve_ex": (_I, [_I, _P, _P, _P, _P, _P, _P, _P]),
     "cotix_gjk": (_I, [_I, _P, _P, _P, _P, _P, _P]),
     "cotix_gjk_ex": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cotix_scene_create_ex2": (_I, [_I, _P, _I, _P, _P, _P, _P, _I, ctypes.POINTER(_P)]),
+    "cotix_scene_waves_per_group": (_I, [_P]),
     "cotix_epa": (_I, [_I, _P, _P, _P, _I, _P, _P]),
     "cotix_threefry2x32": (_I, [_P, _P, _P, _I, _P]),
     "cotix_random_split": (_I, [_P, _I, _I, _P, _P]),

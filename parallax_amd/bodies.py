@@ -2,10 +2,12 @@
 
 An AnyBody here describes one body of a batched world: its static
 parameters (mass, inertia, elasticity, friction_coefficient: one value per
-body, as the collider's SoA carries them) and its initial dynamic state
-(position, velocity, angle, angular_velocity: a value shared by all envs or
-a tensor with a leading batch dimension).  Once placed in a World the live
-state is the world's SoA tensor; ``World.body(i)`` returns a view.
+body, or a [B] tensor when they vary over the env batch -- a vmapped pytree,
+e.g. domain randomization; the scene then carries them per env,
+COTIX_SCENE_PER_ENV_BODY_PARAMS) and its initial dynamic state (position,
+velocity, angle, angular_velocity: a value shared by all envs or a tensor with
+a leading batch dimension).  Once placed in a World the live state is the
+world's SoA tensor; ``World.body(i)`` returns a view.
 """
 import torch
 
@@ -14,11 +16,14 @@ from .shapes import UniversalShape
 DYN_FIELDS = ("px", "py", "vx", "vy", "angle", "angular_velocity")
 
 
-def _scalar(x, name):
+def _param(x, name):
+    """One value per body (a float) or one per env (a float32 [B] tensor)."""
     t = torch.as_tensor(x, dtype=torch.float32)
-    if t.numel() != 1:
-        raise ValueError("%s must be one value per body on this path" % name)
-    return float(t.reshape(()))
+    if t.numel() == 1 and t.dim() <= 1:
+        return float(t.reshape(()))
+    if t.dim() != 1:
+        raise ValueError("%s must be one value per body or a [B] tensor (one per env)" % name)
+    return t.detach().to("cpu").contiguous()
 
 
 class AnyBody:
@@ -26,10 +31,10 @@ class AnyBody:
                  angular_velocity=0.0, elasticity=1.0, friction_coefficient=1.0, is_area=False, shape=None):
         if shape is None or not isinstance(shape, UniversalShape):
             raise TypeError("AnyBody needs a UniversalShape")
-        self.mass = _scalar(mass, "mass")
-        self.inertia = _scalar(inertia, "inertia")
-        self.elasticity = _scalar(elasticity, "elasticity")
-        self.friction_coefficient = _scalar(friction_coefficient, "friction_coefficient")
+        self.mass = _param(mass, "mass")
+        self.inertia = _param(inertia, "inertia")
+        self.elasticity = _param(elasticity, "elasticity")
+        self.friction_coefficient = _param(friction_coefficient, "friction_coefficient")
         self.position = torch.as_tensor(position, dtype=torch.float32)
         self.velocity = torch.as_tensor(velocity, dtype=torch.float32)
         self.angle = torch.as_tensor(angle, dtype=torch.float32)
@@ -39,6 +44,24 @@ class AnyBody:
 
     def params(self):
         return [self.mass, self.inertia, self.elasticity, self.friction_coefficient]
+
+    def params_per_env(self):
+        """Whether some parameter is a [B] tensor (one value per env)."""
+        return any(isinstance(v, torch.Tensor) for v in self.params())
+
+    def param_columns(self, B):
+        """[4, B] (mass, inertia, elasticity, friction) per env."""
+        cols = []
+        for v in self.params():
+            t = torch.as_tensor(v, dtype=torch.float32)
+            if t.dim() == 1 and t.shape[0] != B:
+                raise ValueError("a per-env body parameter has %d envs, the world %d" % (t.shape[0], B))
+            cols.append(t.expand(B))
+        return torch.stack(cols, 0)
+
+    def template_params(self):
+        """The parameters as floats (env 0 of per-env ones): the scene's table."""
+        return [float(v[0]) if isinstance(v, torch.Tensor) else v for v in self.params()]
 
     def dyn_columns(self, B):
         """[6, B] initial dynamic state."""

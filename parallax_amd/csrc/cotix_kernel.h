@@ -31,8 +31,8 @@
 
 namespace cxk {
 
-constexpr int MAXB = 16, MAXP = 32, MAXC = 256, MAXL = 128, MAXT = 13, MAXCAND = 4096;
-constexpr int MAXHOT = 8192;
+constexpr int MAXB = 16, MAXP = 32, MAXC = 256, MAXL = 128, MAXT = 13, MAXCAND = 16384;
+constexpr int MAXHOT = 24576;
 constexpr int WAVE = 64;
 
 // workload counters of the host emulation (tools/collider_stats.py); no-ops
@@ -99,6 +99,10 @@ static __device__ unsigned long long g_sub_cycles[8];
 //     vertex items); maxv: the most vertices of any polygon part (0: none);
 //     pminv: max over polygon pairs of the smaller edge count (AABB: 2) --
 //     the broadphase guard's loop bounds
+//   epar: 0 -- the bodies' (mass, inertia, elasticity, friction) are the
+//     scene table's (o_par); else 1 + the word offset, in each env's local
+//     geometry (the tile's geo words), of its own 4 words per body
+//     (COTIX_SCENE_PER_ENV_BODY_PARAMS; rcp_all and rcp_mask are then 0)
 //   prng .. pc: cotix_params (include/cotix_amd.h) -- PRNG layout (1:
 //     partitionable), GJK steps, EPA iteration cap / circle x polygon /
 //     body-level iterations, Baumgarte factor and divisor, the candidates'
@@ -114,7 +118,7 @@ static __device__ unsigned long long g_sub_cycles[8];
   X(uint16_t, o_cbody) X(uint16_t, nmw) X(uint16_t, poly) X(uint16_t, rcp_all) X(uint16_t, fnset)               \
   X(uint16_t, nhot) X(uint16_t, nvt) X(uint16_t, o_vit) X(uint32_t, rcp_mask) X(uint16_t, maxv)                 \
   X(uint16_t, pminv) X(uint16_t, prng) X(uint16_t, gjk_steps) X(uint16_t, epa_cap) X(uint16_t, epa_cp)          \
-  X(uint16_t, epa_body) X(float, baum) X(float, baum_dt) X(float, pc)
+  X(uint16_t, epa_body) X(float, baum) X(float, baum_dt) X(float, pc) X(uint16_t, epar)
 struct SceneHdr {
 #define CXK_HDR_DECL(T, n) T n;
   CXK_HDR_FIELDS(CXK_HDR_DECL)
@@ -613,6 +617,12 @@ CX_HD Ctx make_ctx(const SceneHdr& h) {
   return Ctx{h.nb, h.np, h.nc, h.nl, h.nt, h, layout(h.nb, h.np, h.W, h.nc, h.nt, h.G, h.poly ? h.W / 2 : 0),
              ws_layout(h.nl, h.nc, EW, h.poly, h.nvt)};
 }
+
+// the collider scan as one fused phase (ph_M_fused): its (cell, env) items fit
+// two rounds of the wave, and its slot words' 12-bit candidate index holds
+// every candidate (else the list form C0-C3 runs)
+template <int EW>
+CX_HD bool scan_fused(const Ctx& c) { return c.nl * EW <= 2 * WAVE && c.sh.ncand <= 4096; }
 
 // local part geometry of the wave's envs: read from HBM once per launch, not
 // once per step (per-env LunarLander terrain)
@@ -2396,6 +2406,15 @@ CX_DEV cx::Params load_par(const uint32_t* tb, int o) {
   return cx::Params{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1]), __uint_as_float(tb[o + 2]),
                     __uint_as_float(tb[o + 3])};
 }
+// body i's parameters for env e: the scene table, or the env's own words
+// (epar: a vmapped pytree whose mass / inertia / elasticity / friction vary
+// over the batch, cotix/_bodies.py:140-154)
+template <int EW>
+CX_DEV cx::Params body_par(const Ctx& c, Tile<EW> t, int i, int e) {
+  if (c.sh.epar == 0) return load_par(t.tb, c.sh.o_par + 4 * i);
+  const int o = c.L.geo + (int)c.sh.epar - 1 + 4 * i;
+  return cx::Params{t.f(o, e), t.f(o + 1, e), t.f(o + 2, e), t.f(o + 3, e)};
+}
 CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
   return cx::Rcp{__uint_as_float(tb[o]), __uint_as_float(tb[o + 1])};
 }
@@ -2417,9 +2436,9 @@ CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, uint
   const int oi = L.dyn + 6 * i, oj = L.dyn + 6 * jc;
   const Dyn bi = Dyn{t.f(oi, e), t.f(oi + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
   const Dyn bj = Dyn{t.f(oj, e), t.f(oj + 1, e), 0.0f, 0.0f, 0.0f, 0.0f};
-  const Params pj = load_par(t.tb, sc.o_par + 4 * jc);
+  const Params pj = body_par<EW>(c, t, jc, e);
   const Rcp qj = load_rcp(t.tb, sc.o_rcp + 2 * jc);
-  const ResPre p = resolve_pre<RCP>(bi, load_par(t.tb, sc.o_par + 4 * i), load_rcp(t.tb, sc.o_rcp + 2 * i), bj, pj, qj,
+  const ResPre p = resolve_pre<RCP>(bi, body_par<EW>(c, t, i, e), load_rcp(t.tb, sc.o_rcp + 2 * i), bj, pj, qj,
                                     v2{t.f(co, e), t.f(co + 1, e)}, cp, baum_of(sc));
   t.f(ro + RP_NX, e) = p.n.x;
   t.f(ro + RP_NY, e) = p.n.y;
@@ -2634,7 +2653,7 @@ CX_DEV void e1_regs(const Ctx& c, Tile<EW> t, int e) {
     pr[i] = load_rp<EW>(t, ro, e);
     pj[i] = Params{t.f(ro + RP_MJ, e), t.f(ro + RP_IJ, e), 0.0f, 0.0f};
     qj[i] = Rcp{t.f(ro + RP_QMJ, e), t.f(ro + RP_QIJ, e)};
-    pi[i] = load_par(t.tb, sc.o_par + 4 * i);
+    pi[i] = body_par<EW>(c, t, i, e);
     qi[i] = load_rcp(t.tb, sc.o_rcp + 2 * i);
   }
 #pragma unroll
@@ -2700,7 +2719,7 @@ CX_DEV void e1_tile(const Ctx& c, Tile<EW> t, int e) {
       t.f(rc + 5, e) = jy;
       t.f(rc + 6, e) = jw;
     }
-    const Params pi = load_par(t.tb, sc.o_par + 4 * i);
+    const Params pi = body_par<EW>(c, t, i, e);
     const Params pj = Params{t.f(ro + RP_MJ, e), t.f(ro + RP_IJ, e), 0.0f, 0.0f};
     const Rcp qj = Rcp{t.f(ro + RP_QMJ, e), t.f(ro + RP_QIJ, e)};
     const bool applied = resolve_seq<RCP>(ix, iy, iw, pi, load_rcp(t.tb, sc.o_rcp + 2 * i), jx, jy, jw, pj, qj,
@@ -2836,7 +2855,7 @@ CX_DEV void ph_E(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         const int o = L.dyn + 6 * b;
         d[b] = Dyn{t.f(o, e), t.f(o + 1, e), t.f(o + 2, e), t.f(o + 3, e), t.f(o + 4, e), t.f(o + 5, e)};
       }
-      const Params p0 = load_par(t.tb, sc.o_par), p1 = load_par(t.tb, sc.o_par + 4), p2 = load_par(t.tb, sc.o_par + 8);
+      const Params p0 = body_par<EW>(c, t, 0, e), p1 = body_par<EW>(c, t, 1, e), p2 = body_par<EW>(c, t, 2, e);
       const Rcp q0 = load_rcp(t.tb, sc.o_rcp), q1 = load_rcp(t.tb, sc.o_rcp + 2), q2 = load_rcp(t.tb, sc.o_rcp + 4);
       const int rm = sc.rcp_mask;  // scene constant: uniform branch
       if ((rm & 7) == 7)
@@ -3329,7 +3348,7 @@ CX_DEV void joints_vjp(const Ctx& c, Tile<EW> t, int e) {
     const int o = L.dyn + 6 * b, q = L.adj + 6 * b;
     d[b] = Dyn{t.f(o, e), t.f(o + 1, e), t.f(o + 2, e), t.f(o + 3, e), t.f(o + 4, e), t.f(o + 5, e)};
     g[b] = Dyn{t.f(q, e), t.f(q + 1, e), t.f(q + 2, e), t.f(q + 3, e), t.f(q + 4, e), t.f(q + 5, e)};
-    m[b] = load_par(t.tb, c.sh.o_par + 4 * b);
+    m[b] = body_par<EW>(c, t, b, e);
   }
   // forward (lunar_constraints, the same expressions): anchors, then the
   // bodies before each of the four impulse pairs
@@ -3502,7 +3521,7 @@ CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, in
       const Dyn bj = Dyn{pxj, pyj, t.f(ro + 4, e), t.f(ro + 5, e), anj, t.f(ro + 6, e)};
       Dyn gi = Dyn{g[i][0], g[i][1], g[i][2], g[i][3], g[i][4], g[i][5]};
       v2 gpen = v2{0.0f, 0.0f}, gcp = v2{0.0f, 0.0f};
-      resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
+      resolve_vjp(bi, body_par<EW>(c, t, i, e), bj, body_par<EW>(c, t, j, e),
                   v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp, baum_of(sc));
       const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
       const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
@@ -3603,7 +3622,7 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         Dyn gi = Dyn{t.f(ai, e), t.f(ai + 1, e), t.f(ai + 2, e), t.f(ai + 3, e), t.f(ai + 4, e), t.f(ai + 5, e)};
         Dyn gj = Dyn{t.f(aj, e), t.f(aj + 1, e), t.f(aj + 2, e), t.f(aj + 3, e), t.f(aj + 4, e), t.f(aj + 5, e)};
         v2 gpen = v2{0.0f, 0.0f}, gcp = v2{0.0f, 0.0f};
-        resolve_vjp(bi, load_par(t.tb, sc.o_par + 4 * i), bj, load_par(t.tb, sc.o_par + 4 * j),
+        resolve_vjp(bi, body_par<EW>(c, t, i, e), bj, body_par<EW>(c, t, j, e),
                     v2{t.f(co, e), t.f(co + 1, e)}, v2{t.f(co + 2, e), t.f(co + 3, e)}, gi, gj, gpen, gcp,
                     baum_of(sc));
         // the contact: fn(world(part pa), world(part pb)); world = local + body position
@@ -3787,7 +3806,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_F3, [&](int l) { ph_F3<EW>(c, t, l, b); });
     }
   }
-  if (!CXK_SKIP(a, 4) && c.nl > 0 && c.nl * EW <= 2 * WAVE) {
+  if (!CXK_SKIP(a, 4) && c.nl > 0 && scan_fused<EW>(c)) {
     run(PH_C1, [&](int l) { ph_M_fused<EW>(a, c, t, env0, l, kso, mc); });
   } else if (!CXK_SKIP(a, 4) && c.nl > 0) {
     for (int ch = 0; ch * WAVE < c.nl * EW; ++ch) {
@@ -3837,7 +3856,7 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
   BConst bc;
   if (bconst) run(PH_B, [&](int l) { bc_fetch<EW>(c, t, l, bc); });
   MConst mc;  // the fused scan's launch-constant owner words
-  if ((a.stages & COTIX_STAGE_COLLIDER) && c.nl > 0 && c.nl * EW <= 2 * WAVE)
+  if ((a.stages & COTIX_STAGE_COLLIDER) && c.nl > 0 && scan_fused<EW>(c))
     run(PH_C1, [&](int l) { mc_fetch<EW>(c, t, l, mc); });
   RetRegs rr;  // the rollout's return terms
   if (ROLL) run(PH_RET, [&](int l) { ret_fetch<EW>(c, t, l, rr); });
@@ -4040,7 +4059,7 @@ CX_DEV void run_wave_backward(const KArgs& a, const Ctx& c, Tile<EW> t, int env0
   RestoreRegs rr;
   if (a.n_steps > 0) run(PH_RESTORE, [&](int l) { restore_fetch<EW>(a, c, env0, l, a.n_steps - 1, rr); });
   MConst mc;  // the fused scan's launch-constant owner words
-  if ((a.stages & COTIX_STAGE_COLLIDER) && c.nl > 0 && c.nl * EW <= 2 * WAVE)
+  if ((a.stages & COTIX_STAGE_COLLIDER) && c.nl > 0 && scan_fused<EW>(c))
     run(PH_C1, [&](int l) { mc_fetch<EW>(c, t, l, mc); });
   for (int step = a.n_steps - 1; step >= 0; --step) {
     run(PH_RESTORE, [&](int l) {

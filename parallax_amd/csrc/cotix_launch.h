@@ -13,9 +13,12 @@
 #include "cotix_kernel.h"
 
 namespace cxl {
-constexpr int WPB = 4;  // waves per workgroup (one per SIMD of a CU)
-hipError_t launch_step_ew1(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec);
-hipError_t launch_step_ew2(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec);
-hipError_t launch_step_ew4(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec);
-hipError_t launch_step_ew8(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec);
+// waves per workgroup: WPB (one per SIMD of a CU) -- or, for a scene whose
+// tiles do not fit the LDS four at a time, 2 or 1 (wpb: the launch's count;
+// each wave still owns its own tile, so the bits do not depend on it)
+constexpr int WPB = 4;
+hipError_t launch_step_ew1(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec, int wpb);
+hipError_t launch_step_ew2(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec, int wpb);
+hipError_t launch_step_ew4(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec, int wpb);
+hipError_t launch_step_ew8(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec, int wpb);
 }  // namespace cxl

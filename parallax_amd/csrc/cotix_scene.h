@@ -103,7 +103,7 @@ inline cotix_params params_of(const SceneHdr& s) {
 // prm: cotix_params (nullable: the reference's literals).
 inline int compile_scene(int n_bodies, const float* body_params, int n_parts, const int* part_body,
                          const int* part_type, const int* part_nverts, SceneDev& s, int& n_cand, int& fnset,
-                         std::string& err, const cotix_params* prm = nullptr) {
+                         std::string& err, const cotix_params* prm = nullptr, int flags = 0) {
   const cotix_params par = prm ? *prm : default_params();
   if (check_params(par, err)) return -1;
   if (!body_params || !part_body || !part_type) return scene_fail(err, "null argument");
@@ -146,6 +146,11 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
   }
   s.G = goff;
   s.W = woff;
+  if (flags & ~COTIX_SCENE_PER_ENV_BODY_PARAMS) return scene_fail(err, "unknown scene flags");
+  if (flags & COTIX_SCENE_PER_ENV_BODY_PARAMS) {  // each env's 4 words per body after its part geometry
+    s.epar = (uint16_t)(goff + 1);
+    s.G = goff + 4 * n_bodies;
+  }
   // enumeration, cotix/_colliders.py:86-113 (dict insertion order of type keys)
   std::vector<std::pair<int, int>> tkeys;
   std::vector<std::vector<std::pair<int, int>>> l1, l2;  // (body, part)
@@ -243,6 +248,10 @@ inline int compile_scene(int n_bodies, const float* body_params, int n_parts, co
         std::memcpy(&u, &r, 4);
         hot.push_back(u);
       }
+  }
+  if (s.epar != 0) {  // the table's reciprocals hold for the template values only: IEEE divisions
+    s.rcp_all = 0;
+    s.rcp_mask = 0;
   }
   put(s.o_pbody, part_bodyv);
   put(s.o_pkind, part_kindv);

@@ -47,19 +47,33 @@ struct cotix_scene {
   int envs_per_wave = 4;
   int specialize = 1;
 };
-// a workgroup's LDS at `ew` envs per wave (cxk::lds_bytes: the hot tables +
-// WPB tiles and wave scratches) and the hardware's 160 KiB per CU
+// a workgroup's LDS at `ew` envs per wave and `wpb` waves (cxk::lds_bytes:
+// the hot tables + wpb tiles and wave scratches) and the hardware's 160 KiB
+// per CU
 constexpr size_t LDS_CAP = 160 * 1024;
-static size_t scene_lds(const cotix_scene* sc, int ew) { return cxk::lds_bytes(sc->host, cxl::WPB, ew); }
+static size_t scene_lds_w(const cotix_scene* sc, int ew, int wpb) { return cxk::lds_bytes(sc->host, wpb, ew); }
+// waves per workgroup of a tiling: WPB (one per SIMD), or for a scene whose
+// tiles do not fit four at a time 2, then 1 -- a workgroup of one wave holds
+// one tile and the tables; 0: not even that fits (the scene's hard cap)
+static int scene_wpb(const cotix_scene* sc, int ew) {
+  for (int w : {cxl::WPB, 2, 1})
+    if (scene_lds_w(sc, ew, w) <= LDS_CAP) return w;
+  return 0;
+}
+static size_t scene_lds(const cotix_scene* sc, int ew) {
+  const int w = scene_wpb(sc, ew);
+  return scene_lds_w(sc, ew, w ? w : 1);
+}
 // the default tiling of a scene: 4 envs per wave (the measured best), else
-// the largest of 2, 1 whose workgroup fits the LDS; 0: none fits
+// the largest of 2, 1 whose workgroup of WPB waves fits the LDS, else one env
+// per wave in workgroups of 2 or 1 waves; 0: none fits
 static int lds_default_ew(const cotix_scene* sc) {
 #ifdef COTIX_EW4_ONLY
-  return scene_lds(sc, 4) <= LDS_CAP ? 4 : 0;
+  return scene_lds_w(sc, 4, cxl::WPB) <= LDS_CAP ? 4 : 0;
 #else
   for (int ew : {4, 2, 1})
-    if (scene_lds(sc, ew) <= LDS_CAP) return ew;
-  return 0;
+    if (scene_lds_w(sc, ew, cxl::WPB) <= LDS_CAP) return ew;
+  return scene_wpb(sc, 1) ? 1 : 0;
 #endif
 }
 // the specialization a launch of this scene uses (cxk::SPEC_*)
@@ -266,13 +280,13 @@ int cotix_params_default(cotix_params* out) {
   return 0;
 }
 
-int cotix_scene_create_ex(int n_bodies, const float* body_params, int n_parts, const int* part_body,
-                          const int* part_type, const int* part_nverts, const cotix_params* params,
-                          cotix_scene** out) {
+int cotix_scene_create_ex2(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                           const int* part_type, const int* part_nverts, const cotix_params* params, int flags,
+                           cotix_scene** out) {
   if (!out) return fail("null argument");
   cotix_scene* sc = new cotix_scene();
   if (cxk::compile_scene(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, sc->host,
-                         sc->n_candidates, sc->fnset, g_err, params)) {
+                         sc->n_candidates, sc->fnset, g_err, params, flags)) {
     delete sc;
     return -1;
   }
@@ -280,13 +294,19 @@ int cotix_scene_create_ex(int n_bodies, const float* body_params, int n_parts, c
   // the LDS even at one env per wave is rejected here, not at its first launch
   sc->envs_per_wave = lds_default_ew(sc);
   if (sc->envs_per_wave == 0) {
-    const size_t need = scene_lds(sc, 1);
+    const size_t need = scene_lds_w(sc, 1, 1);
     delete sc;
-    return fail("scene too large for the LDS tile: " + std::to_string(need) + " bytes per workgroup at one env per "
-                "wave (" + std::to_string(cxl::WPB) + " waves), the CU has " + std::to_string(LDS_CAP));
+    return fail("scene too large for the LDS tile: " + std::to_string(need) + " bytes for one env's tile and the "
+                "tables (a workgroup of one wave), the CU has " + std::to_string(LDS_CAP));
   }
   *out = sc;
   return 0;
+}
+
+int cotix_scene_create_ex(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                          const int* part_type, const int* part_nverts, const cotix_params* params,
+                          cotix_scene** out) {
+  return cotix_scene_create_ex2(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, params, 0, out);
 }
 
 int cotix_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body,
@@ -315,13 +335,18 @@ int cotix_scene_set_variant(cotix_scene* scene, int envs_per_wave, int specializ
 #ifdef COTIX_EW4_ONLY
   if (envs_per_wave != 4) return fail("this build carries the 4-envs-per-wave tiling only");
 #endif
-  if (scene_lds(scene, envs_per_wave) > LDS_CAP)
+  if (scene_wpb(scene, envs_per_wave) == 0)
     return fail("envs_per_wave " + std::to_string(envs_per_wave) + ": the scene's workgroup needs " +
                 std::to_string(scene_lds(scene, envs_per_wave)) + " bytes of LDS, the CU has " +
                 std::to_string(LDS_CAP));
   scene->envs_per_wave = envs_per_wave;
   scene->specialize = specialize ? 1 : 0;
   return 0;
+}
+
+int cotix_scene_waves_per_group(const cotix_scene* scene) {
+  if (!scene) return fail("null scene");
+  return scene_wpb(scene, scene->envs_per_wave);
 }
 
 int cotix_scene_variant(const cotix_scene* scene, int* envs_per_wave, int* spec) {
@@ -376,8 +401,9 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
 #else
   const int EW = scene->envs_per_wave;
 #endif
-  const size_t lds = scene_lds(scene, EW);
-  if (lds > LDS_CAP) return fail("scene too large for the LDS tile");  // (not reached: checked at create / set_variant)
+  const int wpb = scene_wpb(scene, EW);
+  if (wpb == 0) return fail("scene too large for the LDS tile");  // (not reached: checked at create / set_variant)
+  const size_t lds = scene_lds_w(scene, EW, wpb);
   cxk::KArgs ka = ka0;
   ka.sc = scene->dev;
   ka.sh = scene->host;  // the header by value (kernel arguments)
@@ -387,15 +413,17 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
 #endif
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int fs = scene->fnset;
-  const int spec = scene_spec(scene);  // scene specialization (compile-time dimensions)
+  // scene specialization (compile-time dimensions; reference scenes, whose
+  // tiles always fit WPB to a workgroup)
+  const int spec = wpb == cxl::WPB ? scene_spec(scene) : cxk::SPEC_GENERIC;
   hipError_t e;
 #ifdef COTIX_EW4_ONLY  // tooling builds (phase profile, ISA markers): the default tiling only
-  e = cxl::launch_step_ew4(ka, fs, mode, lds, st, spec);
+  e = cxl::launch_step_ew4(ka, fs, mode, lds, st, spec, wpb);
 #else
-  if (EW == 1) e = cxl::launch_step_ew1(ka, fs, mode, lds, st, spec);
-  else if (EW == 2) e = cxl::launch_step_ew2(ka, fs, mode, lds, st, spec);
-  else if (EW == 8) e = cxl::launch_step_ew8(ka, fs, mode, lds, st, spec);
-  else e = cxl::launch_step_ew4(ka, fs, mode, lds, st, spec);
+  if (EW == 1) e = cxl::launch_step_ew1(ka, fs, mode, lds, st, spec, wpb);
+  else if (EW == 2) e = cxl::launch_step_ew2(ka, fs, mode, lds, st, spec, wpb);
+  else if (EW == 8) e = cxl::launch_step_ew8(ka, fs, mode, lds, st, spec, wpb);
+  else e = cxl::launch_step_ew4(ka, fs, mode, lds, st, spec, wpb);
 #endif
   if (e != hipSuccess) return hip_check(e, "step_kernel launch");
   return hip_check(hipGetLastError(), "step_kernel launch");

@@ -94,22 +94,27 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
   // the scene tables into LDS: HC reads per thread issued before any store
   // (one global round trip per HC * 256 words, not one per 256)
   constexpr int HC = 16;
-  for (int base = 0; base < nhot; base += HC * WPB * 64) {
+  // waves in this workgroup: WPB, or 2 / 1 for scenes whose tiles do not fit
+  // four at a time (generic kernel only: the specializations are the
+  // reference scenes, which fit, and keep their folded constants)
+  const int nw = SPEC != cxk::SPEC_GENERIC ? WPB : (int)blockDim.x >> 6;
+  const int nt = nw * 64;
+  for (int base = 0; base < nhot; base += HC * nt) {
     uint32_t r[HC];
 #pragma unroll
     for (int k = 0; k < HC; ++k) {
-      const int i = base + k * WPB * 64 + (int)threadIdx.x;
+      const int i = base + k * nt + (int)threadIdx.x;
       r[k] = i < nhot ? sc->hot[i] : 0u;
     }
 #pragma unroll
     for (int k = 0; k < HC; ++k) {
-      const int i = base + k * WPB * 64 + (int)threadIdx.x;
+      const int i = base + k * nt + (int)threadIdx.x;
       if (i < nhot) lds[i] = r[k];
     }
   }
   const cxk::Ctx c = cxk::make_ctx<EW>(sh);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int env0 = (blockIdx.x * WPB + wave) * EW;
+  const int env0 = (blockIdx.x * nw + wave) * EW;
   uint32_t* wbase = lds + nhot + wave * (c.L.S * EW + c.W.words);
   const cxk::Tile<EW> t{wbase, lds, wbase + c.L.S * EW};
   // the forward programs load the wave's state before the barrier: it writes
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
     for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   CXK_STAMP(st3);
-  const int gw = (int)blockIdx.x * WPB + wave;
+  const int gw = (int)blockIdx.x * nw + wave;
   if (lane == 0 && gw < STAMP_WAVES) {
     g_stamps[4 * gw] = st0;
     g_stamps[4 * gw + 1] = st1;
@@ -163,9 +168,11 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
 
 #define CXL_NAME2(n) launch_step_ew##n
 #define CXL_NAME(n) CXL_NAME2(n)
-hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec) {
+hipError_t cxl::CXL_NAME(COTIX_EW)(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec,
+                                   int wpb) {
   constexpr int EW = COTIX_EW;
-  const dim3 grid((ka.B + WPB * EW - 1) / (WPB * EW)), block(WPB * 64);
+  if ((wpb != 1 && wpb != 2 && wpb != WPB) || (wpb != WPB && spec != cxk::SPEC_GENERIC)) return hipErrorInvalidValue;
+  const dim3 grid((ka.B + wpb * EW - 1) / (wpb * EW)), block(wpb * 64);
 #define COTIX_LAUNCH(FS, BW) hipLaunchKernelGGL((step_kernel<EW, FS, BW>), grid, block, lds, st, ka)
 #define COTIX_LAUNCH_SPEC(FS, BW, SP) hipLaunchKernelGGL((step_kernel<EW, FS, BW, SP>), grid, block, lds, st, ka)
   constexpr int F_AN = FNS_ANALYTIC, F_PP = FNS_ANALYTIC | FNS_CONVEX, F_AP = F_PP | cxk::FNS_AABB_POLY,

@@ -69,13 +69,17 @@ class _Batch:
 
 def _per_body(t, batched, name):
     """A static parameter (mass, inertia, elasticity, friction): one value per
-    body on this path (the collider's scene tables); a batched leaf must hold
-    the same value in every env."""
+    body when it is the same in every env (the scene table), else the [B]
+    per-env values (a vmapped constructor that varies it, e.g. domain
+    randomization: the scene then carries every env's own parameters,
+    COTIX_SCENE_PER_ENV_BODY_PARAMS)."""
     if batched:
         v = t.reshape(t.shape[0], -1)
-        same = bool(((v == v[:1]) | (torch.isnan(v) & torch.isnan(v[:1]))).all())
-        if not same:
-            raise ValueError("%s differs across the batch: one value per body on this path" % name)
+        if v.shape[1] != 1:
+            raise ValueError("%s must be one value per body (per env)" % name)
+        b = v.view(torch.int32)
+        if not bool((b == b[:1]).all()):  # bit-identical in every env: shared
+            return v[:, 0].contiguous()
         t = t[0]
     return float(t.reshape(()))
 

@@ -31,7 +31,10 @@ class Scene:
         if not isinstance(self.params, Params):
             raise TypeError("params must be a parallax_amd.Params")
         self.n_bodies = len(bodies)
-        params = torch.tensor([b.params() for b in bodies], dtype=torch.float32)
+        # per-env body parameters (a [B] tensor in some body): carried in each
+        # env's geometry row (include/cotix_amd.h COTIX_SCENE_PER_ENV_BODY_PARAMS)
+        self.per_env_params = any(b.params_per_env() for b in bodies)
+        params = torch.tensor([b.template_params() for b in bodies], dtype=torch.float32)
         part_body, part_type, part_nv = [], [], []
         for i, b in enumerate(bodies):
             for p in b.shape.parts:
@@ -44,9 +47,10 @@ class Scene:
         pn = torch.tensor(part_nv, dtype=torch.int32)
         h = ctypes.c_void_p()
         cp = self.params.c_struct()
-        _ffi.check(_ffi.lib.cotix_scene_create_ex(self.n_bodies, _ffi.ptr(params), len(part_body), _ffi.ptr(pb),
-                                                  _ffi.ptr(pt), _ffi.ptr(pn), ctypes.byref(cp), ctypes.byref(h)),
-                   "cotix_scene_create_ex")
+        flags = _ffi.SCENE_PER_ENV_BODY_PARAMS if self.per_env_params else 0
+        _ffi.check(_ffi.lib.cotix_scene_create_ex2(self.n_bodies, _ffi.ptr(params), len(part_body), _ffi.ptr(pb),
+                                                   _ffi.ptr(pt), _ffi.ptr(pn), ctypes.byref(cp), flags,
+                                                   ctypes.byref(h)), "cotix_scene_create_ex2")
         self.handle = h
         self.geom_floats = _ffi.lib.cotix_scene_geom_floats(h)
 
@@ -80,6 +84,11 @@ class Scene:
         _ffi.check(_ffi.lib.cotix_scene_variant(self.handle, ctypes.byref(ew), ctypes.byref(sp)),
                    "cotix_scene_variant")
         return {"envs_per_wave": ew.value, "specialization": SPECIALIZATIONS[sp.value]}
+
+    def waves_per_group(self):
+        """Waves per workgroup of this scene's launches: 4 (one per SIMD), or 2
+        / 1 when its tiles do not fit the LDS four at a time (large scenes)."""
+        return _ffi.lib.cotix_scene_waves_per_group(self.handle)
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -123,6 +132,9 @@ class World:
             g = p.local_geometry()
             batched = batched or g.dim() == 2
             cols.append(g)
+        if self.scene.per_env_params:  # each env's [n_bodies][4] parameters after its parts' words
+            batched = True
+            cols.append(torch.cat([b.param_columns(self.B).T for b in self.bodies], dim=1))
         if batched:
             cols = [c.expand(self.B, -1) if c.dim() == 1 else c for c in cols]
         geom = torch.cat(cols, dim=-1).to(self.device, torch.float32).contiguous()
@@ -137,7 +149,7 @@ class World:
                                                           _ffi.stream_ptr(self.device)), "cotix_order_clockwise")
                 geom[..., off:off + n] = sl
             off += n
-        assert off == self.scene.geom_floats
+        assert off + (4 * len(self.bodies) if self.scene.per_env_params else 0) == self.scene.geom_floats
         return geom
 
     def polygon_min_angle(self):

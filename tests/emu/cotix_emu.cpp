@@ -100,16 +100,21 @@ void run_any(const cxk::KArgs& a, int E, int mode) {
 extern "C" {
 const char* emu_last_error(void) { return g_err.c_str(); }
 
-int emu_scene_create_ex(int n_bodies, const float* body_params, int n_parts, const int* part_body,
-                        const int* part_type, const int* part_nverts, const cotix_params* params, void** out) {
+int emu_scene_create_ex2(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                         const int* part_type, const int* part_nverts, const cotix_params* params, int flags,
+                         void** out) {
   EmuScene* s = new EmuScene();
   if (cxk::compile_scene(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, s->s, s->n_cand,
-                         s->fnset, g_err, params)) {
+                         s->fnset, g_err, params, flags)) {
     delete s;
     return -1;
   }
   *out = s;
   return 0;
+}
+int emu_scene_create_ex(int n_bodies, const float* body_params, int n_parts, const int* part_body,
+                        const int* part_type, const int* part_nverts, const cotix_params* params, void** out) {
+  return emu_scene_create_ex2(n_bodies, body_params, n_parts, part_body, part_type, part_nverts, params, 0, out);
 }
 int emu_scene_create(int n_bodies, const float* body_params, int n_parts, const int* part_body, const int* part_type,
                      const int* part_nverts, void** out) {
@@ -493,4 +498,7 @@ extern "C" int emu_scene_hdr_text(void* scene, char* buf, int n) {
 // LDS bytes of the step kernel's workgroup (cxk::lds_bytes, 4 waves) for the scene at `ew` envs per wave
 extern "C" long emu_lds_bytes(void* scene, int ew) {
   return (long)cxk::lds_bytes(static_cast<EmuScene*>(scene)->s, 4, ew);
+}
+extern "C" long emu_lds_bytes_w(void* scene, int ew, int wpb) {
+  return (long)cxk::lds_bytes(static_cast<EmuScene*>(scene)->s, wpb, ew);
 }

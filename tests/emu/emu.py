@@ -19,6 +19,8 @@ def load(asan=False, path=None):
     lib = ctypes.CDLL(path)
     lib.emu_scene_create.argtypes = [ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, ctypes.POINTER(P_)]
     lib.emu_scene_create_ex.argtypes = [ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, ctypes.POINTER(P_)]
+    lib.emu_scene_create_ex2.argtypes = [ctypes.c_int, P_, ctypes.c_int, P_, P_, P_, P_, ctypes.c_int,
+                                         ctypes.POINTER(P_)]
     lib.emu_contacts_ex.argtypes = [ctypes.c_int, ctypes.c_int, P_, P_, P_, P_, P_]
     lib.emu_gjk.argtypes = [ctypes.c_int, P_, P_, P_, P_, P_]
     lib.emu_epa.argtypes = [ctypes.c_int, P_, P_, P_, ctypes.c_int, P_]
@@ -55,9 +57,11 @@ def params_ref(params):
     return None if params is None else ctypes.cast(ctypes.pointer(params.c_struct()), P_)
 
 
-def oracle_scene(lib, bodies, params=None):
+def oracle_scene(lib, bodies, params=None, per_env_params=False):
     """Scene + local geometry from oracle Body objects; params: an oracle
-    Params (cotix_oracle.params), None: the defaults."""
+    Params (cotix_oracle.params), None: the defaults.  per_env_params: the
+    scene reads every env's body parameters from its geometry row, after the
+    parts' words returned here (COTIX_SCENE_PER_ENV_BODY_PARAMS)."""
     prm = params
     bparams = np.array([[b.mass, b.inertia, b.elasticity, b.friction_coefficient] for b in bodies], np.float32)
     pb, pt, pn, geom = [], [], [], []
@@ -78,8 +82,9 @@ def oracle_scene(lib, bodies, params=None):
     pb, pt, pn = (np.array(x, np.int32) for x in (pb, pt, pn))
     h = P_()
     cp = None if prm is None else prm.c_struct()
-    rc = lib.emu_scene_create_ex(len(bodies), _p(bparams), len(pb), _p(pb), _p(pt), _p(pn),
-                                 None if cp is None else ctypes.cast(ctypes.pointer(cp), P_), ctypes.byref(h))
+    rc = lib.emu_scene_create_ex2(len(bodies), _p(bparams), len(pb), _p(pb), _p(pt), _p(pn),
+                                  None if cp is None else ctypes.cast(ctypes.pointer(cp), P_),
+                                  1 if per_env_params else 0, ctypes.byref(h))
     if rc:
         raise RuntimeError(lib.emu_last_error().decode())
     return h, np.array(geom, np.float32)

@@ -206,12 +206,16 @@ def oracle_parallel(case, envs, params=None, workers=8):
 # large terms of both signs (contact_from_edges' terms, the polygon vertex
 # chains), whose f32 rounding is relative to the terms, not to the small sum.
 # Measured (tests/test_grad_cpu.py, host emulation == GPU bit for bit; the
-# floor each case needs at rtol 1e-5): RoboCup 0; box world 0 at 40 steps and
-# 5.75e-9 at 32 (one dyn0 entry near zero, the sum of the two walls' terms);
-# LunarLander 1.3e-10; quad row 8.1e-8; polygon box 5.0e-7; octagon pair
-# 1.19e-6 -- ANALYTIC_TOL's 1e-7 is 17x the box world's, POLYGON_TOL's 4e-6
+# floor each case needs at rtol 1e-5): RoboCup 0 on the small cases, but
+# 2.24e-7 at full size (config 5, 4096 x 64: env 2722's d/d action[0], -2.1900
+# vs -2.1899 within a block whose max |want| is 175 -- the first step's
+# gradient sums the whole 64-step chain; 1 of the 32 finite-gradient envs the
+# full-size test samples); box world 0 at 40 steps and 5.75e-9 at 32 (one
+# dyn0 entry near zero, the sum of the two walls' terms); LunarLander 1.3e-10;
+# quad row 8.1e-8; polygon box 5.0e-7; octagon pair 1.19e-6 --
+# ANALYTIC_TOL's 1e-6 is 4.5x RoboCup's full-size need, POLYGON_TOL's 4e-6
 # 3.4x the largest.
-ANALYTIC_TOL = (1e-5, 1e-7)
+ANALYTIC_TOL = (1e-5, 1e-6)
 POLYGON_TOL = (1e-5, 4e-6)
 MEASURED = {}  # name -> the floor the compared blocks needed at rtol 1e-5 (reported by conftest)
 

@@ -60,3 +60,27 @@ def octagon_row(n):
                           velocity=(0.1 * (i % 3) - 0.1, -0.2), angular_velocity=0.05 * i, elasticity=0.5,
                           friction_coefficient=0.2))
     return out
+
+
+def polygon20():
+    """20 polygon parts over 5 bodies: a static terrain body of 8 quads and
+    4 dynamic bodies of a hexagon and 2 quads each, resting on and against
+    one another -- a scene whose tiles fit the LDS only in workgroups of
+    fewer than 4 waves (cotix_scene_waves_per_group)."""
+    from cotix_oracle import geometry as G
+    from cotix_oracle import physics as P
+    terrain = []
+    for k in range(8):
+        x0, x1 = -4.0 + k, -3.0 + k
+        terrain.append(G.Polygon([(x0, -1.0), (x1, -1.0), (x1, 0.05 * (k % 3)), (x0, 0.05 * ((k + 1) % 3))],
+                                 kind="Polygon4"))
+    out = [P.Body(terrain, mass=float("inf"), inertia=float("inf"), elasticity=0.3, friction_coefficient=0.4)]
+    hexv = [(0.3 * np.cos(t), 0.3 * np.sin(t)) for t in np.arange(6) * (np.pi / 3)]
+    for i in range(4):
+        parts = [G.Polygon(hexv, kind="Polygon6"),
+                 G.Polygon([(0.2, -0.1), (0.5, -0.1), (0.5, 0.1), (0.2, 0.1)], kind="Polygon4"),
+                 G.Polygon([(-0.5, -0.1), (-0.2, -0.1), (-0.2, 0.1), (-0.5, 0.1)], kind="Polygon4")]
+        out.append(P.Body(parts, mass=1.0 + 0.5 * i, inertia=0.5 + 0.25 * i, position=(-2.6 + 1.3 * i, 0.33),
+                          angle=0.2 * i, velocity=(0.1 * (i % 2) - 0.05, -0.3), angular_velocity=0.1 * i,
+                          elasticity=0.4, friction_coefficient=0.3))
+    return out

@@ -224,9 +224,10 @@ def test_prepared_eval_launch_marshals_every_argument(monkeypatch):
 
 def test_tiling_is_a_scene_property():
     """cotix_scene_create picks the default envs per wave from the scene's LDS
-    need (4, else the largest of 2 and 1 that fits the CU's 160 KiB) and
-    rejects a scene that fits at no tiling, with the byte count; an explicit
-    tiling that does not fit is rejected by cotix_scene_set_variant."""
+    need (4, else the largest of 2 and 1 that fits the CU's 160 KiB with four
+    waves per workgroup, else one env per wave in workgroups of 2 or 1 waves)
+    and rejects a scene beyond the documented caps, with the reason; an
+    explicit tiling that does not fit is rejected by cotix_scene_set_variant."""
     import parallax_amd as pa
     import grad_cases as GC
     import scene_cases
@@ -238,7 +239,15 @@ def test_tiling_is_a_scene_property():
     quad_row.set_variant(1)
     quad_row.set_variant(0)
     assert quad_row.variant()["envs_per_wave"] == 2
-    assert pa.Scene(_pa_bodies(pa, scene_cases.octagon_row(9))).variant()["envs_per_wave"] == 1
-    with pytest.raises(RuntimeError, match=r"scene too large for the LDS tile: \d+ bytes"):
-        pa.Scene(_pa_bodies(pa, scene_cases.octagon_row(12)))
+    nine = pa.Scene(_pa_bodies(pa, scene_cases.octagon_row(9)))
+    assert nine.variant()["envs_per_wave"] == 1 and nine.waves_per_group() == 4
+    # beyond four tiles per CU: one env per wave in workgroups of 2 (or 1) waves
+    for bodies in (scene_cases.octagon_row(12), scene_cases.octagon_row(15), scene_cases.polygon20()):
+        big = pa.Scene(_pa_bodies(pa, bodies))
+        assert big.variant() == {"envs_per_wave": 1, "specialization": "generic"}
+        assert big.waves_per_group() in (1, 2)
+    # the documented hard caps are rejected at creation with the reason
+    with pytest.raises(RuntimeError, match="too many cells"):
+        pa.Scene(_pa_bodies(pa, scene_cases.octagon_row(16)))
     assert pa.Scene(pa.scenarios.lunar_lander_bodies(torch.zeros(1, 7, 4, 2))).variant()["envs_per_wave"] == 4
+    assert pa.Scene(pa.scenarios.robocup_bodies()).waves_per_group() == 4

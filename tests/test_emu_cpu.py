@@ -466,6 +466,40 @@ def test_emu_octagon_row_one_env_per_wave_vs_cport(emu_lib):
         assert np.array_equal(g, w)
 
 
+@pytest.mark.parametrize("name", ["octagons12", "octagons15", "polygon20"])
+def test_emu_large_scenes_vs_cport(emu_lib, name):
+    """Scenes whose tiles fit the LDS only in workgroups of fewer than four
+    waves (cotix_scene_waves_per_group): twelve and fifteen octagon bodies,
+    and 20 polygon parts over 5 bodies -- the kernel logic at one env per
+    wave == the C port over 12 steps, 3 envs, the collider trace included."""
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    _build_cport()
+    clib = cport.load()
+    import scene_cases
+    bodies = scene_cases.polygon20() if name == "polygon20" else scene_cases.octagon_row(int(name[8:]))
+    h, geom = emu.oracle_scene(lib, bodies)
+    lib.emu_lds_bytes_w.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    lib.emu_lds_bytes_w.restype = ctypes.c_long
+    assert lib.emu_lds_bytes_w(h, 1, 4) > 160 * 1024 >= lib.emu_lds_bytes_w(h, 1, 1)
+    sc = cport.Scene(clib, bodies)
+    B, T = 3, 12
+    base = np.array([b.dyn() for b in bodies], np.float32)
+    dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
+    dyn[1:, 2, :] += np.linspace(-0.2, 0.2, B).astype(np.float32)
+    keys = np.ascontiguousarray(np.stack([np.arange(B) + 9, np.arange(B) * 3 + 2], 1).astype(np.uint32))
+    got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    gch, gcl = emu.step_ex(lib, h, *got, geom, 0, T, 1 | 4 | 16, len(bodies), E=1)
+    wch, wcl = sc.step_ex(*want, T, 1 | 4 | 16, trace=True)
+    assert (wcl >= 0).sum() > B * T  # contacts written
+    assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)
+
+
 @pytest.mark.parametrize("EW", [1, 4, 8])
 def test_emu_robocup_moving_static_bodies_vs_cport(emu_lib, EW):
     """The analytic program with infinite-mass bodies that do move: restarts

@@ -1222,7 +1222,8 @@ def _world_from_oracle(pa, torch, bodies, B, keys):
     return pa.World(out, B, "cuda", torch.tensor(u32_to_i32(keys), device="cuda"))
 
 
-@pytest.mark.parametrize("scene", ["aabb_poly", "aabb_circle_poly", "straddle", "straddle_ew1", "octagons9"])
+@pytest.mark.parametrize("scene", ["aabb_poly", "aabb_circle_poly", "straddle", "straddle_ew1", "octagons9",
+                                   "octagons12", "octagons15", "polygon20"])
 def test_generic_polygon_scenes_vs_cport(torch_cuda, cport_lib, scene):
     """The generic step programs on the GPU (cxk::launch_fnset: polygon-only
     GJK/EPA for the straddling-part scene, AABB x polygon, circle x polygon)
@@ -1230,13 +1231,17 @@ def test_generic_polygon_scenes_vs_cport(torch_cuda, cport_lib, scene):
     contact choice.  straddle_ew1: one env per wave, where the static floor
     straddles phase T's first two vertex-item chunks.  octagons9: nine
     octagon bodies, whose tile fits the LDS at one env per wave only -- the
-    tiling the library picks at scene creation."""
+    tiling the library picks at scene creation.  octagons12 / octagons15 /
+    polygon20 (20 polygon parts over 5 bodies): tiles that fit only in
+    workgroups of fewer than four waves (cotix_scene_waves_per_group)."""
     torch = torch_cuda
     import parallax_amd as pa
     cport, lib = cport_lib
     import scene_cases
-    if scene == "octagons9":
-        bodies = scene_cases.octagon_row(9)
+    if scene.startswith("octagons"):
+        bodies = scene_cases.octagon_row(int(scene[8:]))
+    elif scene == "polygon20":
+        bodies = scene_cases.polygon20()
     else:
         bodies = scene_cases.straddle_scene(4.0) if scene.startswith("straddle") else scene_cases.mixed_scene(
             scene == "aabb_circle_poly")
@@ -1246,7 +1251,9 @@ def test_generic_polygon_scenes_vs_cport(torch_cuda, cport_lib, scene):
     if scene == "straddle_ew1":
         w.set_variant(1)
     if scene == "octagons9":
-        assert w.scene.variant()["envs_per_wave"] == 1
+        assert w.scene.variant()["envs_per_wave"] == 1 and w.scene.waves_per_group() == 4
+    if scene in ("octagons12", "octagons15", "polygon20"):
+        assert w.scene.variant()["envs_per_wave"] == 1 and w.scene.waves_per_group() in (1, 2)
     base = np.array([b.dyn() for b in bodies], np.float32)
     dyn = np.ascontiguousarray(np.repeat(base[:, :, None], B, axis=2))
     dyn[0, 0, :] += np.linspace(-0.6, 0.6, B).astype(np.float32)

@@ -68,3 +68,44 @@ def test_vmapped_lunar_lander_pytree_steps_like_lunar_lander(torch_cuda):
         ll.world.step(64, 1e-2, ll.stages)
     torch.cuda.synchronize()
     assert _same(torch, w.dyn, ll.world.dyn) and _same(torch, w.keys, ll.world.keys)
+
+
+def test_vmapped_per_env_body_params_vs_cport(torch_cuda):
+    """A vmapped LunarLander whose lander / leg mass, inertia, elasticity and
+    friction vary per env (domain randomization over the parameter leaves,
+    cotix/_bodies.py:140-154; tests/penv_cases.py): World.from_bodies gives a
+    per-env-parameter scene (COTIX_SCENE_PER_ENV_BODY_PARAMS) that steps bit
+    for bit like the C port fed the same parameters -- state, keys, error
+    bits and every contact choice -- over 3 launches of 40 fused steps."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import penv_cases as PC
+    from cotix_oracle import cport
+    clib = cport.load()
+    B = 512
+    obs = PC.lunar_penv_bodies(B, seed=3)
+    w = pa.World.from_bodies(RS.stack([RS.from_oracle(ob) for ob in obs]), device="cuda")
+    assert w.scene.per_env_params and w.scene.variant()["specialization"] == "generic"
+    dyn, keys = PC.state(obs)
+    w.dyn.copy_(torch.tensor(dyn, device="cuda"))
+    w.keys.copy_(torch.tensor(keys.view(np.int32), device="cuda"))
+    sc = cport.Scene(clib, obs[0])
+    G = sc.set_per_env_params(True)
+    geom = PC.rows(lambda ob: cport.Scene(clib, ob).geom, obs)
+    assert np.array_equal(w.geom.cpu().numpy().view(np.uint32), geom.view(np.uint32)) and G == geom.shape[1]
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32)]
+    stages = pa._ffi.STAGES_LUNAR
+    res = 0
+    for _ in range(3):
+        tr = {}
+        w.step(40, 1e-2, stages | pa._ffi.STAGE_BROADPHASE, trace=tr)
+        wch, wcl = sc.step_ex(*want, 40, stages, geom=geom, trace=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(tr["chosen"].cpu().numpy(), wch) and np.array_equal(tr["cells"].cpu().numpy(), wcl)
+        res += int((wch != np.arange(4)[None, :, None]).sum())
+    got = w.dyn.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(want[0]))
+    assert np.array_equal(np.nan_to_num(got).view(np.uint32), np.nan_to_num(want[0]).view(np.uint32))
+    assert np.array_equal(w.keys.cpu().numpy().view(np.uint32), want[1])
+    assert np.array_equal(w.err.cpu().numpy().view(np.uint32), want[2])
+    assert res > B  # the parameters are exercised: resolutions in every launch

@@ -547,6 +547,15 @@ CXK_WAVE_OP void lockstep() {
   ::cxk_simt::lockstep();
 #endif
 }
+// a value whose producing global read must complete here (an empty asm that
+// reads and writes it: the wait lands at this point, not at a later join)
+CXK_WAVE_OP void settle(float& x) {
+#if defined(__HIP__)
+  asm volatile("" : "+v"(x));
+#else
+  (void)x;
+#endif
+}
 // 64-bit ballot of p over the wave's active lanes
 CXK_WAVE_OP uint64_t ballot(bool p) {
 #if defined(__HIP__)
@@ -950,6 +959,11 @@ CX_DEV void euler_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e
       const float* ac = a.action + ((size_t)(a.action_held ? 0 : step) * a.B + env0 + e) * 2;
       ax = ac[0];
       ay = ac[1];
+      // the read completes on this path: merged with the register path, the
+      // compiler waited at the join (s_waitcnt vmcnt(0)) on BOTH paths -- for
+      // every store in flight too (the rollout's saves: ~1.2 k cycles a step)
+      settle(ax);
+      settle(ay);
     }
     t.f(o + 2, e) = t.f(o + 2, e) + ax;
     t.f(o + 3, e) = t.f(o + 3, e) + ay;
@@ -1812,7 +1826,8 @@ CX_DEV cx::v2 minkowski(const PairSide& p, const PairSide&, cx::v2 d) {
 // written read as the zero edge (no zero-fill of the column).  The same
 // expressions on the same operands as cx::epa: bit-identical.
 template <int NE>
-CX_DEV cx::v2 epa_pair(const PairSide& ps, int h, const cx::v2* simplex, int iters, float* col) {
+CX_DEV cx::v2 epa_pair(const PairSide& ps, int h, const cx::v2* simplex, int iters, float* col,
+                       cx::v2* edge = nullptr) {
   using namespace cx;
   constexpr int NH = (NE + 1) / 2;
   EdgeCol es{col, WAVE};
@@ -1904,10 +1919,14 @@ CX_DEV cx::v2 epa_pair(const PairSide& ps, int h, const cx::v2* simplex, int ite
     best0 = g0(bei);
     best1 = g1(bei);
   }
+  if (edge != nullptr) {  // EPA's final edge (the rollout's tape, as cx::epa's)
+    edge[0] = best0;
+    edge[1] = best1;
+  }
   return closest_on_edge_to_origin(best0, best1);
 }
 CX_DEV bool gjk_epa_pair(const cx::Shape& mine, int h, int na, int nb, const cx::NarrowParams& np, bool need_pen,
-                         cx::v2* pen, float* col) {
+                         cx::v2* pen, float* col, cx::v2* edge = nullptr) {
   using namespace cx;
   const PairSide ps{mine, h};
   v2 simplex[3];
@@ -1915,7 +1934,8 @@ CX_DEV bool gjk_epa_pair(const cx::Shape& mine, int h, int na, int nb, const cx:
   if (!gjk(ps, ps, np.d0, simplex, np.gjk_steps)) return false;
   if (!need_pen) return true;
   const int it0 = na + nb + 1, iters = it0 < np.epa_cap ? it0 : np.epa_cap;  // min(48, ...), cotix/_contacts.py:295
-  *pen = iters + 3 <= 14 ? epa_pair<14>(ps, h, simplex, iters, col) : epa_pair<20>(ps, h, simplex, iters, col);
+  *pen = iters + 3 <= 14 ? epa_pair<14>(ps, h, simplex, iters, col, edge)
+                         : epa_pair<20>(ps, h, simplex, iters, col, edge);
   return true;
 }
 // the B list items of the polygon-only program run on lane pairs
@@ -1948,9 +1968,17 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
   const bool self = ((d0w >> 27) & 1u) != 0u;
   float* col = reinterpret_cast<float*>(t.ws + c.W.epa + lane);
   Contact ct;
+  v2 edge[2];
   const bool hit = CXK_SKIP(a, 64) ? (ct.pen = v2{0.0f, 0.0f}, true)  // timing only: no GJK / EPA
-                                     : gjk_epa_pair(S, h, na, nb, narrow_of(sc), !self, &ct.pen, col);
+                                     : gjk_epa_pair(S, h, na, nb, narrow_of(sc), !self, &ct.pen, col,
+                                                    TAPE ? edge : nullptr);
   if (h != 0) return;
+  if (TAPE && a.tape != nullptr && hit && !self) {  // EPA's final edge to the tape (b_item's words)
+    const int o = 5 * c.nb + 4 * ci;
+    const float ev[4] = {edge[0].x, edge[0].y, edge[1].x, edge[1].y};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a.tape[((size_t)step * a.tw + o + q) * a.B + g] = __float_as_uint(ev[q]);
+  }
   ct.cp = v2{qnan(), qnan()};
   if (hit && self && self_cp_finite(S)) ct.cp = v2{0.0f, 0.0f};  // S is A on lane 0 (see b_item)
   else if (hit) t.ws[c.W.cf_flag + w] = 1u;
@@ -1967,9 +1995,9 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
 // terrain -- and cost a little on GJK-only lists, e.g. the self pairs in flight)
 template <int EW, int FNSET, bool TAPE = false>
 CX_DEV void ph_BP2(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int r, bool pairs, int step = 0) {
-  if (b_pairs<FNSET>() && pairs && !TAPE) {  // (the tape's edge words come from the one-lane form)
+  if (b_pairs<FNSET>() && pairs) {  // (the rollout's tape: EPA's edge from lane 0 of the pair)
     const int k = r * (WAVE / 2) + (lane >> 1);
-    if (k < (int)t.ws[c.W.bl_n]) b_item_pair<EW, FNSET>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k]);
+    if (k < (int)t.ws[c.W.bl_n]) b_item_pair<EW, FNSET, TAPE>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k], step);
   } else {
     const int k = r * WAVE + lane;
     if (k < (int)t.ws[c.W.bl_n]) b_item<EW, FNSET, TAPE>(a, c, t, env0, lane, (int)t.ws[c.W.bl_list + k], step);
@@ -3783,7 +3811,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
     run(PH_BP0, [&](int l) { ph_BP0<EW>(a, c, t, env0, l); });
     const int n = (int)t.ws[c.W.bl_n];  // uniform: read after the phase barrier
     CXK_STAT(b_items, 0);
-    const bool pairs = b_pairs<FNSET>() && !TAPE && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the barrier
+    const bool pairs = b_pairs<FNSET>() && t.ws[c.W.bl_mode] != 0u;  // uniform: read after the barrier
     const int per_round = pairs ? WAVE / 2 : WAVE;
     for (int r = 0; r * per_round < n; ++r)
       run(PH_B, [&](int l) { ph_BP2<EW, FNSET, TAPE>(a, c, t, env0, l, r, pairs, step); });

@@ -18,3 +18,13 @@ for k in ('forward','backward'):
     p=d[k]; print('$sc', k, round(p['cycles_per_wave_step_total']), {a:round(b['cycles_per_wave_step']) for a,b in p['phases'].items() if b['cycles_per_wave_step']>40})"
 done
 fi
+if [ -n "$STEPPHASES" ]; then
+L=parallax_amd/_lib/libcotix_amd_prof_tool.so
+for spec in $STEPPHASES; do  # name:args
+  n=${spec%%:*}; args=${spec#*:}; args=${args//,/ }
+  timeout -k 10 200 python tools/phase_prof.py --lib $L $args > $O/phase_$n.json 2> $O/phase_$n.err || { tail -5 $O/phase_$n.err; exit 5; }
+  python -c "
+import json; p=json.load(open('$O/phase_$n.json'))
+print('$n', round(p['cycles_per_wave_step_total']), {a:round(b['cycles_per_wave_step']) for a,b in p['phases'].items() if b['cycles_per_wave_step']>40})"
+done
+fi

@@ -2449,8 +2449,15 @@ CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
 
 // resolution i's velocity-independent operands (phase E0 of the design:
 // computed by the phase-D item (body i, env e) right after its choice j)
+// the rollout forward's per-env staging of a step's tape words, in the
+// layout of the tape (tape_words): 5 words per body [partner | contact id,
+// pen, cp], directly followed by the resolution records (REC_W per body,
+// L.rec) -- the last 5 nb words of the adjoint region, which only the
+// backward uses
+CX_HD int tape_stage(const Ctx& c) { return c.L.rec - 5 * c.nb; }
 template <int EW, bool RCP>
-CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, uint32_t* tp = nullptr, int B = 0) {
+CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, bool stage = false, uint32_t* tp = nullptr,
+                    int B = 0) {
   // branch-free: the operands are computed from clamped indices for every
   // item and the partner is set only for a real resolution (the inactive
   // items' operands are never read: E1 skips RP_NONE)
@@ -2488,8 +2495,19 @@ CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, uint
   const bool res = pair && !vnan(cp);
   if (res) CXK_STAT(resolutions, 1);
   t.w(ro + RP_J, e) = res ? (uint32_t)j : RP_NONE;
-  if (tp != nullptr) {  // the rollout forward's tape words of body i (tape_save's, from the operands in hand)
-    tp[0] = res ? (uint32_t)j | ((uint32_t)cid << 8) : RP_NONE;
+  // the rollout forward's tape words of body i, from the operands in hand:
+  // staged next to the records (analytic scenes, tape_stage), or stored
+  // (polygon scenes: their broadphase pseudo-angles overlay that region)
+  const uint32_t w0 = res ? (uint32_t)j | ((uint32_t)cid << 8) : RP_NONE;
+  if (stage) {
+    const int o = tape_stage(c) + 5 * i;
+    t.w(o, e) = w0;
+    t.f(o + 1, e) = t.f(co, e);
+    t.f(o + 2, e) = t.f(co + 1, e);
+    t.f(o + 3, e) = cp.x;
+    t.f(o + 4, e) = cp.y;
+  } else if (tp != nullptr) {
+    tp[0] = w0;
     if (res) {
       tp[(size_t)B] = __builtin_bit_cast(uint32_t, t.f(co, e));
       tp[2 * (size_t)B] = __builtin_bit_cast(uint32_t, t.f(co + 1, e));
@@ -2502,7 +2520,8 @@ CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, uint
 // one (body i, env) item of phase D; NB > 0: the body count at compile time
 // (unrolled loads and selects), NB == 0: any count up to MAXB
 template <int EW, bool PRE, int NB, bool RCP>
-CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, uint32_t* tp = nullptr, int B = 0) {
+CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, bool stage = false, uint32_t* tp = nullptr,
+                   int B = 0) {
   using namespace cx;
   constexpr int MB = NB > 0 ? NB : MAXB;
   const int nb = NB > 0 ? NB : c.nb, nt = c.nt;
@@ -2553,26 +2572,28 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, uint32_t* t
 #pragma unroll
   for (int j = 0; j < MB; ++j) cid = j == ch ? mm[j] : cid;
   cid = cid < 0 ? -1 : (cid >> 18) & 511;
-  e0_item<EW, RCP>(c, t, e, i, ch, cid, tp, B);
+  e0_item<EW, RCP>(c, t, e, i, ch, cid, stage, tp, B);
 }
-// TAPE: the rollout forward writes each body's tape words (partner, contact
-// id, contact) here, from the operands phase D has in registers, instead of
-// re-reading them from the tile in the next step's save phase (tape_save)
+// TAPE: the rollout forward stages each body's tape words (partner, contact
+// id, contact) here, from the operands phase D has in hand, next to phase
+// E1's resolution records (tape_stage), so that the save phase copies them
+// out as whole rows instead of chasing partner -> cell -> contact
 template <int EW, bool PRE = false, bool TAPE = false>
 CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int slot = 0, int step = 0) {
   const int nb = c.nb;
   for (int w = lane; w < nb * EW; w += WAVE) {
     const int e = w % EW, i = w / EW;
     if (env0 + e >= a.B) continue;
-    uint32_t* tp = TAPE && a.tape != nullptr ? a.tape + ((size_t)step * a.tw + 5 * i) * a.B + env0 + e : nullptr;
+    const bool stage = TAPE && a.tape != nullptr && tape_rec(c.sh);
+    uint32_t* tp = TAPE && a.tape != nullptr && !stage ? a.tape + ((size_t)step * a.tw + 5 * i) * a.B + env0 + e : nullptr;
     if (c.sh.rcp_all) {
-      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, slot, tp, a.B);
-      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, slot, tp, a.B);
-      else d_item<EW, PRE, 0, true>(c, t, e, i, slot, tp, a.B);
+      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, slot, stage, tp, a.B);
+      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, slot, stage, tp, a.B);
+      else d_item<EW, PRE, 0, true>(c, t, e, i, slot, stage, tp, a.B);
     } else {
-      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, slot, tp, a.B);
-      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, slot, tp, a.B);
-      else d_item<EW, PRE, 0, false>(c, t, e, i, slot, tp, a.B);
+      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, slot, stage, tp, a.B);
+      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, slot, stage, tp, a.B);
+      else d_item<EW, PRE, 0, false>(c, t, e, i, slot, stage, tp, a.B);
     }
   }
 }
@@ -2805,6 +2826,29 @@ CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const Ret
   t.f(c.L.ret, e) = acc;
 }
 
+// tile rows [o, o + n) of the wave's envs (row r: EW words, env fastest) to
+// the global rows dst + r * B (env fastest, B per row): with 4 envs per wave,
+// a whole wave and 16-byte aligned rows, one 16-byte store per row (a lane
+// each: the rollout's saves were one 4-byte store per word and env); else one
+// word per (row, env) lane
+struct alignas(16) U4 {
+  uint32_t v[4];
+};
+template <int EW>
+CX_DEV void rows_out(Tile<EW> t, int o, int n, uint32_t* dst, int B, int env0, int lane) {
+  if (EW == 4 && (B & 3) == 0 && env0 + 4 <= B) {
+    for (int r = lane; r < n; r += WAVE) {
+      const U4 w = U4{{t.w(o + r, 0), t.w(o + r, 1), t.w(o + r, 2), t.w(o + r, 3)}};
+      *reinterpret_cast<U4*>(dst + (size_t)r * B + env0) = w;
+    }
+  } else {
+    for (int w = lane; w < n * EW; w += WAVE) {
+      const int e = w % EW, r = w / EW;
+      if (env0 + e < B) dst[(size_t)r * B + env0 + e] = t.w(o + r, e);
+    }
+  }
+}
+
 // REC (backward re-play only): record, per resolution, whether the impulses
 // were applied and the pre-resolution velocities of the two bodies.
 // RET (rollout forward): the return accumulation after the step, on the
@@ -2815,18 +2859,9 @@ CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const Ret
 // the next step's save phase (ph_save) or, for the last step, after the loop
 template <int EW, bool TR>
 CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
-  const Lay& L = c.L;
-  const int nb = c.nb;
-  if (!(TR && tape_rec(c.sh))) return;  // (the resolution words: phase D, e0_item)
-  for (int w = lane; w < nb * EW; w += WAVE) {
-    const int e = w % EW, i = w / EW, g = env0 + e;
-    if (g >= a.B) continue;
-    {  // phase E1's record of the resolution (ph_E TREC)
-      uint32_t* orc = a.tape + ((size_t)step * a.tw + 5 * nb + REC_W * i) * a.B + g;
-#pragma unroll
-      for (int q = 0; q < REC_W; ++q) orc[(size_t)q * a.B] = t.w(L.rec + REC_W * i + q, e);
-    }
-  }
+  // (polygon scenes: phase D stores their resolution words, phase B EPA's edges)
+  if (TR && tape_rec(c.sh)) rows_out<EW>(t, tape_stage(c), (5 + REC_W) * c.nb, a.tape + (size_t)step * a.tw * a.B, a.B,
+                                         env0, lane);
 }
 
 // TREC: the rollout forward with a tape records the resolutions (as REC) for
@@ -3136,21 +3171,8 @@ CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
   if (a.tape != nullptr && step > 0 && (a.stages & COTIX_STAGE_COLLIDER) && !CXK_SKIP(a, 128))
     tape_save<EW, TR>(a, c, t, env0, lane, step - 1);
   if (CXK_SKIP(a, 256)) return;
-  const size_t base = (size_t)step * c.nb * 6 * a.B;
-  const int nd = c.nb * 6 * EW;
-  float v[RQ];  // every LDS read first, then the stores: one LDS round trip, not one per 64 words
-#pragma unroll
-  for (int q = 0; q < RQ; ++q) {
-    if (q * WAVE >= nd) break;  // uniform
-    const int w = q * WAVE + lane;
-    v[q] = t.f(c.L.dyn + (w < nd ? w / EW : 0), w % EW);
-  }
-#pragma unroll
-  for (int q = 0; q < RQ; ++q) {
-    if (q * WAVE >= nd) break;  // uniform
-    const int w = q * WAVE + lane, e = w % EW, off = w / EW, g = env0 + e;
-    if (w < nd && g < a.B) a.save_dyn[base + (size_t)off * a.B + g] = v[q];
-  }
+  rows_out<EW>(t, c.L.dyn, c.nb * 6, reinterpret_cast<uint32_t*>(a.save_dyn) + (size_t)step * c.nb * 6 * a.B, a.B,
+               env0, lane);
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g < a.B) {

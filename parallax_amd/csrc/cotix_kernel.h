@@ -279,6 +279,10 @@ CX_HD bool tape_rec(const SceneHdr& sh) { return sh.poly == 0; }
 // the backward's tape words in registers (tape_fetch): per (body, env) item
 // its resolution word + contact, and the recorded EPA edge
 constexpr int TQ = (MAXB * 8 + WAVE - 1) / WAVE;  // items per lane: nb * EW over 64 lanes (EW <= 8)
+// 16 bytes: 4 envs' words of one row (rows_out, restore_rows_fetch)
+struct alignas(16) U4 {
+  uint32_t v[4];
+};
 struct TapeRegs {
   uint32_t d[TQ][5];
   uint32_t x[TQ][REC_W];  // polygon scenes: the EPA edge (4 float words); analytic: the resolution's record
@@ -2598,6 +2602,56 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
   }
 }
 
+// The tape backward's restore of an analytic scene as 16-byte rows (4 envs per
+// wave, whole waves): row r < 6 nb is state word r (save_dyn), row 6 nb + k
+// tape word k (5 per body, then the records), one 16-byte read per row and
+// lane -- at most 2 rows a lane, 8 registers, so the reads can run two steps
+// ahead (restore_rows_fetch into one of two register sets); the tape rows land
+// in the key-window words, which the analytic backward does not use
+// (rows_tape), and phase D reads them there (ph_D_tape STAGED)
+CX_HD int rows_tape(const Ctx& c) { return c.L.kw; }
+template <int EW>
+CX_DEV bool rows_restore(const KArgs& a, const Ctx& c) {
+  return EW == 4 && (a.B & 3) == 0 && tape_rec(c.sh) && (a.stages & COTIX_STAGE_COLLIDER) && 18 * c.nb <= 2 * WAVE &&
+         (5 + REC_W) * c.nb <= KWIN * c.L.kww;
+}
+struct RowRegs {
+  U4 d[2];
+  uint32_t k0 = 0u, k1 = 0u;
+};
+template <int EW>
+CX_DEV void restore_rows_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step, RowRegs& r) {
+  const int nd = 6 * c.nb, nr = nd + (5 + REC_W) * c.nb;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int row = q * WAVE + lane;
+    const uint32_t* src = row < nd ? reinterpret_cast<const uint32_t*>(a.save_dyn) + ((size_t)step * nd + row) * a.B
+                                   : a.tape + ((size_t)step * a.tw + (row - nd)) * a.B;
+    if (row < nr) r.d[q] = *reinterpret_cast<const U4*>(src + env0);
+  }
+  const int g = env0 + lane;
+  const bool le = lane < EW && g < a.B;
+  r.k0 = le ? a.save_keys[2 * ((size_t)step * a.B + g)] : 0u;
+  r.k1 = le ? a.save_keys[2 * ((size_t)step * a.B + g) + 1] : 0u;
+}
+template <int EW>
+CX_DEV void restore_rows_apply(const Ctx& c, Tile<EW> t, int lane, const RowRegs& r) {
+  const int nd = 6 * c.nb, nr = nd + (5 + REC_W) * c.nb;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int row = q * WAVE + lane;
+    const int o = row < nd ? c.L.dyn + row : rows_tape(c) + (row - nd);
+    if (row < nr)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t.w(o, e) = r.d[q].v[e];
+  }
+  if (lane < EW) {
+    t.w(c.L.key, lane) = r.k0;
+    t.w(c.L.key + 1, lane) = r.k1;
+    t.w(c.L.err, lane) = 0u;
+  }
+}
+
 // phase D of the backward with a tape (MODE 4): the forward's resolution of
 // body i -- partner, cell, contact, and for a GJK/EPA contact EPA's final
 // edge (into ge_edge's words, read by phase GE) -- from the tape registers,
@@ -2607,7 +2661,9 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
 // one field they read)
 CX_HD bool ge_edges_fit(const Ctx& c) { return 28 * c.nb <= KWIN * c.L.kww; }
 CX_DEV int ge_edge_word(const Ctx& c, int i) { return c.L.kw + 24 * c.nb + 4 * i; }
-template <int EW, bool TR>
+// STAGED: the step's tape words are rows of the tile (restore_rows, analytic
+// scenes) instead of this lane's registers
+template <int EW, bool TR, bool STAGED = false>
 CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, const TapeRegs& r) {
   const Lay& L = c.L;
   const int nb = c.nb, ni = nb * EW;
@@ -2617,21 +2673,23 @@ CX_DEV void ph_D_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int la
     if (q * WAVE >= ni) break;  // uniform
     const int w = q * WAVE + lane, e = w % EW, i = w / EW;
     if (w >= ni || env0 + e >= a.B) continue;
-    const uint32_t dec = r.d[q][0];
+    auto dw = [&](int k) { return STAGED ? t.w(rows_tape(c) + 5 * (i < nb ? i : 0) + k, e) : r.d[q][k]; };
+    auto xw = [&](int k) { return STAGED ? t.w(rows_tape(c) + 5 * nb + REC_W * (i < nb ? i : 0) + k, e) : r.x[q][k]; };
+    const uint32_t dec = dw(0);
     const bool res = dec != RP_NONE;
     const int j = res ? (int)(dec & 255u) : i, cid = res ? (int)((dec >> 8) & 511u) : -1;
     t.w(L.ch + i, e) = (uint32_t)j;
     if (TR && tape_rec(c.sh)) {  // the forward's record of the resolution (phase E does not run)
-      t.w(L.rec + REC_W * i, e) = res ? r.x[q][0] : 0u;
+      t.w(L.rec + REC_W * i, e) = res ? xw(0) : 0u;
       if (res)
 #pragma unroll
-        for (int k = 1; k < REC_W; ++k) t.w(L.rec + REC_W * i + k, e) = r.x[q][k];
+        for (int k = 1; k < REC_W; ++k) t.w(L.rec + REC_W * i + k, e) = xw(k);
     }
     if (res) {
       t.w(L.m + i * nb + j, e) = (uint32_t)cid << 18;
       const int co = L.con + 4 * cid;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) t.w(co + k, e) = r.d[q][k + 1];
+      for (int k = 0; k < 4; ++k) t.w(co + k, e) = dw(k + 1);
       if (edges) {
         const int eo = ge_edge_word(c, i);
 #pragma unroll
@@ -2831,9 +2889,6 @@ CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const Ret
 // a whole wave and 16-byte aligned rows, one 16-byte store per row (a lane
 // each: the rollout's saves were one 4-byte store per word and env); else one
 // word per (row, env) lane
-struct alignas(16) U4 {
-  uint32_t v[4];
-};
 template <int EW>
 CX_DEV void rows_out(Tile<EW> t, int o, int n, uint32_t* dst, int B, int env0, int lane) {
   if (EW == 4 && (B & 3) == 0 && env0 + 4 <= B) {
@@ -4042,11 +4097,71 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
   const bool col = (a.stages & COTIX_STAGE_COLLIDER) != 0;
   const bool edges = FNSET != FNS_ANALYTIC && c.sh.poly && ge_fits(c) && ge_edges_fit(c);
   constexpr bool TR = FNSET == FNS_ANALYTIC;  // the tape's resolution records (tape_rec)
-  RestoreRegs rr;
-  GradOut go;       // the previous (later) step's d ret / d action, stored by the restore phase
-  TapeRegs tn, tr;  // the next (earlier) step's tape words, the current step's
+  GradOut go;  // the previous (later) step's d ret / d action, stored by the restore phase
   const bool apf = act_prefetch<EW>(a, c);
-  ActRegs an, ac;  // the actions, one step ahead as the state
+  ActRegs ac;
+  // the step after its restore: Euler, world parts, the tape's resolutions,
+  // the reverse chain (the same for both restore forms)
+  auto reverse_step = [&](int step, auto dphase) {
+    run(PH_A, [&](int l) {  // Euler (+ gravity, + action); no key split, no collider scratch
+      if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
+        for (int w = l; w < c.nb * EW; w += WAVE) {
+          const int e = w % EW, b = w / EW;
+          if (env0 + e < a.B) euler_item<EW>(a, c, t, env0, e, b, step, apf, ac);
+        }
+    });
+    if (col) {
+      transform_phases<EW, FNSET>(a, c, t, env0, run);
+      run(PH_D, dphase);
+    }
+    // phase E re-runs the sequential pass for its records -- unless the tape has them
+    if (!(TR && col && tape_rec(c.sh))) run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
+    if (FNSET != FNS_ANALYTIC && col && ge_fits(c)) {
+      if (edges)
+        run(PH_GE, [&](int l) { ph_GE<EW, true>(a, c, t, env0, l); });
+      else
+        run(PH_GE, [&](int l) { ph_GE<EW>(a, c, t, env0, l); });
+    }
+    run(PH_G, [&](int l) { ph_G<EW, FNSET>(a, c, t, env0, l, step, &go); });
+  };
+  if (TR && rows_restore<EW>(a, c)) {  // rows, two steps ahead (two register sets: the loop unrolled by two)
+    struct Pre {
+      RowRegs rw;
+      ActRegs an;
+    };
+    Pre p0, p1;
+    const TapeRegs none{};
+    auto prefetch = [&](int l, int s, Pre& p) {
+      restore_rows_fetch<EW>(a, c, env0, l, s, p.rw);
+      if (apf) act_fetch<EW>(a, c, env0, l, s, p.an);
+    };
+    if (a.n_steps > 0)
+      run(PH_RESTORE, [&](int l) {
+        prefetch(l, a.n_steps - 1, p0);
+        if (a.n_steps > 1) prefetch(l, a.n_steps - 2, p1);
+      });
+    auto one = [&](int step, Pre& cur) {
+      run(PH_RESTORE, [&](int l) {
+        restore_rows_apply<EW>(c, t, l, cur.rw);
+        ac = cur.an;
+        if (a.grad_action != nullptr) grad_action_flush(a, env0, l, EW, go);  // (stores, then the prefetch reads)
+        if (step > 1) prefetch(l, step - 2, cur);
+      });
+      reverse_step(step, [&](int l) { ph_D_tape<EW, TR, true>(a, c, t, env0, l, none); });
+    };
+    for (int step = a.n_steps - 1; step >= 0; step -= 2) {
+      one(step, p0);
+      if (step >= 1) one(step - 1, p1);
+    }
+    run(PH_ADJ, [&](int l) {
+      if (a.grad_action != nullptr) grad_action_flush(a, env0, l, EW, go);  // step 0's
+      ph_adj_store<EW>(a, c, t, env0, l);
+    });
+    return;
+  }
+  RestoreRegs rr;
+  TapeRegs tn, tr;  // the next (earlier) step's tape words, the current step's
+  ActRegs an;       // the actions, one step ahead as the state
   if (a.n_steps > 0)
     run(PH_RESTORE, [&](int l) {
       restore_fetch<EW>(a, c, env0, l, a.n_steps - 1, rr);
@@ -4068,26 +4183,7 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
         if (apf && !a.action_held) act_fetch<EW>(a, c, env0, l, step - 1, an);
       }
     });
-    run(PH_A, [&](int l) {  // Euler (+ gravity, + action); no key split, no collider scratch
-      if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
-        for (int w = l; w < c.nb * EW; w += WAVE) {
-          const int e = w % EW, b = w / EW;
-          if (env0 + e < a.B) euler_item<EW>(a, c, t, env0, e, b, step, apf, ac);
-        }
-    });
-    if (col) {
-      transform_phases<EW, FNSET>(a, c, t, env0, run);
-      run(PH_D, [&](int l) { ph_D_tape<EW, TR>(a, c, t, env0, l, tr); });
-    }
-    // phase E re-runs the sequential pass for its records -- unless the tape has them
-    if (!(TR && col && tape_rec(c.sh))) run(PH_E, [&](int l) { ph_E<EW, true>(a, c, t, env0, l, c.L.sk0); });
-    if (FNSET != FNS_ANALYTIC && col && ge_fits(c)) {
-      if (edges)
-        run(PH_GE, [&](int l) { ph_GE<EW, true>(a, c, t, env0, l); });
-      else
-        run(PH_GE, [&](int l) { ph_GE<EW>(a, c, t, env0, l); });
-    }
-    run(PH_G, [&](int l) { ph_G<EW, FNSET>(a, c, t, env0, l, step, &go); });
+    reverse_step(step, [&](int l) { ph_D_tape<EW, TR>(a, c, t, env0, l, tr); });
   }
   run(PH_ADJ, [&](int l) {
     if (a.grad_action != nullptr) grad_action_flush(a, env0, l, EW, go);  // step 0's

@@ -70,10 +70,11 @@ def test_oracle_grad_vs_finite_differences():
             assert abs(fd - ga[t, c]) <= 2e-3 * (1 + abs(fd)), (e, t, c, fd, ga[t, c])
 
 
-@pytest.mark.parametrize("E,T", [(1, 40), (4, 32)])  # (T 32: the GPU test's horizon)
-def test_emu_rollout_box_world(emu_lib, E, T):
+# (T 32: the GPU test's horizon; B 8 at 4 envs per wave: the backward's
+# 16-byte row restore, two steps ahead -- B 6 its one-word form)
+@pytest.mark.parametrize("E,T,B", [(1, 40, 6), (4, 32, 6), (4, 32, 8)])
+def test_emu_rollout_box_world(emu_lib, E, T, B):
     emu, lib = emu_lib
-    B = 6
     case = GC.box_case(B, T, seed=1)
     ret, ga, gd, dyn = _emu_run(emu, lib, case, E)
     orc = GC.oracle(case)

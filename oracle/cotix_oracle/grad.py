@@ -339,6 +339,125 @@ def _convex_contact(fname, A, B, d0):
     return pen, _contact_from_edges(A, B)
 
 
+# ---- circle x polygon (cotix/_contacts.py:157-202) ----
+# A circle's support is a function of the search direction (Circle.get_support,
+# cotix/_convex_shapes.py:22-26: d / |d| * r + c), so jax.grad goes through
+# every GJK and EPA step that built the final edge.  Restated in torch with the
+# reference's control flow: every decision (GJK's branches, the polygon
+# support's argmax, EPA's closest edge and stop test, the contact point's edge)
+# is taken by the faithful oracle (geometry.py) on the f32 values of the
+# torch tensors -- the same expressions in the same order, so the values are
+# bit-identical (asserted) -- and the values are torch ops: the derivative is
+# jax.grad's through the executed branches.
+def _f(x):
+    return np.float32(x.item())
+
+
+def _fp(p):
+    return (_f(p[0]), _f(p[1]))
+
+
+def _fnormal(a):  # fast_normal (cotix/_geometry_utils.py:30-34)
+    return (-a[1], a[0])
+
+
+def _circle_polygon_contact(circ, P, d0):
+    r, c = circ
+    poly = P.np
+
+    def mink(d):  # minkowski_diff(circle.get_support, polygon.get_support, d)
+        n = _norm(d)
+        sa = ((d[0] / n) * r + c[0], (d[1] / n) * r + c[1])
+        dn = (-d[0], -d[1])
+        dots = [G.dot(v, _fp(dn)) for v in poly.vertices()]
+        k = G.argmax(dots)
+        sb = P.verts()[k]
+        return (sa[0] - sb[0], sa[1] - sb[1])
+
+    def dotf(a, b):
+        return G.dot(_fp(a), _fp(b))
+
+    # GJK, _get_collision_simplex (cotix/_collisions.py:20-112)
+    s0 = mink((_t(d0[0]), _t(d0[1])))
+    s1 = mink((-s0[0], -s0[1]))
+    direction = _fnormal(_sub(s1, s0))
+    if dotf(direction, (-s1[0], -s1[1])) > 0:
+        s0, s1 = s1, s0
+    else:
+        direction = (-direction[0], -direction[1])
+    s2 = mink(direction)
+    for _ in range(_params.current().gjk_max_steps):
+        c1 = dotf(s2, direction) <= 0
+        c2 = dotf(_fnormal(_sub(s2, s0)), (-s2[0], -s2[1])) < 0
+        c3 = dotf(_fnormal(_sub(s1, s2)), (-s2[0], -s2[1])) < 0
+        if c1 or (c2 and c3):
+            break
+        cc = s2
+        acn, cbn = _fnormal(_sub(cc, s0)), _fnormal(_sub(s1, cc))
+        if dotf(acn, (-cc[0], -cc[1])) >= 0:
+            s1, direction = cc, acn
+        else:
+            s0, direction = cc, cbn
+        s2 = mink(direction)
+    simplex = [s0, s1, s2]
+    sn = [_fp(p) for p in simplex]
+    assert G.is_point_in_triangle((G.ZERO, G.ZERO), *sn), "circle x polygon: not a contact"
+    # EPA, _get_closest_minkowski_diff (cotix/_collisions.py:115-273), 128 iterations (cotix/_contacts.py:162-163)
+    iters = _params.current().epa_circle_iters
+    z = (_t(0.0), _t(0.0))
+    edges = [(z, z)] * (iters + 3)
+    edges[0], edges[1], edges[2] = (s0, s1), (s1, s2), (s2, s0)
+
+    def closest(es):
+        _, k = G._closest_edge([(_fp(a), _fp(b)) for a, b in es])
+        return es[k], k
+
+    best, bei = closest(edges)
+    new_point, prev = s2, edges[0]
+    i = 0
+    for _ in range(iters):
+        bf = (_fp(best[0]), _fp(best[1]))
+        pf = (_fp(prev[0]), _fp(prev[1]))
+        c1 = G.sumsq(G.vsub(bf[0], bf[1])) > np.float32(1e-9)
+        c2 = G.cross(bf[0], bf[1]) >= 0
+        nrm = G.fast_normal(G.vsub(pf[0], pf[1]))
+        nrm = G.vdivs(nrm, G.norm(nrm))
+        dd = G.dot(_fp(new_point), nrm)
+        edist = G.norm(G._closest_point_on_edge_to_point(pf[0], pf[1], (G.ZERO, G.ZERO)))
+        c4 = (dd - edist > np.float32(1e-6)) or (dd <= 0)
+        if not (c4 and not G.vnan(bf[0]) and not G.vnan(bf[1]) and c1 and c2):
+            break
+        n = _fnormal(_sub(best[0], best[1]))
+        nn = _norm(n)
+        n = (n[0] / nn, n[1] / nn)
+        new_point = mink(n)
+        edges[bei] = (best[0], new_point)
+        edges[i + 3] = (new_point, best[1])
+        prev = best
+        best, bei = closest(edges)
+        i += 1
+    best, _ = closest(edges)
+    pen = _closest_to_origin(best[0], best[1])
+    # the contact point (cotix/_contacts.py:168-197): the polygon edge nearest
+    # to the circle's centre, or the centre when it is farther than r
+    disps = []
+    for a, b in P.edges():
+        d = _sub(a, b)
+        length = d[0] * d[0] + d[1] * d[1]
+        pb = _sub(c, b)
+        tt = _clip(_dot(pb, d) / length, _t(0.0), _t(1.0))
+        disps.append(_sub(c, (b[0] + d[0] * tt, b[1] + d[1] * tt)))
+    dists = [G.sumsq(_fp(dv)) for dv in disps]
+    k = G.argmin(dists)
+    rf = _f(r)
+    cp = c if dists[k] > rf * rf else (c[0] + disps[k][0], c[1] + disps[k][1])
+    want = G.circle_vs_polygon(G.Circle(rf, _fp(c)), poly, d0)
+    got = (_fp(pen), _fp(cp))
+    assert all(np.float32(x).view(np.uint32) == np.float32(y).view(np.uint32)
+               for gv, wv in zip(got, want) for x, y in zip(gv, wv)), (got, want)
+    return pen, cp
+
+
 # ---- LunarLander joints (cotix/_lunar_lander.py:145-218) ----
 def _lunar_joints(st):
     f05 = np.float32(0.05)
@@ -406,8 +525,10 @@ def step_torch(S, a, bodies, trace, dt, action_body, gravity=False, d0=None, joi
             pen, cp = CONTACTS[fname](s1, s2)
         elif fname in CONVEX:
             pen, cp = _convex_contact(fname, s1, s2, d0)
+        elif fname == "circle_vs_polygon":
+            pen, cp = _circle_polygon_contact(s1, s2, d0)
         else:
-            raise NotImplementedError("%s is not differentiated (circle support chain through EPA)" % fname)
+            raise NotImplementedError("%s is not differentiated" % fname)
         resolve(st[i], st[j], pen, cp)
     if joints:
         _lunar_joints(st)

@@ -127,6 +127,45 @@ def poly_box_case(B, T, seed=0, octagons=False):
                 tol=POLYGON_TOL, name="octagons" if octagons else "poly_box")
 
 
+def ball_poly_bodies():
+    """Two balls on polygon terrain: a static Polygon4 floor and a static
+    tilted Polygon4 ramp, two dynamic circles resting on them and on each
+    other -- circle x polygon contacts (GJK + EPA with the circle's
+    direction-dependent support, cotix/_contacts.py:157-202) and a circle x
+    circle contact."""
+    from cotix_oracle import geometry as Gm
+    floor = P.Body([Gm.Polygon([(-4.0, -1.0), (4.0, -1.0), (4.0, 0.0), (-4.0, 0.0)], kind="Polygon4")],
+                   mass=np.inf, inertia=np.inf, elasticity=0.3, friction_coefficient=0.4)
+    ramp = P.Body([Gm.Polygon([(1.0, 0.0), (3.0, 0.0), (3.0, 1.0), (1.0, 0.2)], kind="Polygon4")],
+                  mass=np.inf, inertia=np.inf, elasticity=0.3, friction_coefficient=0.4)
+    b1 = P.Body([Gm.Circle(0.3, (0.0, 0.0))], mass=1.0, inertia=0.05, position=(0.0, 0.29),
+                elasticity=0.6, friction_coefficient=0.3)
+    b2 = P.Body([Gm.Circle(0.25, (0.0, 0.0))], mass=0.7, inertia=0.03, position=(0.54, 0.24),
+                elasticity=0.6, friction_coefficient=0.3)
+    return [floor, ramp, b1, b2]
+
+
+def ball_poly_case(B, T, seed=0):
+    make = ball_poly_bodies
+    base = np.array([b.dyn() for b in make()], np.float32)
+    rng = np.random.default_rng(seed)
+    S0 = np.repeat(base[None], B, axis=0)
+    for e in range(B):
+        for b in (2, 3):
+            S0[e, b, 0] += rng.uniform(-0.02, 0.02)
+            S0[e, b, 1] += rng.uniform(-0.02, 0.0)
+            S0[e, b, 2:4] = rng.uniform(-0.4, 0.4, 2)
+            S0[e, b, 5] = rng.uniform(-1.0, 1.0)
+    keys = np.asarray(prng.split(prng.PRNGKey(51 + seed), B), np.uint32)
+    actions = (rng.normal(size=(T, B, 2)) * 0.1).astype(np.float32)
+    w = np.zeros(4 * 6, np.float32)
+    w[2 * 6 + 0] = 1.0   # ball 1 x
+    w[3 * 6 + 1] = 0.5   # ball 2 y
+    w[3 * 6 + 5] = 0.25  # ball 2 angular velocity
+    return dict(make=make, S0=S0.astype(np.float32), keys=keys, actions=actions, w=w, ab=2, step=P.robocup_step,
+                tol=POLYGON_TOL, name="ball_poly")
+
+
 def quad_row_case(B, T, seed=0):
     """Nine Polygon4 bodies (one contact-type key): a static floor quad and a
     row of eight touching boxes on it -- 24 * nb words exceed the key window,

@@ -132,13 +132,20 @@ def _fd_actions(case, e, points, eps=1e-2):
     return out
 
 
-@pytest.mark.parametrize("scene", ["lunar", "poly_box"])
-def test_oracle_grad_polygons_vs_finite_differences(scene):
+@pytest.mark.parametrize("scene", ["lunar", "poly_box", "ball_poly"])
+def test_oracle_grad_polygons_vs_finite_differences(scene, monkeypatch):
     """The checker through GJK/EPA, contact_from_edges and (LunarLander) the
-    joints: torch VJP chain vs central differences of the faithful oracle
-    (cases without discrete flips at eps = 1e-2)."""
-    case = GC.lunar_case(4, 6, seed=0) if scene == "lunar" else GC.poly_box_case(4, 10, seed=0)
+    joints, and (ball_poly) circle x polygon's GJK + EPA with the circle's
+    direction-dependent support: torch VJP chain vs central differences of
+    the faithful oracle (cases without discrete flips at eps = 1e-2)."""
+    case = {"lunar": lambda: GC.lunar_case(4, 6, seed=0), "poly_box": lambda: GC.poly_box_case(4, 10, seed=0),
+            "ball_poly": lambda: GC.ball_poly_case(4, 10, seed=0)}[scene]()
+    from cotix_oracle import grad as OG
+    calls = []
+    real = OG._circle_polygon_contact
+    monkeypatch.setattr(OG, "_circle_polygon_contact", lambda *a: calls.append(1) or real(*a))
     orc = GC.oracle(case)
+    assert (len(calls) > 10) == (scene == "ball_poly")  # circle x polygon resolutions differentiated
     pts = [(0, 0), (0, 1), (2, 0), (5, 1)]
     nontrivial = 0
     for e in range(4):

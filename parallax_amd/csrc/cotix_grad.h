@@ -516,4 +516,255 @@ CX_DEV void resolve_vjp(const Dyn& b1, const Params& m1, const Dyn& b2, const Pa
   g2 = o2;
 }
 
+
+// ---------------------------------------------------------------------------
+// circle_vs_polygon (cotix/_contacts.py:157-202).  A circle's support is a
+// function of the search direction (Circle.get_support, d / |d| * r + c,
+// cotix/_convex_shapes.py:22-26), so the penetration depends on the circle
+// through EVERY GJK and EPA point the final edge descends from: jax.grad
+// differentiates the whole chain.  The forward is re-run with the exact
+// arithmetic of cx::gjk / cx::epa_big (same decisions, same bits) while each
+// Minkowski point records how its direction was made from earlier points;
+// the reverse pass then walks the points in reverse creation order.  The
+// polygon supports (argmax vertices) are constants.  Private memory (this
+// pair is never on the benchmark scenes' path).
+// ---------------------------------------------------------------------------
+// direction kinds: CONST d0; NEG -p[a]; FN s * fnormal(p[a] - p[b]) (GJK);
+// EPAN normalize(fnormal(p[a] - p[b])) (EPA; the circle support normalizes
+// again)
+enum : int { CP_CONST = 0, CP_NEG = 1, CP_FN = 2, CP_EPAN = 3 };
+constexpr int CP_GJK_MAX = 32;  // the default gjk_max_steps: larger values are refused for gradients
+constexpr int CP_NP = 3 + CP_GJK_MAX + 128;
+struct CPRec {
+  v2 p[CP_NP];
+  int16_t pa[CP_NP], pb[CP_NP];
+  int8_t kind[CP_NP], sg[CP_NP], vi[CP_NP];
+  int n = 0;
+};
+// the polygon's support index for direction d (support(Shape), polygon branch:
+// first NaN, else first maximum of v . d)
+CX_DEV int poly_support_idx(const Shape& s, v2 d) {
+  float bv = s.w[0] * d.x + s.w[1] * d.y;
+  int bk = 0;
+  for (int k = 1; k < MAXV; ++k) {
+    const float x = s.w[2 * k], y = s.w[2 * k + 1];
+    const float t = x * d.x + y * d.y;
+    const bool take = (k < s.n) & !isn(bv) & (isn(t) | (t > bv));
+    bv = take ? t : bv;
+    bk = take ? k : bk;
+  }
+  return bk;
+}
+// minkowski(C, P, d) = support(C, d) - support(P, -d), recorded
+CX_DEV int cp_point(const Shape& C, const Shape& P, v2 d, int kind, int a, int b, int sg, CPRec& R) {
+  const int k = poly_support_idx(P, neg(d));
+  const v2 pt = sub(support(C, d), vert(P, k));
+  const int id = R.n++;
+  R.p[id] = pt;
+  R.pa[id] = (int16_t)a;
+  R.pb[id] = (int16_t)b;
+  R.kind[id] = (int8_t)kind;
+  R.sg[id] = (int8_t)sg;
+  R.vi[id] = (int8_t)k;
+  return id;
+}
+// GJK (cx::gjk) + EPA (cx::epa_big) of circle C vs polygon P, recorded; false
+// when there is no contact.  e0 / e1: the ids of EPA's final edge
+CX_DEV bool cp_forward(const Shape& C, const Shape& P, const NarrowParams& np, CPRec& R, int* e0, int* e1) {
+  R.n = 0;
+  int i0 = cp_point(C, P, np.d0, CP_CONST, -1, -1, 1, R);
+  v2 s0 = R.p[i0];
+  int i1 = cp_point(C, P, neg(s0), CP_NEG, i0, -1, 1, R);
+  v2 s1 = R.p[i1];
+  v2 dir = fnormal(sub(s1, s0));
+  const int fa = i1, fb = i0;  // dir = +-fnormal(p[i1] - p[i0])
+  int sg = 1;
+  {
+    const bool sw = dot(dir, neg(s1)) > 0.0f;
+    const v2 t0 = s0;
+    const int j0 = i0;
+    s0 = sw ? s1 : s0;
+    i0 = sw ? i1 : i0;
+    s1 = sw ? t0 : s1;
+    i1 = sw ? j0 : i1;
+    dir = sw ? dir : neg(dir);
+    sg = sw ? 1 : -1;
+  }
+  int i2 = cp_point(C, P, dir, CP_FN, fa, fb, sg, R);
+  v2 s2 = R.p[i2];
+  for (int step = 0; step < np.gjk_steps; ++step) {
+    bool c1 = dot(s2, dir) <= 0.0f;
+    bool c2 = dot(fnormal(sub(s2, s0)), neg(s2)) < 0.0f;
+    bool c3 = dot(fnormal(sub(s1, s2)), neg(s2)) < 0.0f;
+    if (c1 || (c2 && c3)) break;
+    if (R.n >= 3 + CP_GJK_MAX) return false;  // (not reached: gjk_max_steps <= CP_GJK_MAX is checked at launch)
+    const v2 c = s2;
+    const int ic = i2;
+    const v2 acn = fnormal(sub(c, s0)), cbn = fnormal(sub(s1, c));
+    const bool ac = dot(acn, neg(c)) >= 0.0f;
+    const int pa = ac ? ic : i1, pb = ac ? i0 : ic;  // acn = fnormal(c - s0), cbn = fnormal(s1 - c)
+    s1 = ac ? c : s1;
+    i1 = ac ? ic : i1;
+    s0 = ac ? s0 : c;
+    i0 = ac ? i0 : ic;
+    dir = ac ? acn : cbn;
+    i2 = cp_point(C, P, dir, CP_FN, pa, pb, 1, R);
+    s2 = R.p[i2];
+  }
+  if (!point_in_triangle0(s0, s1, s2)) return false;
+  const float area = crs(sub(s1, s0), sub(s2, s0));
+  const bool allzero = s0.x == 0.0f && s0.y == 0.0f && s1.x == 0.0f && s1.y == 0.0f && s2.x == 0.0f && s2.y == 0.0f;
+  if (allzero || vnan(s0) || vnan(s1) || vnan(s2) || area == 0.0f) return false;
+  // EPA (epa_big), edge ids alongside the edges
+  constexpr int NE = 131;
+  v2 g0[NE], g1[NE];
+  int16_t d0[NE], d1[NE];
+  float dist[NE];
+  const int iters = np.epa_cp, ne = iters + 3;
+  const v2 z = v2{0.0f, 0.0f};
+  for (int k = 0; k < ne; ++k) {
+    g0[k] = z;
+    g1[k] = z;
+    d0[k] = d1[k] = -1;
+  }
+  g0[0] = s0; g1[0] = s1; d0[0] = (int16_t)i0; d1[0] = (int16_t)i1;
+  g0[1] = s1; g1[1] = s2; d0[1] = (int16_t)i1; d1[1] = (int16_t)i2;
+  g0[2] = s2; g1[2] = s0; d0[2] = (int16_t)i2; d1[2] = (int16_t)i0;
+  for (int k = 0; k < ne; ++k) dist[k] = edge_dist(g0[k], g1[k]);
+  int bei = argmin_first(dist, ne);
+  v2 best0 = g0[bei], best1 = g1[bei], newp = s2, prev0 = g0[0], prev1 = g1[0];
+  int b0 = d0[bei], b1 = d1[bei];
+  for (int i = 0; i < iters; ++i) {
+    bool c1 = sumsq(sub(best0, best1)) > 1e-9f;
+    bool c2 = crs(best0, best1) >= 0.0f;
+    v2 n = fnormal(sub(prev0, prev1));
+    n = divs(n, nrm(n));
+    float d = dot(newp, n);
+    float ed = nrm(closest_on_edge_to_origin(prev0, prev1));
+    bool c4 = (d - ed > 1e-6f) || (d <= 0.0f);
+    if (!(c4 && !vnan(best0) && !vnan(best1) && c1 && c2)) break;
+    n = fnormal(sub(best0, best1));
+    n = divs(n, nrm(n));
+    const int ip = cp_point(C, P, n, CP_EPAN, b0, b1, 1, R);
+    newp = R.p[ip];
+    g1[bei] = newp;
+    d1[bei] = (int16_t)ip;
+    dist[bei] = edge_dist(best0, newp);
+    g0[i + 3] = newp;
+    g1[i + 3] = best1;
+    d0[i + 3] = (int16_t)ip;
+    d1[i + 3] = (int16_t)b1;
+    dist[i + 3] = edge_dist(newp, best1);
+    prev0 = best0;
+    prev1 = best1;
+    bei = argmin_first(dist, ne);
+    best0 = g0[bei];
+    best1 = g1[bei];
+    b0 = d0[bei];
+    b1 = d1[bei];
+  }
+  *e0 = b0;
+  *e1 = b1;
+  return true;
+}
+// fnormal(a - b) = (-(a.y - b.y), a.x - b.x): cotangent g -> a, b
+CX_DEV void fnormal_diff_vjp(v2 g, v2* ga, v2* gb) {
+  ga->x += g.y;
+  gb->x -= g.y;
+  ga->y -= g.x;
+  gb->y += g.x;
+}
+// the VJP: cotangents (gpen, gcp) of the contact -> the circle's centre (gc)
+// and the polygon's world vertices (gv).  False when the re-run finds no
+// contact (not reached for a resolved contact)
+CX_DEV bool circle_poly_vjp(const Shape& C, const Shape& P, const NarrowParams& np, v2 gpen, v2 gcp, v2* gc,
+                            VGrad& gv) {
+  CPRec R;
+  int e0 = -1, e1 = -1;
+  if (!cp_forward(C, P, np, R, &e0, &e1)) return false;
+  const float r = C.d(0);
+  const v2 pos = v2{C.d(1), C.d(2)};
+  v2 g[CP_NP];
+  for (int k = 0; k < R.n; ++k) g[k] = v2{0.0f, 0.0f};
+  // pen = closest_on_edge_to_origin(e0, e1) (:270-273); a zero edge (never
+  // a contact's) has no points
+  if (e0 >= 0 && e1 >= 0) closest_vjp(R.p[e0], R.p[e1], gpen, &g[e0], &g[e1]);
+  for (int k = R.n - 1; k >= 0; --k) {
+    const v2 gp = g[k];
+    if (gp.x == 0.0f && gp.y == 0.0f) continue;
+    *gc = add(*gc, gp);          // + c
+    gv.add(R.vi[k], neg(gp));    // - vertex
+    const int kd = R.kind[k], a = R.pa[k], b = R.pb[k];
+    // the direction u handed to the circle support, and the point's value
+    // through it: p = (u / |u|) * r + c - v
+    v2 u;
+    v2 fn = v2{0.0f, 0.0f};
+    if (kd == CP_CONST) u = np.d0;
+    else if (kd == CP_NEG) u = neg(R.p[a]);
+    else {
+      fn = fnormal(sub(R.p[a], R.p[b]));
+      u = kd == CP_EPAN ? divs(fn, nrm(fn)) : (R.sg[k] > 0 ? fn : neg(fn));
+    }
+    const v2 gu = vjp_unit(u, scl(gp, r));
+    if (kd == CP_NEG) {
+      g[a] = sub(g[a], gu);
+    } else if (kd == CP_FN) {
+      const v2 gfn = R.sg[k] > 0 ? gu : neg(gu);
+      fnormal_diff_vjp(gfn, &g[a], &g[b]);
+    } else if (kd == CP_EPAN) {
+      fnormal_diff_vjp(vjp_unit(fn, gu), &g[a], &g[b]);
+    }
+  }
+  // the contact point (:168-197): the polygon edge k = (v_k, v_{k-1}) nearest
+  // the centre, or the centre when it is farther than r
+  float dists[MAXV];
+  v2 disps[MAXV];
+  const v2 last = vert(P, P.n - 1);
+  for (int k = 0; k < MAXV; ++k) {
+    dists[k] = 0.0f;
+    disps[k] = v2{0.0f, 0.0f};
+    if (k < P.n) {
+      const v2 a = v2{P.w[2 * k], P.w[2 * k + 1]}, b = k == 0 ? last : v2{P.w[2 * k - 2], P.w[2 * k - 1]};
+      if (a.x == 0.0f && a.y == 0.0f && b.x == 0.0f && b.y == 0.0f) {
+        disps[k] = v2{finf(), finf()};
+      } else {
+        const float len = sumsq(sub(a, b));
+        float t = dot(sub(pos, b), sub(a, b)) / len;
+        t = clip_(t, 0.0f, 1.0f);
+        disps[k] = sub(pos, add(b, scl(sub(a, b), t)));
+      }
+      dists[k] = sumsq(disps[k]);
+    }
+  }
+  const int k = argmin_first_n<MAXV>(dists, P.n);
+  *gc = add(*gc, gcp);  // cp = pos (+ disp)
+  float sk = dists[0];
+  for (int q = 1; q < MAXV; ++q)
+    if (q == k) sk = dists[q];
+  if (!(sk > r * r)) {
+    const int kb = k == 0 ? P.n - 1 : k - 1;
+    const v2 a = vert(P, k), b = vert(P, kb);
+    if (!(a.x == 0.0f && a.y == 0.0f && b.x == 0.0f && b.y == 0.0f)) {
+      // disp = pos - (b + d * tc), d = a - b, tc = clip(dot(pos - b, d) / |d|^2, 0, 1)
+      const v2 d = sub(a, b), pb = sub(pos, b);
+      const float len = sumsq(d), num = dot(pb, d), t = num / len, tc = clip_(t, 0.0f, 1.0f);
+      const v2 gdisp = gcp, gproj = neg(gdisp);
+      *gc = add(*gc, gdisp);
+      v2 ga = v2{0.0f, 0.0f}, gb = gproj, gd = scl(gproj, tc);
+      float gt = 0.0f, glo = 0.0f, ghi = 0.0f;
+      vjp_clip(t, 0.0f, 1.0f, dot(gproj, d), &gt, &glo, &ghi);
+      const float gnum = gt / len, glen = -gt * num / (len * len);
+      *gc = add(*gc, scl(d, gnum));
+      gb = sub(gb, scl(d, gnum));
+      gd = add(gd, scl(pb, gnum));
+      gd = add(gd, scl(d, 2.0f * glen));
+      ga = add(ga, gd);
+      gb = sub(gb, gd);
+      gv.add(k, ga);
+      gv.add(kb, gb);
+    }
+  }
+  return true;
+}
+
 }  // namespace cx

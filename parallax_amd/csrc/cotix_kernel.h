@@ -3734,6 +3734,30 @@ CX_DEV void ph_G(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
         const int pa = t.ti(sc.o_cpa + cid), pb = t.ti(sc.o_cpb + cid), fn = t.ti(sc.o_cfn + cid);
         const int ka = t.ti(sc.o_pkind + pa), kb = t.ti(sc.o_pkind + pb);
         const int wa = L.world + t.ti(sc.o_pwoff + pa), wb = L.world + t.ti(sc.o_pwoff + pb);
+        if ((FNSET & FNS_CIRCLE_POLY) != 0 && fn == FN_CIRCLE_POLY) {
+          // circle x polygon: the whole GJK / EPA chain through the circle's
+          // support (cx::circle_poly_vjp; a = the circle, b = the polygon)
+          const float gw_[12] = {gi.px, gi.py, gi.vx, gi.vy, gi.a, gi.w, gj.px, gj.py, gj.vx, gj.vy, gj.a, gj.w};
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            t.f(ai + k, e) = gw_[k];
+            t.f(aj + k, e) = gw_[6 + k];
+          }
+          const Shape WA = world_shape<EW>(c, t, pa, e), WB = world_shape<EW>(c, t, pb, e);
+          v2 gc = v2{0.0f, 0.0f};
+          VGrad vb;
+          vb.zero();
+          circle_poly_vjp(WA, WB, narrow_of(sc), gpen, gcp, &gc, vb);
+          float gp[3] = {0.0f, 0.0f, 0.0f};
+          part_pose_vjp<EW>(c, t, pb, e, WB, vb, gp);
+          const int qa = L.adj + 6 * t.ti(sc.o_pbody + pa), qb = L.adj + 6 * t.ti(sc.o_pbody + pb);
+          t.f(qa, e) = t.f(qa, e) + gc.x;  // the circle translates with its body
+          t.f(qa + 1, e) = t.f(qa + 1, e) + gc.y;
+          t.f(qb, e) = t.f(qb, e) + gp[0];
+          t.f(qb + 1, e) = t.f(qb + 1, e) + gp[1];
+          t.f(qb + 4, e) = t.f(qb + 4, e) + gp[2];
+          continue;
+        }
         if (FNSET != FNS_ANALYTIC && (fn == FN_POLY_POLY || fn == FN_AABB_POLY)) {
           // (store the resolution's body cotangents first: the contact's go on top)
           const float gw_[12] = {gi.px, gi.py, gi.vx, gi.vy, gi.a, gi.w, gj.px, gj.py, gj.vx, gj.vy, gj.a, gj.w};

@@ -579,9 +579,9 @@ int cotix_rollout_backward_ex(cotix_scene* scene, const float* saved_dyn, const 
     return -1;
   if (!ret_weights) return fail("null argument");
   if (grad_action && !action) return fail("grad_action needs the action the rollout was run with");
-  if (scene->fnset & cxk::FNS_CIRCLE_POLY)
-    return fail("differentiable rollout: circle x polygon contacts are not differentiated (EPA's circle supports "
-                "chain through every iteration); circle/AABB/polygon scenes without that pair only");
+  if ((scene->fnset & cxk::FNS_CIRCLE_POLY) && scene->host.gjk_steps > cx::CP_GJK_MAX)
+    return fail("differentiable rollout: circle x polygon gradients record every GJK point: gjk_max_steps <= " +
+                std::to_string(cx::CP_GJK_MAX));
   if ((stages & COTIX_STAGE_LUNAR) && !(scene->fnset & ~FNS_ANALYTIC))
     return fail("differentiable rollout: the LunarLander joint stage needs the polygon program (a polygon scene)");
   if (B == 0 || n_steps == 0) return 0;

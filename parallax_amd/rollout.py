@@ -15,8 +15,9 @@ over the n_bodies*6 state words (default: the ball's x position, body 4 of
 RoboCup).  Derivatives are jax.grad's through the reference: the executed
 branch of every lax.cond, RandomizedCollider choices held fixed, balanced
 ties for max/min/clip.  Circle, AABB and polygon contacts (GJK/EPA through
-EPA's final edge and contact_from_edges) and the LunarLander joints
-(stages=_ffi.STAGES_LUNAR); circle x polygon scenes are rejected.
+EPA's final edge and contact_from_edges), circle x polygon contacts (through
+every GJK / EPA point the circle's direction-dependent support builds) and
+the LunarLander joints (stages=_ffi.STAGES_LUNAR).
 """
 import numpy as np
 import torch

@@ -248,8 +248,8 @@ int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* sa
                          const float* geom, int gstride, int B, int n_steps, float dt, int stages, const float* action,
                          int action_body, const float* ret_w, float* grad_action, float* grad_dyn0, int E) {
   EmuScene* s = static_cast<EmuScene*>(scene);
-  if (s->fnset & cxk::FNS_CIRCLE_POLY) {  // (the library's admission, cotix_step.hip)
-    g_err = "differentiable rollout: circle x polygon contacts are not differentiated";
+  if ((s->fnset & cxk::FNS_CIRCLE_POLY) && s->s.gjk_steps > cx::CP_GJK_MAX) {  // (the library's admission, cotix_step.hip)
+    g_err = "differentiable rollout: circle x polygon gradients record every GJK point: gjk_max_steps <= 32";
     return -1;
   }
   if ((stages & COTIX_STAGE_LUNAR) && !(s->fnset & ~1)) {
@@ -501,4 +501,32 @@ extern "C" long emu_lds_bytes(void* scene, int ew) {
 }
 extern "C" long emu_lds_bytes_w(void* scene, int ew, int wpb) {
   return (long)cxk::lds_bytes(static_cast<EmuScene*>(scene)->s, wpb, ew);
+}
+
+// circle x polygon: the gradient's recorded re-run (cx::cp_forward) against
+// the forward contact (cx::circle_vs_polygon) -- same penetration bits
+extern "C" int emu_circle_poly_check(int n, const float* a, const float* b, float* pen_fwd, float* pen_rec) {
+  const cx::NarrowParams np = cx::narrow_default();
+  for (int i = 0; i < n; ++i) {
+    cx::Shape C, P;
+    C.kind = cx::KIND_CIRCLE;
+    C.n = 0;
+    P.kind = cx::KIND_POLY;
+    P.n = (int)b[18 * i + 1];
+    for (int k = 0; k < 2 * cx::MAXV; ++k) {
+      C.w[k] = a[18 * i + 2 + k];
+      P.w[k] = b[18 * i + 2 + k];
+    }
+    const cx::Contact ct = cx::circle_vs_polygon(C, P, np);
+    pen_fwd[2 * i] = ct.pen.x;
+    pen_fwd[2 * i + 1] = ct.pen.y;
+    cx::CPRec R;
+    int e0 = -1, e1 = -1;
+    cx::v2 pr = cx::v2{cx::qnan(), cx::qnan()};
+    if (cx::cp_forward(C, P, np, R, &e0, &e1) && e0 >= 0 && e1 >= 0) pr = cx::closest_on_edge_to_origin(R.p[e0], R.p[e1]);
+    else if (cx::cp_forward(C, P, np, R, &e0, &e1)) pr = cx::v2{0.0f, 0.0f};
+    pen_rec[2 * i] = pr.x;
+    pen_rec[2 * i + 1] = pr.y;
+  }
+  return 0;
 }

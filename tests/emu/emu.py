@@ -31,6 +31,7 @@ def load(asan=False, path=None):
     lib.emu_contacts.argtypes = [ctypes.c_int, ctypes.c_int, P_, P_, P_, P_]
     lib.emu_order_clockwise.argtypes = [P_, ctypes.c_int, ctypes.c_int]
     lib.emu_gjk_start.argtypes = [ctypes.c_int, P_, P_, ctypes.c_int, P_]
+    lib.emu_circle_poly_check.argtypes = [ctypes.c_int, P_, P_, P_, P_]
     lib.emu_body_penetration.argtypes = [P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_]
     lib.emu_body_aabb.argtypes = [P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, P_, P_]
     lib.emu_rollout.argtypes = [P_, P_, P_, P_, P_, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,

@@ -673,6 +673,21 @@ def test_rollout_grad_polygon_box_vs_oracle(torch_cuda):
     _check_grad_vs_oracle(case, ret, ga, gd)
 
 
+def test_rollout_grad_ball_on_polygons_vs_oracle(torch_cuda):
+    """Gradients through circle x polygon contacts (cotix/_contacts.py:157-202):
+    GJK + EPA with the circle's direction-dependent support, differentiated
+    through every point of the chain (cx::circle_poly_vjp), against the
+    torch-f32 VJP oracle (checked against finite differences in
+    tests/test_grad_cpu.py); tape and re-play backwards bit for bit."""
+    torch = torch_cuda
+    import parallax_amd as pa
+    import grad_cases as GC
+    case = GC.ball_poly_case(16, 12, seed=1)
+    _, ret, ga, gd, _ = _gpu_rollout(torch, case, _pa_bodies(pa, case["make"]()))
+    _check_grad_vs_oracle(case, ret, ga, gd)
+    assert np.isfinite(ga).all() and np.abs(ga).max() > 0.1
+
+
 def test_rollout_grad_quad_row_vs_oracle(torch_cuda):
     """Nine polygons of one contact type: the contact VJPs inside phase G, at
     the scene's default tiling (2 envs per wave: its tile exceeds the LDS at

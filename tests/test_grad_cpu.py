@@ -3,6 +3,7 @@ and backward wave programs (host emulation, tests/emu) against the torch
 float32 VJP chain of the oracle (oracle/cotix_oracle/grad.py), itself
 checked against central finite differences of the faithful oracle."""
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -292,3 +293,49 @@ def test_g_regs_equals_tile_form(emu_lib):
             nx, ny = np.isnan(x), np.isnan(y)
             assert np.array_equal(nx, ny)
             assert np.array_equal(x[~nx].view(np.uint32), y[~ny].view(np.uint32))
+
+
+def test_circle_poly_recorded_forward_is_the_forward(emu_lib):
+    """The circle x polygon gradient re-runs GJK + EPA while recording every
+    Minkowski point (cx::cp_forward): its final edge gives the forward
+    contact's penetration bit for bit (cx::circle_vs_polygon, 128 EPA
+    iterations) over the golden circle x polygon pairs and random ones."""
+    import ctypes
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import make_golden as M
+    from cotix_oracle import geometry as Gm
+    rng = np.random.default_rng(5)
+    pairs = [(Gm.Circle(np.float32(rng.uniform(0.2, 1.5)), (np.float32(rng.normal() * 0.7),
+                                                             np.float32(rng.normal() * 0.7))),
+              M.rand_poly(rng, n)) for n in (3, 4, 5, 6, 8) for _ in range(200)]
+    a = np.ascontiguousarray(np.array([M.row(c) for c, _ in pairs], np.float32))
+    b = np.ascontiguousarray(np.array([M.row(p) for _, p in pairs], np.float32))
+    n = len(pairs)
+    pf, pr = np.zeros((n, 2), np.float32), np.zeros((n, 2), np.float32)
+    P_ = ctypes.c_void_p
+    lib.emu_circle_poly_check(n, a.ctypes.data_as(P_), b.ctypes.data_as(P_), pf.ctypes.data_as(P_),
+                              pr.ctypes.data_as(P_))
+    hit = ~np.isnan(pr).any(1)
+    assert hit.sum() > 200
+    assert np.array_equal(pf[hit].view(np.uint32), pr[hit].view(np.uint32))
+
+
+@pytest.mark.parametrize("E", [1, 4])
+def test_emu_rollout_ball_on_polygons(emu_lib, E):
+    """Gradients through circle x polygon contacts (GJK + EPA with the
+    circle's direction-dependent support, every point of the chain): the
+    kernel logic's tape backward and re-play agree bit for bit and match the
+    torch-f32 VJP oracle (itself checked against finite differences above)."""
+    emu, lib = emu_lib
+    case = GC.ball_poly_case(8, 12, seed=1)
+    ret, ga, gd = _emu_run_st(emu, lib, case, 1 | 4 | 16, E=E)
+    from cotix_oracle import grad as OG
+    calls = []
+    real = OG._circle_polygon_contact
+    OG._circle_polygon_contact = lambda *a: calls.append(1) or real(*a)
+    try:
+        _check_vs_oracle(case, ret, ga, gd)
+    finally:
+        OG._circle_polygon_contact = real
+    assert len(calls) > 20  # circle x polygon resolutions in the compared gradients

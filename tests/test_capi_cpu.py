@@ -233,9 +233,11 @@ def test_tiling_is_a_scene_property():
     import scene_cases
     from test_gpu_parity import _pa_bodies
     quad_row = pa.Scene(_pa_bodies(pa, GC.quad_row_case(1, 1)["make"]()))
-    assert quad_row.variant()["envs_per_wave"] == 2
+    assert quad_row.variant()["envs_per_wave"] == 2 and quad_row.waves_per_group() == 4
+    quad_row.set_variant(4)  # an explicit tiling beyond four tiles per CU: workgroups of fewer waves
+    assert quad_row.waves_per_group() in (1, 2)
     with pytest.raises(RuntimeError, match="bytes of LDS"):
-        quad_row.set_variant(4)
+        pa.Scene(_pa_bodies(pa, scene_cases.octagon_row(15))).set_variant(8)
     quad_row.set_variant(1)
     quad_row.set_variant(0)
     assert quad_row.variant()["envs_per_wave"] == 2

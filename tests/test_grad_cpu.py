@@ -212,14 +212,16 @@ def test_emu_rollout_quad_row(emu_lib):
     _check_vs_oracle(case, ret, ga, gd)
 
 
-def test_backward_rejects_circle_polygon_and_analytic_joints(emu_lib):
-    """Circle x polygon contacts are not differentiated (EPA's circle supports
-    chain through every iteration); the joint stage needs the polygon program."""
+def test_backward_rejects_long_gjk_circle_polygon_and_analytic_joints(emu_lib):
+    """Circle x polygon gradients record every GJK point: a parameter block
+    with gjk_max_steps > 32 is refused for them; the joint stage needs the
+    polygon program."""
     emu, lib = emu_lib
     from cotix_oracle import geometry as Gm
     from cotix_oracle import physics as P
+    from cotix_oracle import params as OPr
     bodies = GC.poly_box_bodies() + [P.Body([Gm.Circle(0.2, (0.0, 0.0))], position=(1.5, 0.2))]
-    h, geom = emu.oracle_scene(lib, bodies)
+    h, geom = emu.oracle_scene(lib, bodies, OPr.Params(gjk_max_steps=33))
     sd = np.zeros((1, 5, 6, 1), np.float32)
     sk = np.zeros((1, 1, 2), np.uint32)
     with pytest.raises(RuntimeError, match="circle x polygon"):

@@ -88,8 +88,11 @@ def test_adapter_errors():
     with pytest.raises(TypeError, match="Ellipse is not in the contact-function registry"):
         pa.World.from_bodies(bad, device="cpu")
     two = RS.stack([RS.from_oracle(P.robocup_bodies()) for _ in range(2)])
-    two[4].mass = np.array([0.5, 0.6], np.float32)
-    with pytest.raises(ValueError, match="mass differs across the batch"):
+    two[4].mass = np.array([0.5, 0.6], np.float32)  # a varying parameter leaf: per-env parameters
+    w2 = pa.World.from_bodies(two, device="cpu")
+    assert w2.scene.per_env_params and tuple(w2.geom.shape) == (2, w2.scene.geom_floats)
+    two[4].mass = np.array([[0.5], [0.6]], np.float32)
+    with pytest.raises(ValueError, match="expected rank 0"):
         pa.World.from_bodies(two, device="cpu")
     with pytest.raises(ValueError, match="batch"):
         pa.World.from_bodies(RS.stack([sc, RS.from_oracle(P.robocup_bodies())]), batch=3, device="cpu")

@@ -64,6 +64,10 @@ static __device__ unsigned long long g_sub_cycles[8];
 #define CXK_SUB_T1(k, lane) ((void)0)
 #endif
 
+// a lambda that must be inlined (a call would put every local it captures by
+// reference into scratch memory)
+#define CXK_INLINE_LAMBDA __attribute__((always_inline))
+
 // phase-cost experiments of the tooling build (-DCOTIX_TOOLING, KArgs::dbg_skip
 // from COTIX_DEBUG_SKIP) skip whole phases; the release library compiles every
 // skip out, so no environment variable can change what it computes
@@ -4126,7 +4130,7 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
   ActRegs ac;
   // the step after its restore: Euler, world parts, the tape's resolutions,
   // the reverse chain (the same for both restore forms)
-  auto reverse_step = [&](int step, auto dphase) {
+  auto reverse_step = [&](int step, auto dphase) CXK_INLINE_LAMBDA {
     run(PH_A, [&](int l) {  // Euler (+ gravity, + action); no key split, no collider scratch
       if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
         for (int w = l; w < c.nb * EW; w += WAVE) {
@@ -4155,7 +4159,7 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
     };
     Pre p0, p1;
     const TapeRegs none{};
-    auto prefetch = [&](int l, int s, Pre& p) {
+    auto prefetch = [&](int l, int s, Pre& p) CXK_INLINE_LAMBDA {
       restore_rows_fetch<EW>(a, c, env0, l, s, p.rw);
       if (apf) act_fetch<EW>(a, c, env0, l, s, p.an);
     };
@@ -4164,7 +4168,7 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
         prefetch(l, a.n_steps - 1, p0);
         if (a.n_steps > 1) prefetch(l, a.n_steps - 2, p1);
       });
-    auto one = [&](int step, Pre& cur) {
+    auto one = [&](int step, Pre& cur) CXK_INLINE_LAMBDA {
       run(PH_RESTORE, [&](int l) {
         restore_rows_apply<EW>(c, t, l, cur.rw);
         ac = cur.an;

@@ -677,8 +677,14 @@ CX_DEV void fnormal_diff_vjp(v2 g, v2* ga, v2* gb) {
 // the VJP: cotangents (gpen, gcp) of the contact -> the circle's centre (gc)
 // and the polygon's world vertices (gv).  False when the re-run finds no
 // contact (not reached for a resolved contact)
-CX_DEV bool circle_poly_vjp(const Shape& C, const Shape& P, const NarrowParams& np, v2 gpen, v2 gcp, v2* gc,
-                            VGrad& gv) {
+// (not inlined: its private point record and EPA buffer stay out of the
+// calling kernel's register allocation; only this rare pair pays the call)
+#if defined(__HIP__)
+__device__ __attribute__((noinline))
+#else
+static
+#endif
+bool circle_poly_vjp(const Shape& C, const Shape& P, const NarrowParams& np, v2 gpen, v2 gcp, v2* gc, VGrad& gv) {
   CPRec R;
   int e0 = -1, e1 = -1;
   if (!cp_forward(C, P, np, R, &e0, &e1)) return false;

@@ -335,7 +335,9 @@ int cotix_eval(cotix_scene* scene, float* dyn, uint32_t* keys, uint32_t* err, co
  *
  * cotix_rollout runs the forward like cotix_step (no restarts) and saves the
  * state and key before every step: saved_dyn device f32
- * [n_steps][n_bodies][6][B], saved_keys device u32 [n_steps][B][2];
+ * [n_steps][ceil(B/4)][n_bodies*6][4] (env blocks of 4: state word r of env g
+ * at [step][g/4][r][g%4], so that a wave's 4 envs save one contiguous run),
+ * saved_keys device u32 [n_steps][B][2];
  * ret_weights is HOST f32 [n_bodies*6]; ret device f32 [B] (accumulated).
  *
  * cotix_rollout_backward re-plays every step from the saved state (so each
@@ -363,7 +365,8 @@ int cotix_rollout_backward(cotix_scene* scene, const float* saved_dyn, const uin
                            cotix_stream_t stream);
 /* The same with the forward's decision tape (no reference counterpart: the
  * saved outcome of the forward's discrete work).  cotix_rollout_ex also writes
- *   tape device u32 [n_steps][cotix_rollout_tape_words(scene)][B] (nullable):
+ *   tape device u32 [n_steps][ceil(B/4)][cotix_rollout_tape_words(scene)][4]
+ *        (nullable; env blocks of 4 as saved_dyn):
  *        per step and body the resolution RandomizedCollider.resolve applied
  *        (cotix/_colliders.py:274-336: the chosen partner j*, the contact of
  *        cell (i, j*)) and, in polygon scenes, the final EPA edge of every

@@ -15,7 +15,7 @@ from .physics import (ContactInfo, ExplicitEulerPhysics, RandomizedCollider, Sim
                       check_for_collision_convex, compute_penetration_vector_convex, contact_funcs,
                       resolve_collision, run_contacts)
 from .rollout import rollout as differentiable_rollout  # noqa: F401
-from .rollout import rollout_backward, rollout_forward  # noqa: F401
+from .rollout import rollout_backward, rollout_forward, trajectory  # noqa: F401
 from .scenarios import BoxWorld, LunarLander, RoboCupEnv  # noqa: F401
 from .shapes import AABB, Circle, Polygon, Polygon3, Polygon4, Polygon5, Polygon6, UniversalShape  # noqa: F401
 from .world import Scene, World  # noqa: F401

@@ -236,15 +236,16 @@ struct KArgs {
   int32_t* trace_chosen;   // [n_steps][nb][B]
   int32_t* trace_cells;    // [n_steps][nb][nb][B]: i1 | i2 << 9 | type << 18, -1 = empty cell
   // differentiable rollout (cotix_rollout / cotix_rollout_backward)
-  float* save_dyn;         // [n_steps][nb*6][B]: state before each step, or null
+  float* save_dyn;         // [n_steps][B/4][nb*6][4] (row_at): state before each step, or null
   uint32_t* save_keys;     // [n_steps][B][2]
   float* ret;              // [B] += sum_t sum_k ret_w[k] * state_{t+1}[k] (terms with ret_w[k] == 0 skipped)
   float* grad_action;      // backward: [n_steps][B][2] d ret / d action
   float* grad_dyn;         // backward: [nb*6][B] d ret / d initial state, or null
   float ret_w[MAXB * 6];
   // the rollout's decision tape (cotix_rollout_ex / cotix_rollout_backward_ex;
-  // null = off): [n_steps][tw][B] words, written by the forward, read by the
-  // backward instead of re-playing the collider (tape_words below)
+  // null = off): [n_steps][B/4][tw][4] words (row_at), written by the
+  // forward, read by the backward instead of re-playing the collider
+  // (tape_words below)
   uint32_t* tape;
   int tw;
   // cotix_eval (AbstractEnvironment.eval, cotix/_envs.py:37-132, fused):
@@ -258,8 +259,16 @@ struct KArgs {
   CtlArgs ctl;             // device AbstractControl (ctl.on == 0: off)
 };
 
+// The rollout's saved rows (save_dyn: nb*6 state words per env-step; tape:
+// tw words) in env blocks of 4: row r of step s, env g at
+// [((s * ceil(B/4) + g/4) * rows + r) * 4 + g%4].  A wave of 4 envs saves and
+// restores its rows as one contiguous run of 16-byte pieces (a [row][B] layout
+// puts every row of the wave in a cache line of its own)
+CX_HD size_t row_at(int B, int rows, int s, int r, int g) {
+  return (((size_t)s * (size_t)((B + 3) >> 2) + (size_t)(g >> 2)) * (size_t)rows + (size_t)r) * 4u + (size_t)(g & 3);
+}
 // The rollout's decision tape, per env-step (word w of step s, env g at
-// tape[(s * tw + w) * B + g]):
+// tape[row_at(B, tw, s, w, g)]):
 //   5 i        body i's resolution (cotix/_colliders.py:310-336): its partner
 //              j* | the distinct contact id of cell (i, j*) << 8, or RP_NONE
 //              when the body resolves nothing this step
@@ -1376,7 +1385,7 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
         const int o = 5 * c.nb + 4 * ci;
         const float ev[4] = {edge[0].x, edge[0].y, edge[1].x, edge[1].y};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a.tape[((size_t)step * a.tw + o + q) * a.B + g] = __float_as_uint(ev[q]);
+        for (int q = 0; q < 4; ++q) a.tape[row_at(a.B, a.tw, step, o + q, g)] = __float_as_uint(ev[q]);
       }
       ct.cp = v2{qnan(), qnan()};
       // a part paired with itself: only the NaN-ness of its contact point is
@@ -1985,7 +1994,7 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
     const int o = 5 * c.nb + 4 * ci;
     const float ev[4] = {edge[0].x, edge[0].y, edge[1].x, edge[1].y};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) a.tape[((size_t)step * a.tw + o + q) * a.B + g] = __float_as_uint(ev[q]);
+    for (int q = 0; q < 4; ++q) a.tape[row_at(a.B, a.tw, step, o + q, g)] = __float_as_uint(ev[q]);
   }
   ct.cp = v2{qnan(), qnan()};
   if (hit && self && self_cp_finite(S)) ct.cp = v2{0.0f, 0.0f};  // S is A on lane 0 (see b_item)
@@ -2464,8 +2473,7 @@ CX_DEV cx::Rcp load_rcp(const uint32_t* tb, int o) {
 // backward uses
 CX_HD int tape_stage(const Ctx& c) { return c.L.rec - 5 * c.nb; }
 template <int EW, bool RCP>
-CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, bool stage = false, uint32_t* tp = nullptr,
-                    int B = 0) {
+CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, bool stage = false, uint32_t* tp = nullptr) {
   // branch-free: the operands are computed from clamped indices for every
   // item and the partner is set only for a real resolution (the inactive
   // items' operands are never read: E1 skips RP_NONE)
@@ -2517,10 +2525,10 @@ CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, bool
   } else if (tp != nullptr) {
     tp[0] = w0;
     if (res) {
-      tp[(size_t)B] = __builtin_bit_cast(uint32_t, t.f(co, e));
-      tp[2 * (size_t)B] = __builtin_bit_cast(uint32_t, t.f(co + 1, e));
-      tp[3 * (size_t)B] = __builtin_bit_cast(uint32_t, cp.x);
-      tp[4 * (size_t)B] = __builtin_bit_cast(uint32_t, cp.y);
+      tp[4] = __builtin_bit_cast(uint32_t, t.f(co, e));  // (rows 4 words apart, row_at)
+      tp[8] = __builtin_bit_cast(uint32_t, t.f(co + 1, e));
+      tp[12] = __builtin_bit_cast(uint32_t, cp.x);
+      tp[16] = __builtin_bit_cast(uint32_t, cp.y);
     }
   }
 }
@@ -2528,8 +2536,7 @@ CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, bool
 // one (body i, env) item of phase D; NB > 0: the body count at compile time
 // (unrolled loads and selects), NB == 0: any count up to MAXB
 template <int EW, bool PRE, int NB, bool RCP>
-CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, bool stage = false, uint32_t* tp = nullptr,
-                   int B = 0) {
+CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, bool stage = false, uint32_t* tp = nullptr) {
   using namespace cx;
   constexpr int MB = NB > 0 ? NB : MAXB;
   const int nb = NB > 0 ? NB : c.nb, nt = c.nt;
@@ -2580,7 +2587,7 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, bool stage 
 #pragma unroll
   for (int j = 0; j < MB; ++j) cid = j == ch ? mm[j] : cid;
   cid = cid < 0 ? -1 : (cid >> 18) & 511;
-  e0_item<EW, RCP>(c, t, e, i, ch, cid, stage, tp, B);
+  e0_item<EW, RCP>(c, t, e, i, ch, cid, stage, tp);
 }
 // TAPE: the rollout forward stages each body's tape words (partner, contact
 // id, contact) here, from the operands phase D has in hand, next to phase
@@ -2593,15 +2600,15 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     const int e = w % EW, i = w / EW;
     if (env0 + e >= a.B) continue;
     const bool stage = TAPE && a.tape != nullptr && tape_rec(c.sh);
-    uint32_t* tp = TAPE && a.tape != nullptr && !stage ? a.tape + ((size_t)step * a.tw + 5 * i) * a.B + env0 + e : nullptr;
+    uint32_t* tp = TAPE && a.tape != nullptr && !stage ? a.tape + row_at(a.B, a.tw, step, 5 * i, env0 + e) : nullptr;
     if (c.sh.rcp_all) {
-      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, slot, stage, tp, a.B);
-      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, slot, stage, tp, a.B);
-      else d_item<EW, PRE, 0, true>(c, t, e, i, slot, stage, tp, a.B);
+      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, slot, stage, tp);
+      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, slot, stage, tp);
+      else d_item<EW, PRE, 0, true>(c, t, e, i, slot, stage, tp);
     } else {
-      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, slot, stage, tp, a.B);
-      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, slot, stage, tp, a.B);
-      else d_item<EW, PRE, 0, false>(c, t, e, i, slot, stage, tp, a.B);
+      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, slot, stage, tp);
+      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, slot, stage, tp);
+      else d_item<EW, PRE, 0, false>(c, t, e, i, slot, stage, tp);
     }
   }
 }
@@ -2626,12 +2633,18 @@ struct RowRegs {
 template <int EW>
 CX_DEV void restore_rows_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step, RowRegs& r) {
   const int nd = 6 * c.nb, nr = nd + (5 + REC_W) * c.nb;
+  // the row's source as a select of two byte addresses, not of the two
+  // pointer arguments: a per-lane select of kernel arguments compiles into a
+  // vector load of the argument itself, and the s_waitcnt vmcnt(0) it needs
+  // waits for every store in flight (the previous step's grad_action).
+  // The wave's rows are contiguous (row_at): 16 bytes per row from two bases
+  const uintptr_t sd = reinterpret_cast<uintptr_t>(a.save_dyn) + row_at(a.B, nd, step, 0, env0) * 4u;
+  const uintptr_t st = reinterpret_cast<uintptr_t>(a.tape) + row_at(a.B, a.tw, step, 0, env0) * 4u - (size_t)nd * 16u;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int row = q * WAVE + lane;
-    const uint32_t* src = row < nd ? reinterpret_cast<const uint32_t*>(a.save_dyn) + ((size_t)step * nd + row) * a.B
-                                   : a.tape + ((size_t)step * a.tw + (row - nd)) * a.B;
-    if (row < nr) r.d[q] = *reinterpret_cast<const U4*>(src + env0);
+    const uintptr_t src = (row < nd ? sd : st) + (size_t)row * 16u;
+    if (row < nr) r.d[q] = *reinterpret_cast<const U4*>(src);
   }
   const int g = env0 + lane;
   const bool le = lane < EW && g < a.B;
@@ -2889,21 +2902,19 @@ CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const Ret
 }
 
 // tile rows [o, o + n) of the wave's envs (row r: EW words, env fastest) to
-// the global rows dst + r * B (env fastest, B per row): with 4 envs per wave,
-// a whole wave and 16-byte aligned rows, one 16-byte store per row (a lane
-// each: the rollout's saves were one 4-byte store per word and env); else one
-// word per (row, env) lane
+// rows [0, n) of step `step` of a saved-rows array of `rows` rows (row_at):
+// with 4 envs per wave and a whole block, one 16-byte store per row (a lane
+// each, the wave's n rows one contiguous run); else one word per (row, env)
+// lane
 template <int EW>
-CX_DEV void rows_out(Tile<EW> t, int o, int n, uint32_t* dst, int B, int env0, int lane) {
-  if (EW == 4 && (B & 3) == 0 && env0 + 4 <= B) {
-    for (int r = lane; r < n; r += WAVE) {
-      const U4 w = U4{{t.w(o + r, 0), t.w(o + r, 1), t.w(o + r, 2), t.w(o + r, 3)}};
-      *reinterpret_cast<U4*>(dst + (size_t)r * B + env0) = w;
-    }
+CX_DEV void rows_out(Tile<EW> t, int o, int n, uint32_t* dst, int rows, int step, int B, int env0, int lane) {
+  if (EW == 4 && env0 + 4 <= B) {
+    U4* blk = reinterpret_cast<U4*>(dst + row_at(B, rows, step, 0, env0));
+    for (int r = lane; r < n; r += WAVE) blk[r] = U4{{t.w(o + r, 0), t.w(o + r, 1), t.w(o + r, 2), t.w(o + r, 3)}};
   } else {
     for (int w = lane; w < n * EW; w += WAVE) {
       const int e = w % EW, r = w / EW;
-      if (env0 + e < B) dst[(size_t)r * B + env0 + e] = t.w(o + r, e);
+      if (env0 + e < B) dst[row_at(B, rows, step, r, env0 + e)] = t.w(o + r, e);
     }
   }
 }
@@ -2919,8 +2930,7 @@ CX_DEV void rows_out(Tile<EW> t, int o, int n, uint32_t* dst, int B, int env0, i
 template <int EW, bool TR>
 CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
   // (polygon scenes: phase D stores their resolution words, phase B EPA's edges)
-  if (TR && tape_rec(c.sh)) rows_out<EW>(t, tape_stage(c), (5 + REC_W) * c.nb, a.tape + (size_t)step * a.tw * a.B, a.B,
-                                         env0, lane);
+  if (TR && tape_rec(c.sh)) rows_out<EW>(t, tape_stage(c), (5 + REC_W) * c.nb, a.tape, a.tw, step, a.B, env0, lane);
 }
 
 // TREC: the rollout forward with a tape records the resolutions (as REC) for
@@ -3230,8 +3240,7 @@ CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane
   if (a.tape != nullptr && step > 0 && (a.stages & COTIX_STAGE_COLLIDER) && !CXK_SKIP(a, 128))
     tape_save<EW, TR>(a, c, t, env0, lane, step - 1);
   if (CXK_SKIP(a, 256)) return;
-  rows_out<EW>(t, c.L.dyn, c.nb * 6, reinterpret_cast<uint32_t*>(a.save_dyn) + (size_t)step * c.nb * 6 * a.B, a.B,
-               env0, lane);
+  rows_out<EW>(t, c.L.dyn, c.nb * 6, reinterpret_cast<uint32_t*>(a.save_dyn), c.nb * 6, step, a.B, env0, lane);
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g < a.B) {
@@ -3282,13 +3291,13 @@ struct RestoreRegs {
 };
 template <int EW>
 CX_DEV void restore_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int step, RestoreRegs& r) {
-  const size_t base = (size_t)step * c.nb * 6 * a.B;
   const int nd = c.nb * 6 * EW;
 #pragma unroll
   for (int q = 0; q < RQ; ++q) {
     const int w = q * WAVE + lane, e = w % EW, off = w / EW, g = env0 + e;
     if (q * WAVE >= nd) break;  // uniform
-    r.d[q] = (w < nd && g < a.B) ? a.save_dyn[base + (size_t)off * a.B + g] : 0.0f;
+    const bool ok = w < nd && g < a.B;
+    r.d[q] = ok ? a.save_dyn[row_at(a.B, c.nb * 6, step, ok ? off : 0, ok ? g : 0)] : 0.0f;
   }
   const int g = env0 + lane;
   const bool le = lane < EW && g < a.B;
@@ -3326,13 +3335,13 @@ CX_DEV void tape_fetch(const KArgs& a, const Ctx& c, int env0, int lane, int ste
     if (q * WAVE >= ni) break;  // uniform
     const int w = q * WAVE + lane, e = w % EW, i = w / EW, g = env0 + e;
     const bool ok = w < ni && g < a.B;
-    const uint32_t* p = a.tape + ((size_t)step * a.tw + 5 * (ok ? i : 0)) * a.B + (ok ? g : 0);
+    const uint32_t* p = a.tape + row_at(a.B, a.tw, step, 5 * (ok ? i : 0), ok ? g : 0);  // (rows 4 words apart)
 #pragma unroll
-    for (int k = 0; k < 5; ++k) r.d[q][k] = ok ? p[(size_t)k * a.B] : RP_NONE;
+    for (int k = 0; k < 5; ++k) r.d[q][k] = ok ? p[4 * k] : RP_NONE;
     if (TR && tape_rec(c.sh)) {  // the resolution's record (read whether or not it resolved: no dependent round trip)
-      const uint32_t* pr = a.tape + ((size_t)step * a.tw + 5 * c.nb + REC_W * (ok ? i : 0)) * a.B + (ok ? g : 0);
+      const uint32_t* pr = a.tape + row_at(a.B, a.tw, step, 5 * c.nb + REC_W * (ok ? i : 0), ok ? g : 0);
 #pragma unroll
-      for (int k = 0; k < REC_W; ++k) r.x[q][k] = ok ? pr[(size_t)k * a.B] : 0u;
+      for (int k = 0; k < REC_W; ++k) r.x[q][k] = ok ? pr[4 * k] : 0u;
     }
   }
 }
@@ -3345,9 +3354,9 @@ CX_DEV void tape_edge_fetch(const KArgs& a, const Ctx& c, int env0, int lane, in
     const int w = q * WAVE + lane, g = env0 + w % EW;
     const bool ok = w < ni && g < a.B && r.d[q][0] != RP_NONE;
     const int cid = ok ? (int)((r.d[q][0] >> 8) & 511u) : 0;
-    const uint32_t* p = a.tape + ((size_t)step * a.tw + 5 * c.nb + 4 * cid) * a.B + (ok ? g : 0);
+    const uint32_t* p = a.tape + row_at(a.B, a.tw, step, 5 * c.nb + 4 * cid, ok ? g : 0);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r.x[q][k] = ok ? p[(size_t)k * a.B] : 0u;
+    for (int k = 0; k < 4; ++k) r.x[q][k] = ok ? p[4 * k] : 0u;
   }
 }
 

@@ -64,11 +64,12 @@ def rollout_forward(world, actions, action_body=None, ret_weights=None, dt=1e-2,
     nb, B, T = len(world.bodies), world.B, actions.shape[0]
     action_body = nb - 1 if action_body is None else int(action_body)
     w = _weights(world, ret_weights)
-    saved_dyn = torch.empty(T, nb, 6, B, device=world.device, dtype=torch.float32)
+    nblk = (B + 3) // 4  # the saved rows in env blocks of 4 (include/cotix_amd.h, trajectory())
+    saved_dyn = torch.empty(T, nblk, nb * 6, 4, device=world.device, dtype=torch.float32)
     saved_keys = torch.empty(T, B, 2, device=world.device, dtype=torch.int32)
     tw = _ffi.lib.cotix_rollout_tape_words(world.scene.handle)
     try:
-        tp = torch.empty(T, tw, B, device=world.device, dtype=torch.int32) if tape else None
+        tp = torch.empty(T, nblk, tw, 4, device=world.device, dtype=torch.int32) if tape else None
     except torch.OutOfMemoryError as e:
         raise torch.OutOfMemoryError(
             "rollout decision tape: %d x %d x %d u32 words (%.1f MiB) do not fit; tape=False runs the re-play "
@@ -82,6 +83,15 @@ def rollout_forward(world, actions, action_body=None, ret_weights=None, dt=1e-2,
     saved = dict(dyn=saved_dyn, keys=saved_keys, tape=tp, actions=actions, action_body=action_body, w=w,
                  dt=float(dt), stages=int(stages))
     return ret, saved
+
+
+def trajectory(saved, B):
+    """The saved states before each step as [T, n_bodies, 6, B] (a copy): the
+    library keeps them in env blocks of 4, [T][ceil(B/4)][n_bodies*6][4], so
+    that a wave of 4 envs saves and restores one contiguous run."""
+    sd = saved["dyn"]
+    T, nblk, nd, _ = sd.shape
+    return sd.permute(0, 2, 1, 3).reshape(T, nd // 6, 6, nblk * 4)[..., :B].contiguous()
 
 
 def rollout_backward(world, saved, want_dyn0=False, replay=False):

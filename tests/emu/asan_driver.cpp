@@ -66,8 +66,9 @@ int main(int argc, char** argv) {
     wr(o, keys);
     wr(o, err);
   } else {
-    std::vector<float> ret(B, 0.0f), sd((size_t)T * nb * 6 * B), ga((size_t)T * B * 2), gd((size_t)nb * 6 * B);
-    std::vector<uint32_t> sk((size_t)T * B * 2), tape((size_t)T * emu_rollout_tape_words(sc) * B, 0x7FBADBADu);
+    const size_t B4 = (size_t)(B + 3) / 4 * 4;  // saved rows in env blocks of 4 (cxk::row_at)
+    std::vector<float> ret(B, 0.0f), sd((size_t)T * nb * 6 * B4), ga((size_t)T * B * 2), gd((size_t)nb * 6 * B);
+    std::vector<uint32_t> sk((size_t)T * B * 2), tape((size_t)T * emu_rollout_tape_words(sc) * B4, 0x7FBADBADu);
     emu_rollout(sc, dyn.data(), keys.data(), err.data(), geom.data(), gs, B, T, 1e-2f, stages, act.data(), ab,
                 rw.data(), ret.data(), sd.data(), sk.data(), tape.data(), E);
     std::vector<float> ra(ga.size()), rd_(gd.size());

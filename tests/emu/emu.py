@@ -115,14 +115,16 @@ def step_ex(lib, h, dyn, keys, err, geom, gstride, n_steps, stages, nb, dt=1e-2,
 
 def rollout(lib, h, dyn, keys, err, geom, gstride, stages, actions, action_body, w, dt=1e-2, E=4):
     """Forward of the differentiable rollout; returns (ret [B], saved_dyn
-    [T,nb,6,B], saved_keys [T,B,2], tape [T,tape_words,B]); dyn/keys/err
-    advanced in place.  The tape is poisoned first (words the forward leaves
-    unwritten are never read)."""
+    [T,ceil(B/4),nb*6,4], saved_keys [T,B,2], tape [T,ceil(B/4),tape_words,4]
+    -- the library's env-block layout, cxk::row_at); dyn/keys/err advanced in
+    place.  The tape is poisoned first (words the forward leaves unwritten are
+    never read)."""
     T, B = actions.shape[0], dyn.shape[2]
+    nblk = (B + 3) // 4
     ret = np.zeros(B, np.float32)
-    sd = np.zeros((T,) + dyn.shape, np.float32)
+    sd = np.zeros((T, nblk, dyn.shape[0] * 6, 4), np.float32)
     sk = np.zeros((T, B, 2), np.uint32)
-    tape = np.full((T, lib.emu_rollout_tape_words(h), B), 0x7FBADBAD, np.uint32)
+    tape = np.full((T, nblk, lib.emu_rollout_tape_words(h), 4), 0x7FBADBAD, np.uint32)
     actions = np.ascontiguousarray(actions, np.float32)
     w = np.ascontiguousarray(w, np.float32)
     lib.emu_rollout(h, _p(dyn), _p(keys), _p(err), _p(geom), gstride, B, T, dt, stages, _p(actions), action_body,
@@ -133,9 +135,9 @@ def rollout(lib, h, dyn, keys, err, geom, gstride, stages, actions, action_body,
 def rollout_backward(lib, h, sd, sk, geom, gstride, stages, actions, action_body, w, dt=1e-2, E=4, tape=None):
     """The backward: from the forward's tape (MODE 4), or re-playing the
     forward (tape None, MODE 2)."""
-    T, B = actions.shape[0], sd.shape[3]
+    T, B = actions.shape[0], actions.shape[1]
     ga = np.zeros((T, B, 2), np.float32)
-    gd = np.zeros(sd.shape[1:], np.float32)
+    gd = np.zeros((sd.shape[2] // 6, 6, B), np.float32)
     actions = np.ascontiguousarray(actions, np.float32)
     w = np.ascontiguousarray(w, np.float32)
     rc = lib.emu_rollout_backward(h, _p(sd), _p(sk), _p(tape), _p(geom), gstride, B, T, dt, stages, _p(actions),

@@ -45,6 +45,38 @@ def _emu_run(emu, lib, case, E=4):
     return ret, ga, gd, dyn
 
 
+@pytest.mark.parametrize("E", [4, 1])
+def test_saved_rows_env_blocks(emu_lib, E):
+    """The forward saves the state before step t in env blocks of 4
+    (cxk::row_at); parallax_amd.trajectory unpacks them: equal to the state
+    after a t-step rollout, for a batch that is not a multiple of 4."""
+    import torch
+    from parallax_amd.rollout import trajectory
+    emu, lib = emu_lib
+    case = GC.box_case(5, 6, seed=11)
+    T = case["actions"].shape[0]
+    h, geom = emu.oracle_scene(lib, case["make"]())
+
+    def run(n):
+        dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
+        keys = np.array(case["keys"], np.uint32, copy=True)
+        err = np.zeros(dyn.shape[2], np.uint32)
+        out = emu.rollout(lib, h, dyn, keys, err, geom, 0, 1 | 4 | 16, case["actions"][:n], case["ab"], case["w"],
+                          E=E)
+        return dyn, out[1]
+
+    _, sd = run(T)
+    assert sd.shape == (T, 2, dyn_words(case), 4)
+    traj = trajectory({"dyn": torch.from_numpy(sd)}, 5).numpy()
+    for t in range(T):
+        want = run(t)[0] if t > 0 else np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
+        assert np.array_equal(traj[t].view(np.uint32), want.view(np.uint32)), t
+
+
+def dyn_words(case):
+    return case["S0"].shape[1] * 6
+
+
 def test_oracle_grad_vs_finite_differences():
     """The checker itself: torch VJP chain vs central differences of the
     faithful f32 oracle (box world, no discrete flips at eps=1e-2)."""

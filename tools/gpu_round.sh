@@ -37,6 +37,7 @@ for wl in "${ALL[@]}"; do
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT -d $P/pmc_stall -o run --output-format csv -- $B > /dev/null 2> $P/pmc4.err || { tail $P/pmc4.err; exit 6; }
   echo "profile $sc ok"
 done
-if [ "${PHASES:-1}" = 1 ]; then
-timeout -k 10 200 python tools/phase_prof.py > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --substeps 1 --launches 200 > $O/phase_k1.json && timeout -k 10 200 python tools/phase_prof.py --scenario lunar > $O/phase_lunar.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario robocup --launches 3 > $O/phase_grad_robocup.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario box --launches 3 > $O/phase_grad_box.json && timeout -k 10 200 python tools/phase_prof.py --mode grad --scenario lunar --launches 3 > $O/phase_grad_lunar.json && echo "phase ok"
+if [ "${PHASES:-1}" = 1 ]; then  # per-phase cycles (the tooling library of the same sources: COTIX_PHASE_PROF)
+L=parallax_amd/_lib/libcotix_amd_prof_tool.so
+timeout -k 10 200 python tools/phase_prof.py --lib $L > $O/phase_robocup.json && timeout -k 10 200 python tools/phase_prof.py --lib $L --scenario box > $O/phase_box.json && timeout -k 10 200 python tools/phase_prof.py --lib $L --substeps 1 --launches 200 > $O/phase_k1.json && timeout -k 10 200 python tools/phase_prof.py --lib $L --scenario lunar > $O/phase_lunar.json && timeout -k 10 200 python tools/phase_prof.py --lib $L --scenario lunar --warmup 40 --launches 5 > $O/phase_lunar_settled.json && timeout -k 10 200 python tools/phase_prof.py --lib $L --mode grad --scenario robocup --launches 3 > $O/phase_grad_robocup.json && timeout -k 10 200 python tools/phase_prof.py --lib $L --mode grad --scenario box --launches 3 > $O/phase_grad_box.json && timeout -k 10 200 python tools/phase_prof.py --lib $L --mode grad --scenario lunar --launches 3 > $O/phase_grad_lunar.json && echo "phase ok"
 fi

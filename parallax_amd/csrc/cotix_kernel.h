@@ -42,6 +42,7 @@ struct Stats {
   unsigned long long wave_steps, active_items, rounds, resolutions, f_items, b_items, draws, valid_draws, r1_left, lvl_env, lvl_wave, e1_slots;
   unsigned long long valid_cands, fit64;  // valid candidates of the active items; wave-steps where they fit 64 lanes
   unsigned long long bp_cand, bp_guard_fail;  // broadphase: pairs past the gap test; of them, not certified by bp_guard
+  unsigned long long epa_runs;                // polygon contacts whose GJK hit (EPA ran, not a self pair)
 };
 inline Stats g_stats{};
 #define CXK_STAT(f, v) (cxk::g_stats.f += (unsigned long long)(v))
@@ -1381,6 +1382,7 @@ CX_DEV void b_item(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane,
                        : (FNSET & FNS_AABB_POLY) == 0
                            ? convex_vs_polygon_pen_col<true>(A, Bs, np, !self, &ct.pen, col, WAVE, TAPE ? edge : nullptr)
                            : convex_vs_polygon_pen_col<false>(A, Bs, np, !self, &ct.pen, col, WAVE, TAPE ? edge : nullptr);
+      CXK_STAT(epa_runs, hit && !self ? 1 : 0);
       if (TAPE && a.tape != nullptr && hit && !self) {  // (a tape only with the polygon words, tape_words)
         const int o = 5 * c.nb + 4 * ci;
         const float ev[4] = {edge[0].x, edge[0].y, edge[1].x, edge[1].y};
@@ -1990,6 +1992,7 @@ CX_DEV void b_item_pair(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
                                      : gjk_epa_pair(S, h, na, nb, narrow_of(sc), !self, &ct.pen, col,
                                                     TAPE ? edge : nullptr);
   if (h != 0) return;
+  CXK_STAT(epa_runs, hit && !self ? 1 : 0);
   if (TAPE && a.tape != nullptr && hit && !self) {  // EPA's final edge to the tape (b_item's words)
     const int o = 5 * c.nb + 4 * ci;
     const float ev[4] = {edge[0].x, edge[0].y, edge[1].x, edge[1].y};
@@ -2906,11 +2909,32 @@ CX_DEV void ret_accum(const KArgs& a, const Ctx& c, Tile<EW> t, int e, const Ret
 // with 4 envs per wave and a whole block, one 16-byte store per row (a lane
 // each, the wave's n rows one contiguous run); else one word per (row, env)
 // lane
+// (dbg, tooling builds only -- the save-phase experiments of tools/gpu_fwd_exp.sh:
+// 1 stores zeros without the LDS reads, 2 reads without storing, 3 non-temporal stores)
 template <int EW>
-CX_DEV void rows_out(Tile<EW> t, int o, int n, uint32_t* dst, int rows, int step, int B, int env0, int lane) {
+CX_DEV void rows_out(Tile<EW> t, int o, int n, uint32_t* dst, int rows, int step, int B, int env0, int lane,
+                     int dbg = 0) {
   if (EW == 4 && env0 + 4 <= B) {
     U4* blk = reinterpret_cast<U4*>(dst + row_at(B, rows, step, 0, env0));
-    for (int r = lane; r < n; r += WAVE) blk[r] = U4{{t.w(o + r, 0), t.w(o + r, 1), t.w(o + r, 2), t.w(o + r, 3)}};
+    for (int r = lane; r < n; r += WAVE) {
+      if (dbg == 1) {
+        blk[r] = U4{{0u, 0u, 0u, 0u}};
+        continue;
+      }
+      const U4 w = U4{{t.w(o + r, 0), t.w(o + r, 1), t.w(o + r, 2), t.w(o + r, 3)}};
+#if defined(__HIP__)
+      if (dbg == 2) {
+        asm volatile("" ::"v"(w.v[0]), "v"(w.v[1]), "v"(w.v[2]), "v"(w.v[3]));
+        continue;
+      }
+      if (dbg == 3) {  // non-temporal (streaming) store
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(v4u{w.v[0], w.v[1], w.v[2], w.v[3]}, reinterpret_cast<v4u*>(blk + r));
+        continue;
+      }
+#endif
+      blk[r] = w;
+    }
   } else {
     for (int w = lane; w < n * EW; w += WAVE) {
       const int e = w % EW, r = w / EW;
@@ -2928,9 +2952,10 @@ CX_DEV void rows_out(Tile<EW> t, int o, int n, uint32_t* dst, int rows, int step
 // the next step's phase A resets the collider scratch, so the save runs in
 // the next step's save phase (ph_save) or, for the last step, after the loop
 template <int EW, bool TR>
-CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+CX_DEV void tape_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step, int dbg = 0) {
   // (polygon scenes: phase D stores their resolution words, phase B EPA's edges)
-  if (TR && tape_rec(c.sh)) rows_out<EW>(t, tape_stage(c), (5 + REC_W) * c.nb, a.tape, a.tw, step, a.B, env0, lane);
+  if (TR && tape_rec(c.sh))
+    rows_out<EW>(t, tape_stage(c), (5 + REC_W) * c.nb, a.tape, a.tw, step, a.B, env0, lane, dbg);
 }
 
 // TREC: the rollout forward with a tape records the resolutions (as REC) for
@@ -3209,8 +3234,8 @@ CX_DEV void ph_store(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lan
       a.keys[2 * (size_t)g] = t.w(c.L.key, e);
       a.keys[2 * (size_t)g + 1] = t.w(c.L.key + 1, e);
       a.err[g] = t.w(c.L.err, e);
-      if (a.resets) a.resets[g] = t.w(c.L.nres, e);
-      if (ROLL) a.ret[g] += t.f(c.L.ret, e);
+      if (a.resets && !ROLL) a.resets[g] = t.w(c.L.nres, e);
+      if (ROLL) a.ret[g] = t.f(c.L.nres, e) + t.f(c.L.ret, e);  // (the incoming return, ph_load_fwd)
       if (EVAL && a.judge.on) {
         if (a.reward) a.reward[g] = t.f(c.L.jr, e);
         if (a.finished) a.finished[g] = t.w(c.L.jfin, e);
@@ -3237,10 +3262,14 @@ constexpr int RQ = (MAXB * 6 * 8 + 63) / 64;  // words per lane: nb * 6 * EW ove
 // (+ the tape words of the step before it, tape_save)
 template <int EW, bool TR>
 CX_DEV void ph_save(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int step) {
+  if (CXK_SKIP(a, 8192)) step = step > 0 ? 1 : 0;  // (tooling, timing only: every step's saves to one slot)
+  const int dbg = CXK_SKIP(a, 512) ? 1 : CXK_SKIP(a, 1024) ? 2 : CXK_SKIP(a, 2048) ? 3 : 0;  // tooling only (rows_out)
   if (a.tape != nullptr && step > 0 && (a.stages & COTIX_STAGE_COLLIDER) && !CXK_SKIP(a, 128))
-    tape_save<EW, TR>(a, c, t, env0, lane, step - 1);
+    tape_save<EW, TR>(a, c, t, env0, lane, step - 1, dbg);
   if (CXK_SKIP(a, 256)) return;
-  rows_out<EW>(t, c.L.dyn, c.nb * 6, reinterpret_cast<uint32_t*>(a.save_dyn), c.nb * 6, step, a.B, env0, lane);
+  rows_out<EW>(t, c.L.dyn, c.nb * 6, reinterpret_cast<uint32_t*>(a.save_dyn), c.nb * 6, step, a.B, env0, lane,
+               dbg);
+  if (CXK_SKIP(a, 4096)) return;  // (tooling: the save phase without the key pair)
   for (int e = lane; e < EW; e += WAVE) {
     int g = env0 + e;
     if (g < a.B) {
@@ -3972,11 +4001,19 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
 // on), both compiled out of the plain step kernel
 // the forward programs' load phase (the kernel may run it before its
 // workgroup barrier: it touches only the wave's own tile)
+// ROLL: the incoming return is read with the state (ph_store adds the launch's
+// sum to it without a read: a read at the end waited behind every store in
+// flight, ~15 us per launch); it lives in the restart-counter word, which the
+// rollout programs (no restarts, no counter) do not use
 template <int EW, bool ROLL, bool EVAL = false>
 CX_DEV void ph_load_fwd(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int l) {
+  const float r0 = (ROLL && l < EW && env0 + l < a.B) ? a.ret[env0 + l] : 0.0f;
   ph_load<EW, EVAL>(a, c, t, env0, l);
   if (ROLL) {
-    for (int e = l; e < EW; e += WAVE) t.f(c.L.ret, e) = 0.0f;
+    for (int e = l; e < EW; e += WAVE) {
+      t.f(c.L.ret, e) = 0.0f;
+      t.f(c.L.nres, e) = r0;
+    }
     stage_ret_terms<EW>(a, c, t, l);
   }
 }

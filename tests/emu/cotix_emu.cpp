@@ -414,8 +414,9 @@ extern "C" int emu_stats(unsigned long long* out) {
   out[13] = cxk::g_stats.fit64;
   out[14] = cxk::g_stats.bp_cand;
   out[15] = cxk::g_stats.bp_guard_fail;
+  out[16] = cxk::g_stats.epa_runs;
   cxk::g_stats = cxk::Stats{};
-  return 16;
+  return 17;
 }
 #endif
 

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--ew", type=int, default=4)
     ap.add_argument("--broadphase", action="store_true", help="COTIX_STAGE_BROADPHASE (polygon scenes)")
     ap.add_argument("--drop", type=float, default=0.0, help="lunar: lower the lander and legs by this much (contact)")
+    ap.add_argument("--settle", type=int, default=0, help="driver steps run first on the C port (lunar settles by ~2560)")
     a = ap.parse_args()
     src = os.path.join(ROOT, "tests", "emu", "cotix_emu.cpp")
     subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
@@ -64,7 +65,12 @@ def main():
     keys = np.ascontiguousarray(np.array(prng.split(prng.PRNGKey(3), B), np.uint32))
     dyn_reset = dyn.copy()
     err = np.zeros(B, np.uint32)
-    out = (ctypes.c_ulonglong * 16)()
+    if a.settle:  # the settled regime: advance on the C port (same bits), count the next steps only
+        from cotix_oracle import cport
+        src_bodies = P.robocup_bodies() if a.scenario == "robocup" else P.lunar_lander_bodies(prng.split(prng.PRNGKey(0), B)[0])
+        sc = cport.Scene(cport.load(), src_bodies)
+        sc.step(dyn, keys, err, a.settle, stages, geom=None if gstride == 0 else geom, dyn_reset=dyn_reset, nthreads=8)
+    out = (ctypes.c_ulonglong * 17)()
     lib.emu_stats(out)
     emu.step(lib, h, dyn, keys, err, geom, gstride, a.steps, stages, E=a.ew, dyn_reset=dyn_reset)
     lib.emu_stats(out)
@@ -77,7 +83,8 @@ def main():
            "resolution_levels_per_env_step": out[9] / (B * a.steps), "resolution_levels_per_wave_step": out[10] / ws,
            "sequential_slots_per_wave_step": out[11] / ws,
            "valid_candidates_of_active_items_per_wave_step": out[12] / ws, "fit64_frac": out[13] / ws,
-           "bp_candidates_per_wave_step": out[14] / ws, "bp_guard_fail_frac": out[15] / max(out[14], 1)})
+           "bp_candidates_per_wave_step": out[14] / ws, "bp_guard_fail_frac": out[15] / max(out[14], 1),
+           "epa_runs_per_wave_step": out[16] / ws})
 
 
 if __name__ == "__main__":

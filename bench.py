@@ -88,8 +88,17 @@ def parse():
                     help="the jax.random threefry layout of the collider (cotix_params; JAX 0.4.x: legacy, "
                          "JAX >= 0.5: partitionable)")
     ap.add_argument("--lib", default=None, help="another build of libcotix_amd.so (A/B tooling); recorded in config")
+    ap.add_argument("--key-helper", type=int, default=1, choices=[0, 1],
+                    help="step launches of more than 16 steps with the key-window helper wave (the library "
+                         "default, 1) or the step wave alone (0); recorded in config")
+    ap.add_argument("--split-bwd", type=int, default=1, choices=[0, 1],
+                    help="--mode grad: the tape backward at two waves per env group (the library default, 1) "
+                         "or one (0); recorded in config")
     a = ap.parse_args()
     refuse_overrides()
+    # the two-wave forms' library switches (read at the first launch)
+    os.environ["COTIX_KEY_HELPER"] = str(a.key_helper)
+    os.environ["COTIX_SPLIT_BWD"] = str(a.split_bwd)
     if a.lib:  # read by parallax_amd._ffi at import
         os.environ["COTIX_AMD_LIB"] = os.path.abspath(a.lib)
     return a
@@ -98,6 +107,14 @@ def parse():
 # environment variables the bench itself reads; any other COTIX_* variable
 # could select another library or kernel behaviour behind the line's back
 BENCH_ENV_OK = {"COTIX_BENCH_FORCE_DIST"}
+
+
+def two_wave_forms():
+    """The two-wave kernel forms this run allowed (--key-helper, --split-bwd):
+    the key-window helper wave of step launches with more than one key
+    window, the split tape backward of the analytic scenes."""
+    return {"key_helper": int(os.environ.get("COTIX_KEY_HELPER", "1")),
+            "split_bwd": int(os.environ.get("COTIX_SPLIT_BWD", "1"))}
 
 
 def refuse_overrides():
@@ -358,7 +375,7 @@ def sub_step(pa, dev, name, B, substeps, steps, warmup, key=None, layout="legacy
     out = {"workload": WORKLOAD[name] % B, "substeps_per_launch": substeps, "launches": steps,
            "value": B * substeps * steps / wall, "unit": "env-steps/s", "launch_ms": ev_ms,
            "hbm_GBs": bytes_per_env(name, len(scen.bodies)) * B / (ev_ms * 1e-3) / 1e9, "prng_layout": layout,
-           "kernel_variant": scen.world.scene.variant()}
+           "kernel_variant": dict(scen.world.scene.variant(), **two_wave_forms())}
     v = valu_roofline(key, B, substeps, ev_ms, warmup if name == "lunar" else None, layout)
     if v is not None:  # the committed PMC pass of this workload (profiles/latest_pmc_<key>.json)
         out["valu"] = {"achieved": v["valu_instr_per_launch"] / (ev_ms * 1e-3) / 1e9,
@@ -568,7 +585,7 @@ def main():
             "autoreset_on_error": True,
             "library": library_build(),
             "library_path": a.lib or "parallax_amd/_lib/libcotix_amd.so",
-            "kernel_variant": scen.world.scene.variant(),
+            "kernel_variant": dict(scen.world.scene.variant(), **two_wave_forms()),
             "prng_layout": a.prng_layout,
             "episode_restarts": resets,
             "restarts_per_env_step": resets / (B * a.substeps * (a.steps + a.warmup)),
@@ -772,7 +789,7 @@ def main_grad(a):
             "bwd_ms": r["bwd_ms"],
             "finite_grad_env_fraction": r["finite"],
             "library": library_build(),
-            "kernel_variant": r["variant"],
+            "kernel_variant": dict(r["variant"], **two_wave_forms()),
             "parallelism": "dp%d (independent env shards)" % world_size,
         },
         "roofline": {

@@ -2539,7 +2539,7 @@ CX_DEV void e0_item(const Ctx& c, Tile<EW> t, int e, int i, int j, int cid, bool
 // one (body i, env) item of phase D; NB > 0: the body count at compile time
 // (unrolled loads and selects), NB == 0: any count up to MAXB
 template <int EW, bool PRE, int NB, bool RCP>
-CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, bool stage = false, uint32_t* tp = nullptr) {
+CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int kso, bool stage = false, uint32_t* tp = nullptr) {
   using namespace cx;
   constexpr int MB = NB > 0 ? NB : MAXB;
   const int nb = NB > 0 ? NB : c.nb, nt = c.nt;
@@ -2568,7 +2568,7 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, bool stage 
       cumsum_n(p, nb, cs);
     float u;
     if (PRE) {
-      u = t.f(L.kw + slot * L.kww + 2 + 2 * nt + i, e);
+      u = t.f(kso + 2 + 2 * nt + i, e);  // the window slot's choice uniforms
     } else {
       const int so = nt > 0 ? L.skt + 2 * (nt - 1) : L.sk0;
       const bool part = c.sh.prng != 0;
@@ -2597,7 +2597,7 @@ CX_DEV void d_item(const Ctx& c, Tile<EW> t, int e, int i, int slot, bool stage 
 // E1's resolution records (tape_stage), so that the save phase copies them
 // out as whole rows instead of chasing partner -> cell -> contact
 template <int EW, bool PRE = false, bool TAPE = false>
-CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int slot = 0, int step = 0) {
+CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, int kso = 0, int step = 0) {
   const int nb = c.nb;
   for (int w = lane; w < nb * EW; w += WAVE) {
     const int e = w % EW, i = w / EW;
@@ -2605,13 +2605,13 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
     const bool stage = TAPE && a.tape != nullptr && tape_rec(c.sh);
     uint32_t* tp = TAPE && a.tape != nullptr && !stage ? a.tape + row_at(a.B, a.tw, step, 5 * i, env0 + e) : nullptr;
     if (c.sh.rcp_all) {
-      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, slot, stage, tp);
-      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, slot, stage, tp);
-      else d_item<EW, PRE, 0, true>(c, t, e, i, slot, stage, tp);
+      if (nb == 5) d_item<EW, PRE, 5, true>(c, t, e, i, kso, stage, tp);
+      else if (nb == 4) d_item<EW, PRE, 4, true>(c, t, e, i, kso, stage, tp);
+      else d_item<EW, PRE, 0, true>(c, t, e, i, kso, stage, tp);
     } else {
-      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, slot, stage, tp);
-      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, slot, stage, tp);
-      else d_item<EW, PRE, 0, false>(c, t, e, i, slot, stage, tp);
+      if (nb == 5) d_item<EW, PRE, 5, false>(c, t, e, i, kso, stage, tp);
+      else if (nb == 4) d_item<EW, PRE, 4, false>(c, t, e, i, kso, stage, tp);
+      else d_item<EW, PRE, 0, false>(c, t, e, i, kso, stage, tp);
     }
   }
 }
@@ -2625,7 +2625,7 @@ CX_DEV void ph_D(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane, i
 // (rows_tape), and phase D reads them there (ph_D_tape STAGED)
 CX_HD int rows_tape(const Ctx& c) { return c.L.kw; }
 template <int EW>
-CX_DEV bool rows_restore(const KArgs& a, const Ctx& c) {
+CX_HD bool rows_restore(const KArgs& a, const Ctx& c) {
   return EW == 4 && (a.B & 3) == 0 && tape_rec(c.sh) && (a.stages & COTIX_STAGE_COLLIDER) && 18 * c.nb <= 2 * WAVE &&
          (5 + REC_W) * c.nb <= KWIN * c.L.kww;
 }
@@ -3629,17 +3629,19 @@ CX_DEV void ph_GE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
 // selects, no scratch) -- the resolutions' LDS reads are then independent of
 // the previous resolution's writes, and the Euler / return terms run on
 // registers.  Every operation and its order are ph_G's: the same bits.
+// g_chain: the step's reverse on the adjoints g held by the caller (g_regs
+// reads them from and writes them to the tile's adj words; the split backward's
+// consumer wave carries them in registers from step to step)
 template <int EW, int NB>
-CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step, GradOut* go = nullptr) {
+CX_DEV void g_chain(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step, float (&g)[NB][6],
+                    GradOut* go = nullptr) {
   using namespace cx;
   const SceneHdr& sc = c.sh;
   const Lay& L = c.L;
-  float g[NB][6], px[NB], py[NB], an[NB];
+  float px[NB], py[NB], an[NB];
   uint32_t fl[NB], jj[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) g[b][k] = t.f(L.adj + 6 * b + k, e);
     px[b] = t.f(L.dyn + 6 * b, e);
     py[b] = t.f(L.dyn + 6 * b + 1, e);
     an[b] = t.f(L.dyn + 6 * b + 4, e);
@@ -3731,9 +3733,20 @@ CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, in
     if (step > 0)
 #pragma unroll
       for (int k = 0; k < 6; ++k) g[b][k] = g[b][k] + t.f(L.rst + 6 * b + k, e);  // ret_w (staged)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) t.f(L.adj + 6 * b + k, e) = g[b][k];
   }
+}
+template <int EW, int NB>
+CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step, GradOut* go = nullptr) {
+  float g[NB][6];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) g[b][k] = t.f(c.L.adj + 6 * b + k, e);
+  g_chain<EW, NB>(a, c, t, env0, e, step, g, go);
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) t.f(c.L.adj + 6 * b + k, e) = g[b][k];
 }
 
 template <int EW, int FNSET = FNS_ANALYTIC>
@@ -3993,7 +4006,7 @@ CX_DEV void collider_phases(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, 
       run(PH_C3, [&](int l) { ph_C3<EW>(c, t, l, par); });
     }
   }
-  if (!CXK_SKIP(a, 8)) run(PH_D, [&](int l) { ph_D<EW, PRE, TAPE>(a, c, t, env0, l, slot, step); });
+  if (!CXK_SKIP(a, 8)) run(PH_D, [&](int l) { ph_D<EW, PRE, TAPE>(a, c, t, env0, l, kso, step); });
 }
 
 // forward: n_steps fused steps; ROLL adds the trajectory save and the return
@@ -4017,9 +4030,89 @@ CX_DEV void ph_load_fwd(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int 
     stage_ret_terms<EW>(a, c, t, l);
   }
 }
-template <int EW, int FNSET, bool ROLL, bool EVAL = false, bool SDEFER = false, class R = void>
-CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, bool loaded = false) {
+// ---------------------------------------------------------------------------
+// The key-window helper (the step program at two waves per env group).  Phase
+// K's window -- the driver key chain, the per-type keys and every body's
+// choice uniform for 16 steps -- depends on the env's launch key only, never
+// on the physics (the chain k_{s+1} = split(k_s)[0] is what phase E stores as
+// the key; restarts keep it).  So a helper wave can compute window w + 1 while
+// the env group's step wave runs the steps of window w: the step wave computes
+// window 0 itself, then at each later window start waits at one workgroup
+// barrier and reads the window from one of two buffers -- its own tile's key
+// window (even windows) or the helper's (odd), `kwalt` words from it in the
+// tile's [word][env] addressing.  The same K0 / K1 / K2 code writes the same
+// words (K0 with the chain key carried in the helper lane's registers): the
+// same bits (tests/test_emu_cpu.py runs it on the host emulation, the
+// helper's window computed at the step wave's barrier).
+// ---------------------------------------------------------------------------
+struct NoKeyHelp {
+  static constexpr bool on = false;
+  int kwalt = 0;
+  CX_MF void bar() const {}
+};
+template <int EW>
+struct KeyHelper {
+  Tile<EW> tm;  // the step wave's tile: window buffer 0 is its key window
+  Tile<EW> th;  // a view whose key window is buffer 1 (th.u = buffer 1 - L.kw * EW)
+  int env0 = 0;
+  int w = 0;  // windows produced (window 0 is the step wave's)
+  cx::key2 k = cx::key2{0u, 0u};  // this lane's (env, half) chain key at the next window
+};
+// K0 on the key in the lane's registers: items (env, half) on lanes < 2 EW,
+// split_at_pair as ph_K0; write: the window's sk0 words (else only advance)
+template <int EW>
+CX_DEV void k0_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int lane, int n, cx::key2& k, bool write) {
+  using namespace cx;
+  const Lay& L = c.L;
+  for (int w = lane; w < 2 * EW; w += WAVE) {
+    const int e = w >> 1, h = w & 1;
+    for (int s = 0; s < n; ++s) {
+      const key2 s0 = split_at_pair(k, 2u, 0u, h, c.sh.prng != 0);
+      if (write && h == 0) {
+        t.w(L.kw + s * L.kww, e) = s0.a;
+        t.w(L.kw + s * L.kww + 1, e) = s0.b;
+      }
+      if (a.stages & COTIX_STAGE_ADVANCE_KEY) k = s0;
+    }
+  }
+}
+// the helper's start: the env's launch key (the input keys, as ph_load reads
+// them), advanced past window 0
+template <int EW, class R>
+CX_DEV void key_helper_init(const KArgs& a, const Ctx& c, KeyHelper<EW>& h, const R& run) {
+  run(PH_K, [&](int l) {
+    const int e = l >> 1, g = h.env0 + e;
+    if (l < 2 * EW && g < a.B) h.k = cx::key2{a.keys[2 * (size_t)g], a.keys[2 * (size_t)g + 1]};
+    k0_regs<EW>(a, c, h.tm, l, a.n_steps < KWIN ? a.n_steps : KWIN, h.k, false);
+  });
+}
+// window h.w + 1 (steps 16 (w + 1) ..) into buffer (w + 1) & 1
+template <int EW, class R>
+CX_DEV void key_helper_next(const KArgs& a, const Ctx& c, KeyHelper<EW>& h, const R& run) {
+  const int w = ++h.w, step0 = w * KWIN, n = a.n_steps - step0 < KWIN ? a.n_steps - step0 : KWIN;
+  const Tile<EW> t = (w & 1) ? h.th : h.tm;
+  run(PH_K, [&](int l) { k0_regs<EW>(a, c, t, l, n, h.k, true); });
+  run(PH_K, [&](int l) { ph_K1<EW>(c, t, l, n); });
+  if (a.stages & COTIX_STAGE_COLLIDER) run(PH_K, [&](int l) { ph_K2<EW>(c, t, l, n); });
+}
+// the barriers of a launch with a helper: one per window after the first
+CX_HD int key_helper_windows(const KArgs& a) { return a.n_steps > KWIN ? (a.n_steps - 1) / KWIN : 0; }
+// a step wave's LDS region with a helper (tile + scratch, a multiple of EW
+// words: the buffer offset kwalt is whole tile words) and the workgroup's LDS
+// bytes (tables, wpb regions, wpb helper window buffers)
+template <int EW>
+CX_HD int help_region_words(const Ctx& c) { return (c.L.S * EW + c.W.words + EW - 1) / EW * EW; }
+template <int EW>
+CX_HD size_t help_lds_bytes(const SceneHdr& s, int wpb) {
+  const Ctx c = make_ctx<EW>(s);
+  return 4 * ((size_t)s.nhot + (size_t)wpb * (help_region_words<EW>(c) + KWIN * c.L.kww * EW));
+}
+
+template <int EW, int FNSET, bool ROLL, bool EVAL = false, bool SDEFER = false, class R = void, class H = NoKeyHelp>
+CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, bool loaded = false,
+                     const H& help = H{}) {
   static_assert(!(ROLL && EVAL), "the rollout has no judge");
+  static_assert(!(H::on && (ROLL || EVAL)), "the key helper runs the step program only");
   if (!loaded) run(PH_LOAD, [&](int l) { ph_load_fwd<EW, ROLL, EVAL>(a, c, t, env0, l); });
   const bool keys = keys_on(a);
   if (EVAL && a.judge.on) {  // the first NFE's start
@@ -4075,7 +4168,9 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
     if (awin && step % AWIN == 0) run(PH_K, [&](int l) { act_window_fill<EW>(a, c, t, env0, l, step); });
     if (ROLL) run(PH_SAVE, [&](int l) { ph_save<EW, FNSET == FNS_ANALYTIC>(a, c, t, env0, l, step); });
     const int slot = step % KWIN;
-    if (keys && slot == 0 && !(step == 0 && k_in_prologue(a))) {
+    if (H::on && keys && slot == 0 && step > 0) {
+      help.bar();  // the helper's window (key_helper_next)
+    } else if (keys && slot == 0 && !(step == 0 && k_in_prologue(a))) {
       const int n = a.n_steps - step < KWIN ? a.n_steps - step : KWIN;
       if (n == 1) {  // (a launch's last window: the keys from the tile)
         run(PH_K, [&](int l) {
@@ -4088,7 +4183,8 @@ CX_DEV void run_wave(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R
         if (a.stages & COTIX_STAGE_COLLIDER) run(PH_K, [&](int l) { ph_K2<EW>(c, t, l, n); });
       }
     }
-    const int kso = c.L.kw + slot * c.L.kww;  // this step's sk0, skt in the key window
+    // this step's sk0, skt in the key window (with a helper: odd windows in its buffer)
+    const int kso = c.L.kw + (H::on && ((step / KWIN) & 1) ? help.kwalt : 0) + slot * c.L.kww;
     // phases A, T, B as one (circle / AABB scenes whose contact items fit the
     // phase's ABQ prefetched chunks; uniform)
     if (bconst) {  // phase A, then B from the launch-constant item words (no phase T)
@@ -4263,6 +4359,121 @@ CX_DEV void run_wave_backward_tape(const KArgs& a, const Ctx& c, Tile<EW> t, int
     if (a.grad_action != nullptr) grad_action_flush(a, env0, l, EW, go);  // step 0's
     ph_adj_store<EW>(a, c, t, env0, l);
   });
+}
+
+// ---------------------------------------------------------------------------
+// The tape backward at two waves per env group (split backward).  MODE 4's
+// step is an adjoint-independent part -- the restore of the saved state and
+// tape rows, Euler, the world parts, phase D from the tape -- and the reverse
+// chain G, which reads only the tile that part leaves and the adjoints.  G is
+// a chain of dependent LDS reads and IEEE divisions on 4 of 64 lanes (VALU
+// active ~27 % of the backward's wave cycles at one wave per SIMD), so here a
+// producer wave runs the first part of step s into one tile of the group while
+// its consumer wave runs G of step s + 1 on the other tile; the two share a
+// SIMD (waves w and w + WPB of the workgroup) and G's latency overlaps the
+// producer's phases instead of following them.  One workgroup barrier per step
+// hands the filled tile to the consumer and the read one back to the
+// producer; the consumer carries the adjoints in registers (g_chain).  Every
+// phase is MODE 4's own code on the same tile words -- the same bits
+// (tests/test_grad_cpu.py runs this program on the host emulation, producer
+// then consumer per step, against run_wave_backward_tape).
+// Scenes: analytic, the row restore (rows_restore), G in registers (5 or 7
+// bodies: RoboCup, the box world); the launcher also needs the two tiles per
+// group to fit the LDS (cotix_step.hip).
+template <int EW>
+CX_HD bool split_bwd_ok(const KArgs& a, const Ctx& c) {
+#ifdef COTIX_NO_GREGS
+  (void)a;
+  (void)c;
+  return false;
+#else
+  return rows_restore<EW>(a, c) && (c.nb == 5 || c.nb == 7) && c.sh.poly == 0;
+#endif
+}
+// the producer's prefetch registers of one step (two sets: the loop is
+// unrolled by two, as run_wave_backward_tape's)
+struct SplitPre {
+  RowRegs rw;
+  ActRegs an;
+};
+template <int EW>
+CX_DEV void split_prefetch(const KArgs& a, const Ctx& c, int env0, int l, int s, bool apf, SplitPre& p) {
+  restore_rows_fetch<EW>(a, c, env0, l, s, p.rw);
+  if (apf) act_fetch<EW>(a, c, env0, l, s, p.an);
+}
+// the producer's part of step `step` on tile t: restore, Euler, world parts, D
+template <int EW, class R>
+CX_DEV void split_produce(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, const R& run, int step, SplitPre& cur,
+                          bool apf) {
+  ActRegs ac;
+  run(PH_RESTORE, [&](int l) {
+    restore_rows_apply<EW>(c, t, l, cur.rw);
+    ac = cur.an;
+    if (step > 1) split_prefetch<EW>(a, c, env0, l, step - 2, apf, cur);
+  });
+  run(PH_A, [&](int l) {  // Euler (+ gravity, + action)
+    if (a.stages & (COTIX_STAGE_EULER | COTIX_STAGE_GRAVITY))
+      for (int w = l; w < c.nb * EW; w += WAVE) {
+        const int e = w % EW, b = w / EW;
+        if (env0 + e < a.B) euler_item<EW>(a, c, t, env0, e, b, step, apf, ac);
+      }
+  });
+  transform_phases<EW, FNS_ANALYTIC>(a, c, t, env0, run);
+  const TapeRegs none{};
+  run(PH_D, [&](int l) { ph_D_tape<EW, true, true>(a, c, t, env0, l, none); });
+}
+// role: 1 producer, 2 consumer (the GPU's two waves of a group), 3 both in
+// turn (the host emulation: a step's producer part, then the consumer's);
+// bar(): the workgroup barrier (nothing on the host)
+template <int EW, int NB, class R, class BAR>
+CX_DEV void run_backward_split(const KArgs& a, const Ctx& c, Tile<EW> t0, Tile<EW> t1, int env0, const R& run,
+                               int role, const BAR& bar) {
+  const bool prod = (role & 1) != 0, cons = (role & 2) != 0, live = env0 < a.B;
+  const int n = a.n_steps;
+  const bool apf = act_prefetch<EW>(a, c);
+  SplitPre p0, p1;
+  float g[NB][6];
+  if (prod && live)
+    run(PH_ADJ, [&](int l) {
+      for (int q = 0; q < 2; ++q) {
+        const Tile<EW> t = q ? t1 : t0;
+        ph_geo<EW>(a, c, t, env0, l);
+        stage_ret_w<EW>(a, c, t, l);
+        for (int e = l; e < EW; e += WAVE) t.w(c.L.pcv, e) = 0u;  // phase T's pose entries
+      }
+      if (n > 0) split_prefetch<EW>(a, c, env0, l, n - 1, apf, p0);
+      if (n > 1) split_prefetch<EW>(a, c, env0, l, n - 2, apf, p1);
+    });
+  if (cons)  // d ret / d state_T (ph_adj_init's words)
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g[b][k] = a.ret_w[6 * b + k];
+  bar();
+  // iteration k: the producer fills tile k & 1 with step n-1-k, the consumer
+  // reverses step n-k on tile (k-1) & 1, which the producer filled at k-1
+  auto iter = [&](int k, Tile<EW> tp, Tile<EW> tc, SplitPre& pre) CXK_INLINE_LAMBDA {
+    if (prod && live && k < n) split_produce<EW>(a, c, tp, env0, run, n - 1 - k, pre, apf);
+    if (cons && live && k >= 1)
+      run(PH_G, [&](int l) CXK_INLINE_LAMBDA {
+        if (l < EW && env0 + l < a.B) g_chain<EW, NB>(a, c, tc, env0, l, n - k, g);
+      });
+    if (k < n) bar();
+  };
+  for (int k = 0; k <= n; k += 2) {
+    iter(k, t0, t1, p0);
+    if (k + 1 <= n) iter(k + 1, t1, t0, p1);
+  }
+  if (cons && live)
+    run(PH_ADJ, [&](int l) {
+      if (l < EW)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int k = 0; k < 6; ++k) t0.f(c.L.adj + 6 * b + k, l) = g[b][k];
+      cxk::lockstep();
+      ph_adj_store<EW>(a, c, t0, env0, l);
+    });
 }
 
 // backward: steps n_steps-1 .. 0, each re-played from the saved state (so

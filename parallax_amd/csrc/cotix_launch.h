@@ -21,4 +21,14 @@ hipError_t launch_step_ew1(const cxk::KArgs& ka, int fs, int mode, size_t lds, h
 hipError_t launch_step_ew2(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec, int wpb);
 hipError_t launch_step_ew4(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec, int wpb);
 hipError_t launch_step_ew8(const cxk::KArgs& ka, int fs, int mode, size_t lds, hipStream_t st, int spec, int wpb);
+// the tape backward at two waves per env group (EW = 4, analytic scenes of 5
+// or 7 bodies; cxk::run_backward_split), workgroups of 2 * WPB waves with
+// `lds` = cxk::lds_bytes(header, 2 * WPB, 4): 0 launched, 1 not compiled for
+// this scene (the caller launches MODE 4)
+int launch_bwd_split(const cxk::KArgs& ka, int spec, size_t lds, hipStream_t st);
+// the step program (mode 0) with a key-window helper wave per env group
+// (EW = 4, RoboCup's specialization; cxk::KeyHelper), workgroups of 2 * WPB
+// waves with `lds` = cxk::help_lds_bytes<4>(header, WPB): 0 launched, 1 not
+// compiled for this scene (the caller launches step_kernel)
+int launch_step_help(const cxk::KArgs& ka, int spec, size_t lds, hipStream_t st);
 }  // namespace cxl

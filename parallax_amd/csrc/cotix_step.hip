@@ -393,6 +393,24 @@ static int check_step_args(const cotix_scene* scene, const float* dyn, const uin
   return 0;
 }
 
+// the split tape backward is the default; COTIX_SPLIT_BWD=0 launches MODE 4
+// at one wave per env group instead (A/B measurements; the same bits)
+static bool split_bwd_enabled() {
+  static const int on = [] {
+    const char* v = getenv("COTIX_SPLIT_BWD");
+    return v == nullptr || atoi(v) != 0 ? 1 : 0;
+  }();
+  return on != 0;
+}
+// the key-window helper is the default for the step launches it applies to;
+// COTIX_KEY_HELPER=0 launches step_kernel alone (A/B measurements; the same bits)
+static bool key_helper_enabled() {
+  static const int on = [] {
+    const char* v = getenv("COTIX_KEY_HELPER");
+    return v == nullptr || atoi(v) != 0 ? 1 : 0;
+  }();
+  return on != 0;
+}
 // launch the fused step kernel (mode 0 step, 1 rollout forward, 2 backward re-play, 3 eval with a judge/control)
 static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_stream_t stream) {
   if (scene_upload(scene)) return -1;
@@ -416,6 +434,23 @@ static int launch(cotix_scene* scene, const cxk::KArgs& ka0, int mode, cotix_str
   // scene specialization (compile-time dimensions; reference scenes, whose
   // tiles always fit WPB to a workgroup)
   const int spec = wpb == cxl::WPB ? scene_spec(scene) : cxk::SPEC_GENERIC;
+  // the tape backward at two waves per env group where the scene allows it
+  // and two tiles per group fit (cxk::run_backward_split; the same bits)
+  if (mode == 4 && EW == 4 && wpb == cxl::WPB && split_bwd_enabled() &&
+      cxk::launch_fnset(fs, mode) == cxk::FNS_ANALYTIC &&
+      cxk::split_bwd_ok<4>(ka, cxk::make_ctx<4>(scene->host)) &&
+      scene_lds_w(scene, 4, 2 * cxl::WPB) <= LDS_CAP) {
+    const int r = cxl::launch_bwd_split(ka, spec, scene_lds_w(scene, 4, 2 * cxl::WPB), st);
+    if (r == 0) return hip_check(hipGetLastError(), "bwd_split_kernel launch");
+  }
+  // the step program with a key-window helper wave per env group where the
+  // launch has more than one key window (cxk::KeyHelper; the same bits)
+  if (mode == 0 && EW == 4 && wpb == cxl::WPB && ka.n_steps > cxk::KWIN && key_helper_enabled() &&
+      cxk::launch_fnset(fs, mode) == cxk::FNS_ANALYTIC &&
+      cxk::help_lds_bytes<4>(scene->host, cxl::WPB) <= LDS_CAP) {
+    const int r = cxl::launch_step_help(ka, spec, cxk::help_lds_bytes<4>(scene->host, cxl::WPB), st);
+    if (r == 0) return hip_check(hipGetLastError(), "step_help_kernel launch");
+  }
   hipError_t e;
 #ifdef COTIX_EW4_ONLY  // tooling builds (phase profile, ISA markers): the default tiling only
   e = cxl::launch_step_ew4(ka, fs, mode, lds, st, spec, wpb);

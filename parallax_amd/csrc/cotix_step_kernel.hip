@@ -164,7 +164,152 @@ __global__ __launch_bounds__(WPB * 64) void step_kernel(cxk::KArgs a) {
 #endif
 }
 
+#if COTIX_EW == 4
+// the tape backward at two waves per env group (cxk::run_backward_split):
+// waves g and g + WPB of the workgroup are env group g's producer and
+// consumer (one SIMD each pair), the group's two tiles are the LDS regions of
+// those two waves.  The workgroup barrier waits for LDS only: the producer's
+// prefetch reads (two steps ahead) and the consumer's gradient stores stay in
+// flight across it.
+CX_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+template <int NB, int SPEC>
+__global__ __launch_bounds__(2 * WPB * 64) void bwd_split_kernel(cxk::KArgs a) {
+  constexpr int EW = 4;
+  extern __shared__ uint32_t lds[];
+  const SceneDev* sc = a.sc;
+  const cxk::SceneHdr sh = cxk::spec_hdr<SPEC>(a.sh);
+  const int nhot = sh.nhot;
+  constexpr int HC = 8, NT = 2 * WPB * 64;
+  for (int base = 0; base < nhot; base += HC * NT) {
+    uint32_t r[HC];
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      const int i = base + k * NT + (int)threadIdx.x;
+      r[k] = i < nhot ? sc->hot[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      const int i = base + k * NT + (int)threadIdx.x;
+      if (i < nhot) lds[i] = r[k];
+    }
+  }
+  const cxk::Ctx c = cxk::make_ctx<EW>(sh);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = wave % WPB, role = wave < WPB ? 1 : 2;
+  const int env0 = (blockIdx.x * WPB + grp) * EW;
+  const int rw = c.L.S * EW + c.W.words;  // one wave's region: tile + scratch
+  uint32_t* r0 = lds + nhot + grp * rw;
+  uint32_t* r1 = lds + nhot + (grp + WPB) * rw;
+  uint32_t* ws = (role == 1 ? r0 : r1) + c.L.S * EW;
+  const cxk::Tile<EW> t0{r0, lds, ws}, t1{r1, lds, ws};
+  __syncthreads();
+#ifdef COTIX_PHASE_PROF
+  unsigned long long acc[cxk::PH_COUNT];
+  for (int q = 0; q < cxk::PH_COUNT; ++q) acc[q] = 0ull;
+  const WaveRun run{lane, acc};
+#else
+  const WaveRun run{lane};
+#endif
+  cxk::run_backward_split<EW, NB>(a, c, t0, t1, env0, run, role, [] { lds_barrier(); });
+#ifdef COTIX_PHASE_PROF
+  if (lane == 0 && env0 < a.B)
+    for (int q = 0; q < cxk::PH_COUNT; ++q) atomicAdd(&g_phase_cycles[q], acc[q]);
+#endif
+}
+// the step program with a key-window helper wave per env group
+// (cxk::KeyHelper): waves g < WPB step env group g, wave g + WPB computes its
+// key windows; LDS: the tables, WPB wave regions (tile + scratch, stride rounded
+// to a multiple of EW words), then WPB helper window buffers
+struct GpuKeyHelp {
+  static constexpr bool on = true;
+  int kwalt;
+  __device__ __forceinline__ void bar() const { lds_barrier(); }
+};
+template <int FNSET, int SPEC, bool SDEFER>
+__global__ __launch_bounds__(2 * WPB * 64) void step_help_kernel(cxk::KArgs a) {
+  constexpr int EW = 4;
+  extern __shared__ uint32_t lds[];
+  const SceneDev* sc = a.sc;
+  const cxk::SceneHdr sh = cxk::spec_hdr<SPEC>(a.sh);
+  const int nhot = sh.nhot;
+  constexpr int HC = 8, NT = 2 * WPB * 64;
+  for (int base = 0; base < nhot; base += HC * NT) {
+    uint32_t r[HC];
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      const int i = base + k * NT + (int)threadIdx.x;
+      r[k] = i < nhot ? sc->hot[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      const int i = base + k * NT + (int)threadIdx.x;
+      if (i < nhot) lds[i] = r[k];
+    }
+  }
+  const cxk::Ctx c = cxk::make_ctx<EW>(sh);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = wave % WPB;
+  const bool stepper = wave < WPB;
+  const int env0 = (blockIdx.x * WPB + grp) * EW;
+  const int rw = cxk::help_region_words<EW>(c), hw = cxk::KWIN * c.L.kww * EW;
+  uint32_t* um = lds + nhot + grp * rw;
+  uint32_t* hb = lds + nhot + WPB * rw + grp * hw;
+  const cxk::Tile<EW> tm{um, lds, um + c.L.S * EW};
+  if (stepper && env0 < a.B) cxk::ph_load_fwd<EW, false>(a, c, tm, env0, lane);
+  __syncthreads();
+  const WaveRun run{lane};
+  const int nbar = cxk::keys_on(a) ? cxk::key_helper_windows(a) : 0;
+  if (env0 >= a.B) {  // an idle wave keeps the barrier count
+    for (int q = 0; q < nbar; ++q) lds_barrier();
+    return;
+  }
+  if (stepper) {
+    const GpuKeyHelp help{(int)(hb - um) / EW - c.L.kw};
+    cxk::run_wave<EW, FNSET, false, false, SDEFER>(a, c, tm, env0, run, true, help);
+  } else {
+    cxk::KeyHelper<EW> h;
+    h.tm = tm;
+    h.th = cxk::Tile<EW>{hb - c.L.kw * EW, lds, nullptr};
+    h.env0 = env0;
+    if (nbar > 0) cxk::key_helper_init<EW>(a, c, h, run);
+    for (int q = 0; q < nbar; ++q) {
+      cxk::key_helper_next<EW>(a, c, h, run);
+      lds_barrier();
+    }
+  }
+}
+#endif
+
 }  // namespace
+
+#if COTIX_EW == 4
+// 0: launched; 1: not compiled for this scene / launch (the caller launches step_kernel)
+int cxl::launch_step_help(const cxk::KArgs& ka, int spec, size_t lds, hipStream_t st) {
+  const dim3 grid((ka.B + WPB * 4 - 1) / (WPB * 4)), block(2 * WPB * 64);
+  if (spec == cxk::SPEC_ROBOCUP)
+    hipLaunchKernelGGL((step_help_kernel<FNS_ANALYTIC, cxk::SPEC_ROBOCUP, true>), grid, block, lds, st, ka);
+  else
+    return 1;
+  return 0;
+}
+// 0: launched; 1: not this scene / launch (the caller runs MODE 4)
+int cxl::launch_bwd_split(const cxk::KArgs& ka, int spec, size_t lds, hipStream_t st) {
+  const dim3 grid((ka.B + WPB * 4 - 1) / (WPB * 4)), block(2 * WPB * 64);
+  const int nb = ka.sh.nb;
+#define COTIX_LAUNCH_SPLIT(NB, SP) hipLaunchKernelGGL((bwd_split_kernel<NB, SP>), grid, block, lds, st, ka)
+  // the specializations only: with the header's dimensions as run-time
+  // values the two roles' registers exceed 256 VGPRs and spill (the generic
+  // scenes keep MODE 4)
+  if (spec == cxk::SPEC_ROBOCUP && nb == 5)
+    COTIX_LAUNCH_SPLIT(5, cxk::SPEC_ROBOCUP);
+  else if (spec == cxk::SPEC_BOX && nb == 7)
+    COTIX_LAUNCH_SPLIT(7, cxk::SPEC_BOX);
+  else
+    return 1;
+#undef COTIX_LAUNCH_SPLIT
+  return 0;
+}
+#endif
 
 #define CXL_NAME2(n) launch_step_ew##n
 #define CXL_NAME(n) CXL_NAME2(n)

@@ -7,6 +7,7 @@
 // as collective points.  Used to (a) check the kernel logic against the
 // oracle on CPU and (b) run it under AddressSanitizer/UBSan (GPU sanitizers
 // are unavailable).
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -20,6 +21,8 @@
 
 namespace {
 std::string g_err;
+bool g_split_bwd = false;
+bool g_key_helper = false;
 struct EmuScene {
   cxk::SceneDev s;
   int n_cand = 0, fnset = 0;
@@ -51,6 +54,24 @@ struct HostRun {
   }
 };
 
+// the step wave's side of the key helper on the host: the helper's next
+// window is computed at the step wave's barrier (cxk::KeyHelper)
+template <int EW>
+struct HostKeyHelp {
+  static constexpr bool on = true;
+  int kwalt;
+  cxk::KeyHelper<EW>* h;
+  const cxk::KArgs* a;
+  const cxk::Ctx* c;
+  const HostRun* run;
+  bool* init;
+  void bar() const {
+    if (!*init) cxk::key_helper_init<EW>(*a, *c, *h, *run);
+    *init = true;
+    cxk::key_helper_next<EW>(*a, *c, *h, *run);
+  }
+};
+
 // one wave at a time (waves are independent), through the kernel's own
 // wave programs (cxk::run_wave / run_wave_backward) on 64 fiber lanes
 template <int EW>
@@ -58,17 +79,33 @@ void run_blocks(const cxk::KArgs& a, int mode) {
   const cxk::SceneDev& sc = *a.sc;
   const cxk::Ctx c = cxk::make_ctx<EW>(sc);
   const int nwaves = (a.B + EW - 1) / EW;
-  std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)c.L.S * EW + (size_t)cxk::ws_words(sc, EW));
+  // the wave's tile and scratch (a multiple of EW words), then the split
+  // backward's second tile (mode 5) or the key helper's window buffer (mode 6)
+  const int rw = cxk::help_region_words<EW>(c), x2 = std::max(c.L.S * EW, cxk::KWIN * c.L.kww * EW);
+  std::vector<uint32_t> lds((size_t)sc.nhot + (size_t)rw + (size_t)x2);
   for (int q = 0; q < sc.nhot; ++q) lds[q] = sc.hot[q];
   for (int wv = 0; wv < nwaves; ++wv) {
     std::fill(lds.begin() + sc.nhot, lds.end(), 0x7FBADBADu);  // poison (a NaN pattern)
     const cxk::Tile<EW> t{lds.data() + sc.nhot, lds.data(), lds.data() + sc.nhot + (size_t)c.L.S * EW};
+    uint32_t* const x2b = lds.data() + sc.nhot + rw;
+    const cxk::Tile<EW> t1{x2b, lds.data(), t.ws};
     // the kernel instantiation the library launches (cxk::launch_fnset)
-    const int F = cxk::launch_fnset(sc.fnset, mode);
+    const int F = cxk::launch_fnset(sc.fnset, mode == 5 ? 4 : mode == 6 ? 0 : mode);
     const int env0 = wv * EW;
     cxk_simt::run([&](int lane) {
       const HostRun run{lane};
-      if (mode == 4)
+      if (mode == 6) {  // the step with a key helper: its window computed at the step wave's barrier
+        cxk::KeyHelper<EW> kh;
+        kh.tm = t;
+        kh.th = cxk::Tile<EW>{x2b - c.L.kw * EW, lds.data(), nullptr};
+        kh.env0 = env0;
+        bool init = false;
+        const HostKeyHelp<EW> help{(int)(x2b - t.u) / EW - c.L.kw, &kh, &a, &c, &run, &init};
+        cxk::run_wave<EW, 1, false, false, false>(a, c, t, env0, run, false, help);
+      } else if (mode == 5)  // the split tape backward: each step's producer part, then its consumer's
+        c.nb == 5 ? cxk::run_backward_split<EW, 5>(a, c, t, t1, env0, run, 3, [] {})
+                  : cxk::run_backward_split<EW, 7>(a, c, t, t1, env0, run, 3, [] {});
+      else if (mode == 4)
         F == 1 ? cxk::run_wave_backward_tape<EW, 1>(a, c, t, env0, run)
                : cxk::run_wave_backward_tape<EW, 15>(a, c, t, env0, run);
       else if (mode == 2)
@@ -90,6 +127,10 @@ void run_blocks(const cxk::KArgs& a, int mode) {
   }
 }
 void run_any(const cxk::KArgs& a, int E, int mode) {
+  // the GPU's key helper (cotix_step.hip launch) where it applies and is asked for
+  if (mode == 0 && g_key_helper && E == 4 && a.n_steps > cxk::KWIN &&
+      cxk::launch_fnset(a.sc->fnset, 0) == cxk::FNS_ANALYTIC)
+    mode = 6;
   if (E == 1) run_blocks<1>(a, mode);
   else if (E == 4) run_blocks<4>(a, mode);
   else if (E == 8) run_blocks<8>(a, mode);
@@ -273,7 +314,22 @@ int emu_rollout_backward(void* scene, const float* saved_dyn, const uint32_t* sa
   a.grad_action = grad_action;
   a.grad_dyn = grad_dyn0;
   for (int k = 0; k < s->s.nb * 6; ++k) a.ret_w[k] = ret_w[k];
-  run_any(a, E, tape ? 4 : 2);
+  // the GPU's split backward (cotix_step.hip launch) where it applies and is asked for
+  const bool split = g_split_bwd && tape && E == 4 && cxk::launch_fnset(s->fnset, 4) == cxk::FNS_ANALYTIC &&
+                     cxk::split_bwd_ok<4>(a, cxk::make_ctx<4>(s->s));
+  run_any(a, E, tape ? (split ? 5 : 4) : 2);
+  return 0;
+}
+// 1: the step launches run the step program with the key helper
+// (run_wave + KeyHelper) where the library would; 0 (default): run_wave alone
+int emu_set_key_helper(int on) {
+  g_key_helper = on != 0;
+  return 0;
+}
+// 1: emu_rollout_backward runs the split tape backward (run_backward_split)
+// where the library would; 0 (default): run_wave_backward_tape
+int emu_set_split_bwd(int on) {
+  g_split_bwd = on != 0;
   return 0;
 }
 

@@ -177,6 +177,52 @@ def test_emu_robocup_autoreset_vs_cport(emu_lib):
         assert np.array_equal(g, w)
 
 
+@pytest.mark.parametrize("T", [64, 40, 33])
+def test_emu_key_helper_vs_cport(emu_lib, T):
+    """The step program with the key-window helper (cxk::KeyHelper: windows
+    1.. computed by a helper wave into two alternating buffers, here at the
+    step wave's barrier) on RoboCup with autoreset, actions and the collider
+    trace == the C port -- and == the step without the helper, trace
+    included.  T: 4 whole windows; a partial last window; a last window of one
+    step (the helper's K0-K2 for n = 1 in place of k_one_regs)."""
+    import ctypes
+    emu, lib = emu_lib
+    sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+    from cotix_oracle import cport
+    from cotix_oracle import physics as P
+    _build_cport()
+    clib = cport.load()
+    lib.emu_set_key_helper.argtypes = [ctypes.c_int]
+    B = 12
+    dyn, keys = cport.robocup_batch(B)
+    dyn, keys = np.ascontiguousarray(dyn, np.float32), np.ascontiguousarray(keys, np.uint32)
+    reset = dyn.copy()
+    h, geom = emu.oracle_scene(lib, P.robocup_bodies())
+    sc = cport.Scene(clib, P.robocup_bodies())
+    act = np.ascontiguousarray((np.random.default_rng(T).normal(size=(T, B, 2)) * 0.1).astype(np.float32))
+    runs = []
+    for helper in (1, 0):
+        got = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32), np.zeros(B, np.uint32)]
+        try:
+            lib.emu_set_key_helper(helper)
+            tr = emu.step_ex(lib, h, got[0], got[1], got[2], geom, 0, T, 1 | 4 | 16, 5, E=4, action=act,
+                             action_body=4, dyn_reset=reset, resets=got[3])
+        finally:
+            lib.emu_set_key_helper(0)
+        runs.append((got, tr))
+    want = [dyn.copy(), keys.copy(), np.zeros(B, np.uint32), np.zeros(B, np.uint32)]
+    wch, wcl = sc.step_ex(want[0], want[1], want[2], T, cport.STAGES_ROBOCUP, None, act, 4, reset, want[3],
+                          trace=True)
+    (got, (gch, gcl)), (plain, (pch, pcl)) = runs
+    assert want[3].sum() > 0
+    assert same_f32(got[0], want[0])
+    for g, w in zip(got[1:], want[1:]):
+        assert np.array_equal(g, w)
+    assert np.array_equal(gch, wch) and np.array_equal(gcl, wcl)
+    assert np.array_equal(got[0].view(np.uint32), plain[0].view(np.uint32))
+    assert np.array_equal(gch, pch) and np.array_equal(gcl, pcl)
+
+
 @pytest.mark.parametrize("EW", [2, 4, 8])
 def test_emu_trace_actions_autoreset_vs_cport(emu_lib, EW):
     """cotix_step_ex on CPU: actions + episode restarts + the collider trace

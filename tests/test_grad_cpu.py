@@ -329,6 +329,38 @@ def test_g_regs_equals_tile_form(emu_lib):
             assert np.array_equal(x[~nx].view(np.uint32), y[~ny].view(np.uint32))
 
 
+@pytest.mark.parametrize("scene", ["box", "robocup"])
+def test_split_backward_equals_tape_backward(emu_lib, scene):
+    """The split tape backward (cxk::run_backward_split: a producer wave's
+    restore / Euler / world parts / phase D of step s into one of two tiles
+    while a consumer wave reverses step s + 1 on the other, adjoints in the
+    consumer's registers) run on the emulation as producer-then-consumer per
+    step: bit for bit the one-wave tape backward (MODE 4), NaN patterns
+    included -- odd and even horizons (the two tiles' alternation), a batch
+    whose last wave is partly idle."""
+    import ctypes
+    emu, lib = emu_lib
+    lib.emu_set_split_bwd.argtypes = [ctypes.c_int]
+    for T, B in ((7, 8), (8, 12)):
+        case = GC.box_case(B, T, seed=5) if scene == "box" else GC.robocup_case(B, T, seed=2)
+        h, geom = emu.oracle_scene(lib, case["make"]())
+        dyn = np.ascontiguousarray(case["S0"].transpose(1, 2, 0))
+        keys = np.array(case["keys"], np.uint32, copy=True)
+        err = np.zeros(dyn.shape[2], np.uint32)
+        _, sd, sk, tape = emu.rollout(lib, h, dyn, keys, err, geom, 0, 1 | 4 | 16, case["actions"], case["ab"],
+                                      case["w"], E=4)
+        args = (geom, 0, 1 | 4 | 16, case["actions"], case["ab"], case["w"])
+        try:
+            lib.emu_set_split_bwd(1)
+            sa, sg = emu.rollout_backward(lib, h, sd, sk, *args, E=4, tape=tape)
+        finally:
+            lib.emu_set_split_bwd(0)
+        ta, tg = emu.rollout_backward(lib, h, sd, sk, *args, E=4, tape=tape)
+        assert np.array_equal(sa.view(np.uint32), ta.view(np.uint32)), (scene, T, "grad_action")
+        assert np.array_equal(sg.view(np.uint32), tg.view(np.uint32)), (scene, T, "grad_dyn0")
+        assert np.isfinite(sa).any()
+
+
 def test_circle_poly_recorded_forward_is_the_forward(emu_lib):
     """The circle x polygon gradient re-runs GJK + EPA while recording every
     Minkowski point (cx::cp_forward): its final edge gives the forward

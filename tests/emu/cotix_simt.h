@@ -104,8 +104,11 @@ struct Wave {
 #endif
 };
 
-inline thread_local Wave* g_wave = nullptr;
-inline thread_local char* g_stacks = nullptr;  // NL stacks, mapped once per thread (never unmapped)
+// static, not inline: an inline variable is a GNU_UNIQUE symbol, bound once per
+// process across every emulation build a test loads (plain, ASan with 4 MiB
+// stacks, mutation builds) -- one build's stride over another's mapping.
+static thread_local Wave* g_wave = nullptr;
+static thread_local char* g_stacks = nullptr;  // NL stacks, mapped once per thread (never unmapped)
 
 [[noreturn]] inline void fail(const char* what, int lane) {
   std::fprintf(stderr, "cotix_simt: %s (lane %d)\n", what, lane);

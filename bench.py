@@ -92,8 +92,8 @@ def parse():
                     help="step launches of more than 16 steps with the key-window helper wave (the library "
                          "default, 1) or the step wave alone (0); recorded in config")
     ap.add_argument("--split-bwd", type=int, default=1, choices=[0, 1],
-                    help="--mode grad: the tape backward at two waves per env group (the library default, 1) "
-                         "or one (0); recorded in config")
+                    help="--mode grad: the RoboCup tape backward at two waves per env group (the library default, 1) "
+                         "or one (0; other scenes always run one, DESIGN section 3); recorded in config")
     a = ap.parse_args()
     refuse_overrides()
     # the two-wave forms' library switches (read at the first launch)
@@ -112,7 +112,7 @@ BENCH_ENV_OK = {"COTIX_BENCH_FORCE_DIST"}
 def two_wave_forms():
     """The two-wave kernel forms this run allowed (--key-helper, --split-bwd):
     the key-window helper wave of step launches with more than one key
-    window, the split tape backward of the analytic scenes."""
+    window, the split tape backward (RoboCup; other scenes run MODE 4)."""
     return {"key_helper": int(os.environ.get("COTIX_KEY_HELPER", "1")),
             "split_bwd": int(os.environ.get("COTIX_SPLIT_BWD", "1"))}
 

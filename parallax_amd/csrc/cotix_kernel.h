@@ -3632,7 +3632,10 @@ CX_DEV void ph_GE(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int lane) 
 // g_chain: the step's reverse on the adjoints g held by the caller (g_regs
 // reads them from and writes them to the tile's adj words; the split backward's
 // consumer wave carries them in registers from step to step)
-template <int EW, int NB>
+// TILE: the adjoints are read from and written to the tile's adj words inside
+// the chain's own loops (g_regs: the one-wave form's schedule, the adjoints
+// live only across one step); otherwise the caller's registers carry them
+template <int EW, int NB, bool TILE = false>
 CX_DEV void g_chain(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step, float (&g)[NB][6],
                     GradOut* go = nullptr) {
   using namespace cx;
@@ -3642,6 +3645,9 @@ CX_DEV void g_chain(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, i
   uint32_t fl[NB], jj[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
+    if (TILE)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g[b][k] = t.f(L.adj + 6 * b + k, e);
     px[b] = t.f(L.dyn + 6 * b, e);
     py[b] = t.f(L.dyn + 6 * b + 1, e);
     an[b] = t.f(L.dyn + 6 * b + 4, e);
@@ -3733,20 +3739,15 @@ CX_DEV void g_chain(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, i
     if (step > 0)
 #pragma unroll
       for (int k = 0; k < 6; ++k) g[b][k] = g[b][k] + t.f(L.rst + 6 * b + k, e);  // ret_w (staged)
+    if (TILE)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) t.f(L.adj + 6 * b + k, e) = g[b][k];
   }
 }
 template <int EW, int NB>
 CX_DEV void g_regs(const KArgs& a, const Ctx& c, Tile<EW> t, int env0, int e, int step, GradOut* go = nullptr) {
   float g[NB][6];
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) g[b][k] = t.f(c.L.adj + 6 * b + k, e);
-  g_chain<EW, NB>(a, c, t, env0, e, step, g, go);
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) t.f(c.L.adj + 6 * b + k, e) = g[b][k];
+  g_chain<EW, NB, true>(a, c, t, env0, e, step, g, go);
 }
 
 template <int EW, int FNSET = FNS_ANALYTIC>

@@ -241,6 +241,7 @@ def valu_roofline(scenario, B, substeps, launch_ms, warmup=None, layout="legacy"
                 "valu_active_frac_of_wave_cycles": pmc["valu_active_frac_of_wave_cycles"],
                 "wait_frac_of_wave_cycles": pmc.get("wait_frac_of_wave_cycles"),
                 "stall": pmc.get("stall"),
+                "kernel": pmc.get("kernel"),
                 "pmc_avg_launch_ms": pmc["avg_launch_ns"] * 1e-6}
     except (OSError, KeyError, ValueError):
         return None
@@ -274,6 +275,8 @@ def roofline(scenario, B, substeps, launch_ms, nb, layout="legacy"):
                    traffic_source=v["source"], valu_active_frac_of_wave_cycles=v["valu_active_frac_of_wave_cycles"],
                    wait_frac_of_wave_cycles=v["wait_frac_of_wave_cycles"], stall=v["stall"],
                    pmc_avg_launch_ms=v["pmc_avg_launch_ms"])
+        if v.get("kernel"):  # the profiled kernel's full name (the RoboCup step: step_help_kernel)
+            out["kernel"] = v["kernel"]
     return out
 
 

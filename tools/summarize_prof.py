@@ -16,6 +16,14 @@ scen = sys.argv[2] if len(sys.argv) > 2 else "robocup"
 src = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/prof_%s" % scen
 out = "profiles"
 K = "step_kernel"
+# the fused step program's kernels: step_kernel, and the RoboCup step with its
+# key-window helper wave (step_help_kernel); the config-5 backward may be the
+# split tape backward (bwd_split_kernel)
+STEP_KERNELS = ("step_kernel", "step_help_kernel")
+
+
+def is_step(name):
+    return any(k in name for k in STEP_KERNELS)
 
 
 def last_dispatches(rows, n):
@@ -44,7 +52,7 @@ def have(d):
 
 
 def pmc(d, n=None):
-    rows = [r for r in csv.DictReader(open(os.path.join(src, d, "run_counter_collection.csv"))) if K in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(os.path.join(src, d, "run_counter_collection.csv"))) if is_step(r["Kernel_Name"])]
     if n:
         rows = last_dispatches(rows, n)
     agg = defaultdict(list)
@@ -72,10 +80,12 @@ if scen.startswith("grad"):
         m = re.search(r"step_kernel<\d+, \d+, (\d+)", name)
         return int(m.group(1)) if m else -1
 
-    # the backward: MODE 4 (from the forward's tape), else the re-play (MODE 2)
+    # the backward: the split tape backward, else MODE 4 (from the forward's
+    # tape), else the re-play (MODE 2)
+    split = [r for r in stats if "bwd_split_kernel" in r["Name"]]
     bmode = 4 if any(K in r["Name"] and mode_of(r["Name"]) == 4 for r in stats) else 2
     for part, mode in (("fwd", 1), ("bwd", bmode)):
-        row = [r for r in stats if K in r["Name"] and mode_of(r["Name"]) == mode][0]
+        row = split[0] if part == "bwd" and split else [r for r in stats if K in r["Name"] and mode_of(r["Name"]) == mode][0]
         c = {}
         for d in ("pmc_fetch", "pmc_write", "pmc_sq"):
             c.update(pmc_k(d, row["Name"]))
@@ -98,11 +108,11 @@ if scen.startswith("grad"):
     sys.exit(0)
 
 stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
-row = [r for r in stats if K in r["Name"]][0]
+row = [r for r in stats if is_step(r["Name"])][0]
 bench = json.load(open(os.path.join(src, "trace_bench.json")))
 nt = int(bench["steps"])  # the timed launches
 trows = last_dispatches([r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
-                         if K in r["Kernel_Name"]], nt)
+                         if is_step(r["Kernel_Name"])], nt)
 avg_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trows) / len(trows)
 c = {}
 for d in ("pmc_fetch", "pmc_write", "pmc_sq"):

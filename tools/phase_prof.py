@@ -41,6 +41,12 @@ def main():
     if a.build:
         return build()
     os.environ["COTIX_AMD_LIB"] = os.path.abspath(a.lib)
+    # the one-wave kernels only: the phase-profiling build of step_help_kernel
+    # (build 0ac7b676) constructs its WaveRun without the cycle accumulators,
+    # so its phases write through a null pointer (a GPU memory fault on the
+    # r06z box); the per-phase cycles are the step wave's program either way
+    os.environ["COTIX_KEY_HELPER"] = "0"
+    os.environ["COTIX_SPLIT_BWD"] = "0"
     sys.path.insert(0, ROOT)
     import torch
     import parallax_amd as pa
